@@ -1,0 +1,147 @@
+/*
+ * spwgnn.h — C-ABI of libspwgnn_hip.so, the MI355X (gfx950) propagation-network engine.
+ *
+ * The reference (irmakguzey/SPWGNN) has no FFI: its hot path is a Keras graph built by
+ * PropagationNetwork.getModel (src/Networks.py:106-194) over MLP blocks (src/Blocks.py:12-91),
+ * driven by model.fit (src/main.py:92-98) and model.predict (src/JengaBuilder.py:328-329,
+ * src/TowerCreator.py:430-431). Each entry point below replaces one piece of that graph; the
+ * cited lines say which. Everything is plain C: raw pointers, sizes, an int status. All device
+ * memory is caller-owned; the library never allocates and never synchronises, so every
+ * launch function is hipGraph-capturable on the caller's stream.
+ *
+ * Status codes: 0 = ok, SPWGNN_E_* below, or a positive hipError_t from a failed launch.
+ */
+#ifndef SPWGNN_H
+#define SPWGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPWGNN_ABI_VERSION 1
+
+#define SPWGNN_OK 0
+#define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
+#define SPWGNN_E_SHAPE (-2)         /* shape outside what the kernels support                 */
+#define SPWGNN_E_RELATION (-3)      /* relation matrix column is not one-hot / both-or-neither */
+#define SPWGNN_E_WORKSPACE (-4)     /* workspace smaller than spwgnn_workspace_bytes()        */
+#define SPWGNN_E_CAPACITY (-5)      /* caller-provided output array too small                 */
+#define SPWGNN_E_NOTRAIN (-6)       /* backward on a workspace run with training == 0         */
+
+typedef void* spwgnn_stream_t;      /* a hipStream_t (NULL = default stream) */
+
+/* ---------------------------------------------------------------- parameters ------------ */
+/* The 22 Keras weight tensors of rm, om, rmp, omp (Networks.py:136-140, Blocks.py:20-28/60-68)
+ * live in ONE flat fp32 buffer, Keras layout (kernel = [in][out] row-major, bias = [out]),
+ * each tensor starting on a 64-float boundary. 209,501 real parameters. */
+typedef struct spwgnn_param_info {
+    const char* name;   /* e.g. "rmp.0.kernel" */
+    int64_t offset;     /* in floats from the start of the flat buffer */
+    int32_t rows;       /* kernel: in-features; bias: 1 */
+    int32_t cols;       /* out-features */
+} spwgnn_param_info;
+
+int32_t spwgnn_version(void);
+const char* spwgnn_strerror(int32_t status);
+int32_t spwgnn_param_tensor_count(void);
+int64_t spwgnn_param_count(void);                 /* padded flat length (floats)       */
+int64_t spwgnn_param_real_count(void);            /* 209,501                           */
+int32_t spwgnn_param_tensor(int32_t index, spwgnn_param_info* out);
+
+/* ------------------------------------------------------------- host-side input builders -- */
+/* Dense relation matrices → compact edge list. Replaces the one-hot batch_dot gathers of
+ * Networks.py:117-123/:174-175 and the segment-sum of :178 at the input boundary: a column k
+ * of (Rs, Rr) that is one-hot in both is edge k (sender, receiver); an all-zero column is an
+ * inactive relation (it never reaches an output, Networks.py:178); a column one-hot in Rs only
+ * also never reaches an output and is dropped; anything else → SPWGNN_E_RELATION.
+ * Rs, Rr: host fp32 [B][N][E], E = N(N-1). Output edges are tower-major, slot order (the
+ * sender-major enumeration of main.py:72-81). src/dst are GLOBAL node ids (b*N + local). */
+int32_t spwgnn_dense_to_edges(const float* Rs, const float* Rr, int32_t B, int32_t N,
+                              int32_t* src, int32_t* dst, int32_t* slot, int64_t capacity,
+                              int64_t* n_edges, int32_t* tower_edge_count);
+
+/* Work plan for the edge kernels: towers are packed into wave-tiles of whole towers with at
+ * most nw_max nodes; each wave-tile's edges are cut into 32-edge blocks (last one padded with
+ * -1). blk_csr holds, per block, the block's edge slots sorted by local receiver and by local
+ * sender (deterministic segment sums). Two phases: sizes, then fill. Host memory. */
+typedef struct spwgnn_plan_sizes {
+    int32_t n_wtiles;
+    int32_t n_eblocks;
+    int32_t nw_max;     /* max nodes in any wave-tile (<= requested nw_max) */
+} spwgnn_plan_sizes;
+
+int32_t spwgnn_plan_size(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                         int32_t nw_max, spwgnn_plan_sizes* out);
+int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                         const int32_t* src, const int32_t* dst, int32_t nw_max,
+                         const spwgnn_plan_sizes* sizes, int32_t* wtile /* [n_wtiles][4] */,
+                         int32_t* edge_src /* [n_eblocks*32] */, int32_t* edge_dst,
+                         int32_t* edge_id /* [n_eblocks*32] original edge index or -1 */,
+                         uint8_t* blk_csr /* [n_eblocks][128] */);
+
+/* ------------------------------------------------------------------- device batch ------- */
+typedef struct spwgnn_batch {
+    int32_t n_towers;
+    int32_t n_nodes;        /* Σ N over towers */
+    int32_t n_wtiles;
+    int32_t n_eblocks;
+    int32_t nw_max;
+    int32_t pad0;
+    const float* pos;           /* [n_nodes][4]: objects (x, y, w)/170 + 0 pad (Networks.py:112)   */
+    const float* prop;          /* [n_nodes][100] 'propagation' input (Networks.py:119); NULL = 0  */
+    const int32_t* node_tower;  /* [n_nodes] tower id (dropout key)                                */
+    const int32_t* node_local; /* [n_nodes] node index inside its tower (dropout key)             */
+    const int32_t* wtile;       /* [n_wtiles][4] first block, #blocks, first node, #nodes         */
+    const int32_t* edge_src;    /* [n_eblocks*32] global sender, -1 = padding                     */
+    const int32_t* edge_dst;    /* [n_eblocks*32] global receiver, -1 = padding                   */
+    const uint8_t* blk_csr;     /* [n_eblocks][128]                                                */
+} spwgnn_batch;
+
+typedef struct spwgnn_run {
+    int32_t mp_steps;   /* propagation steps; the reference hard-codes 5 (Networks.py:173)      */
+    int32_t training;   /* 1: keep activations for backward + apply dropout                      */
+    float dropout;      /* Dropout rate on the two encodings (Networks.py:167-168); 0 = off      */
+    int32_t pad0;
+    uint64_t seed;      /* dropout mask key                                                       */
+} spwgnn_run;
+
+/* Workspace bytes for (n_nodes, n_eblocks, mp_steps, training). */
+int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training);
+
+/* Forward: the whole graph of Networks.py:121-186 → per-node logits z (the model output is
+ * sigmoid(z), Networks.py:184). logits: [n_nodes] device fp32. */
+int32_t spwgnn_forward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run,
+                       void* workspace, int64_t workspace_bytes, float* logits,
+                       spwgnn_stream_t stream);
+
+/* Backward of the last spwgnn_forward on the same workspace (training == 1): dlogits [n_nodes]
+ * → grads (flat, same layout as params; overwritten) and, if dprop != NULL, d/d propagation
+ * [n_nodes][100]. Replaces TF autodiff of the graph (Networks.py:192 compile → fit). */
+int32_t spwgnn_backward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run,
+                        void* workspace, int64_t workspace_bytes, const float* dlogits,
+                        float* grads, float* dprop, spwgnn_stream_t stream);
+
+/* Keras binary_crossentropy on sigmoid(logits) (Networks.py:192), mean over n:
+ * out3 = {loss, sum of correct (binary_accuracy numerator), n}; dlogits = dloss/dlogit.
+ * scratch: >= spwgnn_bce_scratch_bytes(n) device bytes. Deterministic. */
+int64_t spwgnn_bce_scratch_bytes(int64_t n);
+int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* out3,
+                   float* dlogits, void* scratch, spwgnn_stream_t stream);
+
+/* Keras-2.x Adam (Networks.py:191: lr=5e-4, decay=0): in-place on the flat buffer.
+ * g' = grad_scale*grad + 2*l2*param; lr_t = lr*sqrt(1-b2^t)/(1-b1^t);
+ * m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2; p -= lr_t m/(sqrt(v)+eps). step = t >= 1. */
+int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64_t n, int32_t step,
+                    float lr, float beta1, float beta2, float eps, float l2, float grad_scale,
+                    spwgnn_stream_t stream);
+
+/* Sigmoid readout (Networks.py:183-186) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
+int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPWGNN_H */

@@ -1,0 +1,95 @@
+"""ctypes binding of libspwgnn_hip.so (the C-ABI in include/spwgnn.h).
+
+The product path has no fallback: if the library is missing or cannot be loaded, every entry
+point raises. Device pointers are passed as plain integers (torch ``data_ptr()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+from typing import Optional
+
+_LIB_PATH = Path(__file__).resolve().parent / "libspwgnn_hip.so"
+_lib: Optional[C.CDLL] = None
+
+
+class SpwgnnError(RuntimeError):
+    pass
+
+
+class ParamInfo(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("offset", C.c_int64), ("rows", C.c_int32), ("cols", C.c_int32)]
+
+
+class PlanSizes(C.Structure):
+    _fields_ = [("n_wtiles", C.c_int32), ("n_eblocks", C.c_int32), ("nw_max", C.c_int32)]
+
+
+class BatchC(C.Structure):
+    _fields_ = [
+        ("n_towers", C.c_int32), ("n_nodes", C.c_int32), ("n_wtiles", C.c_int32), ("n_eblocks", C.c_int32),
+        ("nw_max", C.c_int32), ("pad0", C.c_int32),
+        ("pos", C.c_void_p), ("prop", C.c_void_p), ("node_tower", C.c_void_p), ("node_local", C.c_void_p),
+        ("wtile", C.c_void_p), ("edge_src", C.c_void_p), ("edge_dst", C.c_void_p), ("blk_csr", C.c_void_p),
+    ]
+
+
+class RunC(C.Structure):
+    _fields_ = [("mp_steps", C.c_int32), ("training", C.c_int32), ("dropout", C.c_float), ("pad0", C.c_int32),
+                ("seed", C.c_uint64)]
+
+
+def _declare(lib: C.CDLL) -> None:
+    i32, i64, vp, f32 = C.c_int32, C.c_int64, C.c_void_p, C.c_float
+    sig = {
+        "spwgnn_version": (i32, []),
+        "spwgnn_strerror": (C.c_char_p, [i32]),
+        "spwgnn_param_tensor_count": (i32, []),
+        "spwgnn_param_count": (i64, []),
+        "spwgnn_param_real_count": (i64, []),
+        "spwgnn_param_tensor": (i32, [i32, C.POINTER(ParamInfo)]),
+        "spwgnn_dense_to_edges": (i32, [vp, vp, i32, i32, vp, vp, vp, i64, C.POINTER(i64), vp]),
+        "spwgnn_plan_size": (i32, [i32, vp, vp, i32, C.POINTER(PlanSizes)]),
+        "spwgnn_plan_fill": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
+        "spwgnn_workspace_bytes": (i64, [i32, i32, i32, i32]),
+        "spwgnn_forward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp]),
+        "spwgnn_backward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp, vp, vp]),
+        "spwgnn_bce_scratch_bytes": (i64, [i64]),
+        "spwgnn_bce": (i32, [vp, vp, i64, vp, vp, vp, vp]),
+        "spwgnn_adam": (i32, [vp, vp, vp, vp, i64, i32, f32, f32, f32, f32, f32, f32, vp]),
+        "spwgnn_sigmoid": (i32, [vp, vp, i64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib() -> C.CDLL:
+    """Load (once) the in-tree HIP library. Raises if it is absent: there is no fallback."""
+    global _lib
+    if _lib is None:
+        path = Path(os.environ.get("SPWGNN_LIB", _LIB_PATH))
+        if not path.exists():
+            raise SpwgnnError(f"{path} not found — build it with `python -m spwgnn_amd.build` "
+                              "(the HIP path has no CPU fallback)")
+        _lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+        _declare(_lib)
+    return _lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib().spwgnn_strerror(status).decode()
+        raise SpwgnnError(f"{what}: {msg} (status {status})")
+
+
+def param_tensors():
+    L = lib()
+    out = []
+    info = ParamInfo()
+    for i in range(L.spwgnn_param_tensor_count()):
+        check(L.spwgnn_param_tensor(i, C.byref(info)), "param_tensor")
+        out.append((info.name.decode(), int(info.offset), int(info.rows), int(info.cols)))
+    return out

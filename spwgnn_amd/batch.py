@@ -1,0 +1,196 @@
+"""TowerBatch: the reference's 4-tensor input dict, compacted for the HIP kernels.
+
+The reference feeds Keras (B, N, 3) objects, two dense (B, N, E) one-hot relation matrices and a
+(B, N, 100) propagation state (src/Networks.py:112-119; built by src/main.py:66-93). Every active
+relation column is one sender and one receiver, so the batch becomes a union graph: node rows
+(objects, propagation) and an edge list, packed by the C library into wave-tiles of whole towers
+and 32-edge blocks (spwgnn_plan_size/fill). Conversion happens once per batch on the host (C++);
+the device arrays then stay resident in HBM.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def default_nw_max(max_nodes: int) -> int:
+    """Nodes per wave-tile: at least one whole tower, at least ~10 nodes so small towers share a
+    wave (bounded by the LDS node accumulators)."""
+    return int(min(_NW_LIMIT, max(max_nodes, 10)))
+
+
+_NW_LIMIT = 32
+
+
+@dataclass
+class TowerBatch:
+    n_towers: int
+    n_nodes: int
+    tower_nodes: np.ndarray          # (T,) int32
+    tower_edges: np.ndarray          # (T,) int32 active relations per tower
+    src: np.ndarray                  # (Ne,) int32 global sender (host copy)
+    dst: np.ndarray                  # (Ne,) int32 global receiver
+    n_wtiles: int
+    n_eblocks: int
+    nw_max: int
+    device: torch.device
+    pos: torch.Tensor                # (Nn, 4) f32
+    prop: Optional[torch.Tensor]     # (Nn, 100) f32 or None (= zeros)
+    node_tower: torch.Tensor
+    node_local: torch.Tensor
+    wtile: torch.Tensor
+    edge_src: torch.Tensor
+    edge_dst: torch.Tensor
+    blk_csr: torch.Tensor
+    edge_id: np.ndarray              # (n_eblocks*32,) original edge index or -1
+    node_shape: Optional[tuple] = None   # (B, N) when built from a uniform-N dense batch
+    _cstruct: Optional[_lib.BatchC] = field(default=None, repr=False)
+
+    @property
+    def n_edges(self) -> int:
+        return int(len(self.src))
+
+    # ------------------------------------------------------------------ constructors
+    @staticmethod
+    def from_edges(pos: np.ndarray, tower_nodes, src, dst, tower_edges, prop=None, device="cuda",
+                   nw_max: Optional[int] = None, node_shape=None) -> "TowerBatch":
+        """pos (Nn, >=3) objects rows (already /170); towers are consecutive node ranges;
+        edges tower-major with global node ids."""
+        L = _lib.lib()
+        tower_nodes = np.ascontiguousarray(tower_nodes, dtype=np.int32)
+        tower_edges = np.ascontiguousarray(tower_edges, dtype=np.int32)
+        src = np.ascontiguousarray(src, dtype=np.int32)
+        dst = np.ascontiguousarray(dst, dtype=np.int32)
+        T = len(tower_nodes)
+        Nn = int(tower_nodes.sum())
+        if pos.shape[0] != Nn:
+            raise ValueError(f"pos has {pos.shape[0]} rows, towers hold {Nn} nodes")
+        if int(tower_edges.sum()) != len(src) or len(src) != len(dst):
+            raise ValueError("edge counts do not match the edge list")
+        if nw_max is None:
+            nw_max = default_nw_max(int(tower_nodes.max()) if T else 1)
+        if T and int(tower_nodes.max()) > _NW_LIMIT:
+            raise ValueError(f"towers of more than {_NW_LIMIT} nodes are not supported by this build")
+        sizes = _lib.PlanSizes()
+        _lib.check(L.spwgnn_plan_size(T, _ptr(tower_nodes), _ptr(tower_edges), nw_max, C.byref(sizes)), "plan_size")
+        wtile = np.zeros((sizes.n_wtiles, 4), np.int32)
+        esrc = np.zeros(sizes.n_eblocks * 32, np.int32)
+        edst = np.zeros(sizes.n_eblocks * 32, np.int32)
+        eid = np.zeros(sizes.n_eblocks * 32, np.int32)
+        csr = np.zeros((sizes.n_eblocks, 128), np.uint8)
+        _lib.check(L.spwgnn_plan_fill(T, _ptr(tower_nodes), _ptr(tower_edges), _ptr(src) if len(src) else None,
+                                      _ptr(dst) if len(dst) else None, nw_max, C.byref(sizes), _ptr(wtile),
+                                      _ptr(esrc), _ptr(edst), _ptr(eid), _ptr(csr)), "plan_fill")
+        node_tower = np.repeat(np.arange(T, dtype=np.int32), tower_nodes)
+        starts = np.concatenate([[0], np.cumsum(tower_nodes)[:-1]]).astype(np.int64)
+        node_local = (np.arange(Nn) - np.repeat(starts, tower_nodes)).astype(np.int32)
+        pos4 = np.zeros((Nn, 4), np.float32)
+        pos4[:, :3] = np.asarray(pos, np.float32)[:, :3]
+        dev = torch.device(device)
+        tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        prop_t = None
+        if prop is not None:
+            prop_t = torch.as_tensor(np.asarray(prop, np.float32).reshape(Nn, 100)).to(dev).contiguous()
+        return TowerBatch(T, Nn, tower_nodes, tower_edges, src, dst, sizes.n_wtiles, sizes.n_eblocks,
+                          sizes.nw_max, dev, tt(pos4), prop_t, tt(node_tower), tt(node_local), tt(wtile),
+                          tt(esrc), tt(edst), tt(csr), eid, node_shape)
+
+    @staticmethod
+    def from_dense(objects, sender_relations, receiver_relations, propagation=None, device="cuda",
+                   nw_max: Optional[int] = None) -> "TowerBatch":
+        """The reference input dict (Networks.py:112-119) → compact batch (C++ conversion)."""
+        to_np = lambda x: x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+        obj = np.ascontiguousarray(to_np(objects), np.float32)
+        Rs = np.ascontiguousarray(to_np(sender_relations), np.float32)
+        Rr = np.ascontiguousarray(to_np(receiver_relations), np.float32)
+        B, N = obj.shape[:2]
+        E = N * (N - 1)
+        if Rs.shape != (B, N, E) or Rr.shape != (B, N, E):
+            raise ValueError(f"relation matrices must be (B, N, N(N-1)) = {(B, N, E)}; got {Rs.shape}, {Rr.shape}")
+        L = _lib.lib()
+        cap = B * E
+        src = np.zeros(max(cap, 1), np.int32)
+        dst = np.zeros(max(cap, 1), np.int32)
+        tec = np.zeros(B, np.int32)
+        ne = C.c_int64(0)
+        _lib.check(L.spwgnn_dense_to_edges(_ptr(Rs), _ptr(Rr), B, N, _ptr(src), _ptr(dst), None, cap, C.byref(ne),
+                                           _ptr(tec)), "dense_to_edges")
+        n = int(ne.value)
+        prop = None
+        if propagation is not None:
+            p = to_np(propagation)
+            if np.any(p != 0):
+                prop = np.asarray(p, np.float32).reshape(B * N, 100)
+        return TowerBatch.from_edges(obj.reshape(B * N, 3), np.full(B, N, np.int32), src[:n], dst[:n], tec, prop,
+                                     device, nw_max, node_shape=(B, N))
+
+    @staticmethod
+    def fully_connected(objects: np.ndarray, propagation=None, device="cuda", nw_max=None) -> "TowerBatch":
+        """Fast path for (B, N, 3) towers whose relations are all active (the inference relation
+        set of JengaBuilder.py:309-326 and the benchmark configs)."""
+        obj = np.asarray(objects, np.float32)
+        B, N = obj.shape[:2]
+        m_idx, j_idx = np.nonzero(~np.eye(N, dtype=bool))
+        base = (np.arange(B, dtype=np.int64) * N)[:, None]
+        src = (base + m_idx[None, :]).reshape(-1).astype(np.int32)
+        dst = (base + j_idx[None, :]).reshape(-1).astype(np.int32)
+        prop = None if propagation is None else np.asarray(propagation, np.float32).reshape(B * N, 100)
+        return TowerBatch.from_edges(obj.reshape(B * N, 3), np.full(B, N, np.int32), src, dst,
+                                     np.full(B, N * (N - 1), np.int32), prop, device, nw_max, node_shape=(B, N))
+
+    @staticmethod
+    def ragged(objects_list, relation_threshold: Optional[float] = None, device="cuda", nw_max=None,
+               raw_positions_list=None) -> "TowerBatch":
+        """Towers of different sizes: list of (N_b, 3) objects; relations fully connected, or
+        thresholded on ``raw_positions_list`` (pixels) like main.py:71-81."""
+        tower_nodes = np.array([len(o) for o in objects_list], np.int32)
+        srcs, dsts, tes = [], [], []
+        off = 0
+        for b, o in enumerate(objects_list):
+            N = len(o)
+            m_idx, j_idx = np.nonzero(~np.eye(N, dtype=bool))
+            if relation_threshold is not None:
+                raw = np.asarray(raw_positions_list[b])
+                keep = np.linalg.norm(raw[m_idx, 0:2] - raw[j_idx, 0:2], axis=1) < relation_threshold
+                m_idx, j_idx = m_idx[keep], j_idx[keep]
+            srcs.append(off + m_idx)
+            dsts.append(off + j_idx)
+            tes.append(len(m_idx))
+            off += N
+        src = np.concatenate(srcs).astype(np.int32) if srcs else np.zeros(0, np.int32)
+        dst = np.concatenate(dsts).astype(np.int32) if dsts else np.zeros(0, np.int32)
+        pos = np.concatenate([np.asarray(o, np.float32) for o in objects_list], axis=0)
+        return TowerBatch.from_edges(pos, tower_nodes, src, dst, np.array(tes, np.int32), None, device, nw_max)
+
+    # ------------------------------------------------------------------ C view
+    def cstruct(self) -> _lib.BatchC:
+        if self._cstruct is None:
+            b = _lib.BatchC()
+            b.n_towers, b.n_nodes = self.n_towers, self.n_nodes
+            b.n_wtiles, b.n_eblocks, b.nw_max = self.n_wtiles, self.n_eblocks, self.nw_max
+            b.pos = self.pos.data_ptr()
+            b.prop = self.prop.data_ptr() if self.prop is not None else None
+            b.node_tower = self.node_tower.data_ptr()
+            b.node_local = self.node_local.data_ptr()
+            b.wtile = self.wtile.data_ptr()
+            b.edge_src = self.edge_src.data_ptr()
+            b.edge_dst = self.edge_dst.data_ptr()
+            b.blk_csr = self.blk_csr.data_ptr()
+            self._cstruct = b
+        return self._cstruct
+
+    def with_prop(self, prop: Optional[torch.Tensor]) -> "TowerBatch":
+        """Same graph, different propagation input (device tensor (Nn, 100) or None)."""
+        nb = TowerBatch(**{k: getattr(self, k) for k in self.__dataclass_fields__ if k != "_cstruct"})
+        nb.prop = None if prop is None else prop.reshape(self.n_nodes, 100).to(self.device, torch.float32).contiguous()
+        return nb

@@ -1,0 +1,638 @@
+// C-ABI entry points of libspwgnn_hip.so: workspace layout and launch sequences.
+#include <cmath>
+#include <cstring>
+#include "kernels.h"
+#include "../../include/spwgnn.h"
+
+namespace spw {
+
+static inline int64_t up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------- workspace layout -----------
+struct Ws {
+    int64_t total = 0;  // bytes
+    int S, training;
+    int64_t RN, RE, NB;
+    // floats offsets (bytes / 4) — every array starts on 256 bytes
+    int64_t pk;
+    int64_t zo1, co, P, a, o1, U, V, H2s;           // node
+    int64_t A, z1, z2, z3, cr;                       // edge
+    int64_t mask1, mask2;                            // u32
+    int64_t dx, do1, g, G3, dU, dV, dP, dco, dzo2, dzo1;   // node (bwd)
+    int64_t dA, dz4, dz3, dz2, dz1;                  // edge (bwd)
+    int64_t slab, bce;
+    int64_t slab_floats;
+    PackSlots ps;
+    int sP() const { return training ? S + 1 : 2; }
+    int sStep() const { return training ? S : 1; }
+    int64_t P_at(int s) const { return P + (int64_t)(training ? s : (s & 1)) * RN * kLdN; }
+    int64_t U_at(int s) const { return U + (int64_t)(training ? s : 0) * RN * kLdE; }
+    int64_t V_at(int s) const { return V + (int64_t)(training ? s : 0) * RN * kLdE; }
+    int64_t H2s_at(int s) const { return H2s + (int64_t)(training ? s : 0) * RN * kLdE; }
+    int64_t a_at(int s) const { return a + (int64_t)s * RN * kLdN; }
+    int64_t o1_at(int s) const { return o1 + (int64_t)s * RN * kLdN; }
+    int64_t m1_at(int s) const { return mask1 + (int64_t)s * NB * kLdE; }
+    int64_t m2_at(int s) const { return mask2 + (int64_t)s * NB * 160; }
+    int64_t dx_at(int s) const { return dx + (int64_t)s * RN * kLdN; }
+    int64_t do1_at(int s) const { return do1 + (int64_t)s * RN * kLdN; }
+    int64_t g_at(int s) const { return g + (int64_t)s * RN * kLdN; }
+    int64_t G3_at(int s) const { return G3 + (int64_t)s * RN * kLdE; }
+    int64_t dU_at(int s) const { return dU + (int64_t)s * RN * kLdE; }
+    int64_t dV_at(int s) const { return dV + (int64_t)s * RN * kLdE; }
+    int64_t dP_at(int k) const { return dP + (int64_t)(k & 1) * RN * kLdN; }
+};
+
+static constexpr int kMaxChunks = 1024;
+
+static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
+    Ws w;
+    w.S = S;
+    w.training = training;
+    w.RN = up(std::max<int64_t>(n_nodes, 1), 32);
+    w.NB = n_eblocks;
+    w.RE = n_eblocks * 32;
+    int64_t cur = 0;  // floats
+    auto take = [&](int64_t nfl) {
+        int64_t o = cur;
+        cur += up(nfl, 64);
+        return o;
+    };
+    // packs
+    int64_t poff = 0;
+    for (int id = 0; id < PK_COUNT; ++id) {
+        w.ps.off[id] = poff;
+        poff += up((int64_t)pack_rows(id) * pack_cols(id), 64);
+    }
+    w.ps.total = poff;
+    w.pk = take(poff);
+    const int64_t nN = w.RN * kLdN, nE = w.RN * kLdE, eE = w.RE * kLdE;
+    w.co = take(nN);
+    w.P = take(nN * w.sP());
+    w.U = take(nE * w.sStep());
+    w.V = take(nE * w.sStep());
+    w.H2s = take(nE * w.sStep());
+    w.A = take(eE);
+    if (training) {
+        w.zo1 = take(nN);
+        w.a = take(nN * S);
+        w.o1 = take(nN * S);
+        w.z1 = take(eE);
+        w.z2 = take(eE);
+        w.z3 = take(eE);
+        w.cr = take(eE);
+        w.mask1 = take(w.NB * kLdE * S);
+        w.mask2 = take(w.NB * 160 * S);
+        w.dx = take(nN * S);
+        w.do1 = take(nN * S);
+        w.g = take(nN * S);
+        w.G3 = take(nE * S);
+        w.dU = take(nE * S);
+        w.dV = take(nE * S);
+        w.dP = take(nN * 2);
+        w.dco = take(nN);
+        w.dzo2 = take(nN);
+        w.dzo1 = take(nN);
+        w.dA = take(eE);
+        w.dz4 = take(eE);
+        w.dz3 = take(eE);
+        w.dz2 = take(eE);
+        w.dz1 = take(eE);
+        w.slab_floats = (int64_t)kMaxChunks * 160 * 160;
+        w.slab = take(w.slab_floats);
+    } else {
+        w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = -1;
+        w.dx = w.do1 = w.g = w.G3 = w.dU = w.dV = w.dP = w.dco = w.dzo2 = w.dzo1 = -1;
+        w.dA = w.dz4 = w.dz3 = w.dz2 = w.dz1 = w.slab = -1;
+        w.slab_floats = 0;
+    }
+    w.total = cur * 4;
+    return w;
+}
+
+// ---------------------------------------------------------------- weight packs ---------------
+static void build_packs(const Ws& w, PrepArgs& pa) {
+    const ParamTable& pt = param_table();
+    auto T = [&](int id) { return pt.t[id]; };
+    auto mk = [&](int pid, int tid, int src_rows, int src_cols, int row0, int transpose, int perm) {
+        PackDesc d{};
+        d.dst_off = w.ps.off[pid];
+        d.src_off = T(tid).offset;
+        d.rows = pack_rows(pid);
+        d.cols = pack_cols(pid);
+        d.src_rows = src_rows;
+        d.src_cols = src_cols;
+        d.src_ld = T(tid).cols;
+        d.src_row0 = row0;
+        d.transpose = transpose;
+        d.perm = perm;
+        pa.desc[pid] = d;
+    };
+    // forward [in][out]
+    mk(PK_RM1, T_RM1K, 150, 150, 0, 0, 0);
+    mk(PK_RM2, T_RM2K, 150, 150, 0, 0, 0);
+    mk(PK_RM3, T_RM3K, 150, 150, 0, 0, 0);
+    mk(PK_W1A, T_RMP0K, 150, 150, 0, 0, 0);
+    mk(PK_OM1, T_OM1K, 100, 100, 0, 0, 0);
+    mk(PK_W1B, T_RMP0K, 100, 150, 150, 0, 0);
+    mk(PK_W1C, T_RMP0K, 100, 150, 250, 0, 0);
+    mk(PK_W2, T_RMP1K, 150, 150, 0, 0, 0);
+    mk(PK_W3A, T_RMP2K, 150, 100, 0, 0, 0);   // row 150 (bias) patched below
+    mk(PK_WO1C, T_OMP0K, 100, 100, 0, 0, 0);
+    mk(PK_WO1A, T_OMP0K, 100, 100, 100, 0, 0);
+    mk(PK_WO1P, T_OMP0K, 100, 100, 200, 0, 0);
+    mk(PK_WO2, T_OMP1K, 100, 101, 0, 0, 1);
+    // backward transposes: dst[r][c] = src[c + row0][perm? (r)]; (transpose: source row = c, source col = r)
+    mk(PK_W2T, T_RMP1K, 150, 150, 0, 1, 0);
+    mk(PK_W1BT, T_RMP0K, 100, 150, 150, 1, 0);
+    mk(PK_W1CT, T_RMP0K, 100, 150, 250, 1, 0);
+    mk(PK_WO2T, T_OMP1K, 100, 101, 0, 1, 1);
+    mk(PK_WO1CT, T_OMP0K, 100, 100, 0, 1, 0);
+    mk(PK_WO1AT, T_OMP0K, 100, 100, 100, 1, 0);
+    mk(PK_WO1PT, T_OMP0K, 100, 100, 200, 1, 0);
+    mk(PK_W3T, T_RMP2K, 150, 100, 0, 1, 0);
+    mk(PK_W1AT, T_RMP0K, 150, 150, 0, 1, 0);
+    mk(PK_RM3T, T_RM3K, 150, 150, 0, 1, 0);
+    mk(PK_RM2T, T_RM2K, 150, 150, 0, 1, 0);
+    mk(PK_RM1T, T_RM1K, 150, 150, 0, 1, 0);
+    mk(PK_OM1T, T_OM1K, 100, 100, 0, 1, 0);
+    // biases (rows = 1)
+    mk(PB_RM1, T_RM1B, 1, 150, 0, 0, 0);
+    mk(PB_RM2, T_RM2B, 1, 150, 0, 0, 0);
+    mk(PB_RM3, T_RM3B, 1, 150, 0, 0, 0);
+    mk(PB_W1A, T_RMP0B, 1, 150, 0, 0, 0);
+    mk(PB_W2, T_RMP1B, 1, 150, 0, 0, 0);
+    mk(PB_OM1, T_OM1B, 1, 100, 0, 0, 0);
+    mk(PB_O1, T_OMP0B, 1, 100, 0, 0, 0);
+    mk(PB_O2P, T_OMP1B, 1, 101, 0, 0, 1);
+    mk(PK_RM0, T_RM0K, 2, 150, 0, 0, 0);
+    mk(PK_OM0, T_OM0K, 2, 100, 0, 0, 0);
+    mk(PB_RM0, T_RM0B, 1, 150, 0, 0, 0);
+    mk(PB_OM0, T_OM0B, 1, 100, 0, 0, 0);
+}
+
+struct Ctx {
+    const Ws& w;
+    char* base;
+    float* f(int64_t off) const { return off < 0 ? nullptr : reinterpret_cast<float*>(base) + off; }
+    uint32_t* u(int64_t off) const { return off < 0 ? nullptr : reinterpret_cast<uint32_t*>(base) + off; }
+    const float* pk(int id) const { return reinterpret_cast<const float*>(base) + w.pk + w.ps.off[id]; }
+};
+
+static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
+    if (!b || !r) return SPWGNN_E_ARG;
+    if (b->n_nodes < 1 || b->n_wtiles < 1 || b->n_eblocks < 1) return SPWGNN_E_SHAPE;
+    if (b->nw_max < 1 || b->nw_max > kNwMaxLimit) return SPWGNN_E_SHAPE;
+    if (r->mp_steps < 1 || r->mp_steps > 64) return SPWGNN_E_SHAPE;
+    if (!b->pos || !b->wtile || !b->edge_src || !b->edge_dst || !b->blk_csr) return SPWGNN_E_ARG;
+    if (r->dropout < 0.f || r->dropout >= 1.f) return SPWGNN_E_ARG;
+    if (r->training && r->dropout > 0.f && (!b->node_tower || !b->node_local)) return SPWGNN_E_ARG;
+    return SPWGNN_OK;
+}
+
+#define SPW_CHECK(x)                                  \
+    do {                                              \
+        hipError_t e_ = (x);                          \
+        if (e_ != hipSuccess) return (int32_t)e_;     \
+    } while (0)
+
+static int32_t run_forward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w,
+                           char* base, float* logits, hipStream_t st) {
+    Ctx c{w, base};
+    PrepArgs pa{};
+    pa.params = params;
+    pa.pk = c.f(w.pk);
+    build_packs(w, pa);
+    SPW_CHECK(launch_prep_weights(pa, st));
+    // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
+    SPW_CHECK(hipMemcpyAsync(c.f(w.pk + w.ps.off[PK_W3A] + 150 * 128), params + param_table().t[T_RMP2B].offset,
+                             100 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    const bool drop = r->training && r->dropout > 0.f;
+    const uint32_t thresh = (uint32_t)std::min(4294967295.0, std::floor((double)r->dropout * 4294967296.0));
+    const float scale = drop ? 1.0f / (1.0f - r->dropout) : 1.0f;
+
+    EncNodeArgs en{};
+    en.n_nodes = b->n_nodes;
+    en.pos = b->pos;
+    en.prop = b->prop;
+    en.node_tower = b->node_tower;
+    en.node_local = b->node_local;
+    en.w_om0 = c.pk(PK_OM0);
+    en.b_om0 = c.pk(PB_OM0);
+    en.w_om1 = c.pk(PK_OM1);
+    en.b_om1 = c.pk(PB_OM1);
+    en.w1b = c.pk(PK_W1B);
+    en.w1c = c.pk(PK_W1C);
+    en.zo1 = c.f(w.zo1);
+    en.co = c.f(w.co);
+    en.P0 = c.f(w.P_at(0));
+    en.U0 = c.f(w.U_at(0));
+    en.V0 = c.f(w.V_at(0));
+    en.dropout_on = drop;
+    en.thresh = thresh;
+    en.scale = scale;
+    en.seed = r->seed;
+    SPW_CHECK(launch_enc_node(en, st));
+
+    EncEdgeArgs ee{};
+    ee.n_eblocks = b->n_eblocks;
+    ee.pos = b->pos;
+    ee.esrc = b->edge_src;
+    ee.edst = b->edge_dst;
+    ee.node_tower = b->node_tower;
+    ee.node_local = b->node_local;
+    ee.w_rm0 = c.pk(PK_RM0);
+    ee.b_rm0 = c.pk(PB_RM0);
+    ee.w_rm1 = c.pk(PK_RM1);
+    ee.b_rm1 = c.pk(PB_RM1);
+    ee.w_rm2 = c.pk(PK_RM2);
+    ee.b_rm2 = c.pk(PB_RM2);
+    ee.w_rm3 = c.pk(PK_RM3);
+    ee.b_rm3 = c.pk(PB_RM3);
+    ee.w_w1a = c.pk(PK_W1A);
+    ee.b_w1a = c.pk(PB_W1A);
+    ee.z1 = c.f(w.z1);
+    ee.z2 = c.f(w.z2);
+    ee.z3 = c.f(w.z3);
+    ee.cr = c.f(w.cr);
+    ee.A = c.f(w.A);
+    ee.dropout_on = drop;
+    ee.thresh = thresh;
+    ee.scale = scale;
+    ee.seed = r->seed;
+    SPW_CHECK(launch_enc_edge(ee, st));
+
+    const int S = r->mp_steps;
+    for (int s = 0; s < S; ++s) {
+        EdgeFwdArgs ef{};
+        ef.n_wtiles = b->n_wtiles;
+        ef.nw_max = b->nw_max;
+        ef.wpg = edge_wpg(edge_fwd_lds_per_wave(b->nw_max));
+        ef.wtile = b->wtile;
+        ef.esrc = b->edge_src;
+        ef.edst = b->edge_dst;
+        ef.csr = reinterpret_cast<const uint32_t*>(b->blk_csr);
+        ef.A = c.f(w.A);
+        ef.U = c.f(w.U_at(s));
+        ef.V = c.f(w.V_at(s));
+        ef.w2 = c.pk(PK_W2);
+        ef.b2 = c.pk(PB_W2);
+        ef.H2s = c.f(w.H2s_at(s));
+        ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
+        ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
+        SPW_CHECK(launch_edge_fwd(ef, st));
+
+        NodeFwdArgs nf{};
+        nf.n_nodes = b->n_nodes;
+        nf.H2s = c.f(w.H2s_at(s));
+        nf.P = c.f(w.P_at(s));
+        nf.co = c.f(w.co);
+        nf.a_out = r->training ? c.f(w.a_at(s)) : nullptr;
+        nf.o1_out = r->training ? c.f(w.o1_at(s)) : nullptr;
+        nf.Pn = c.f(w.P_at(s + 1));
+        nf.logits = (s == S - 1) ? logits : nullptr;
+        nf.U = (s + 1 < S) ? c.f(w.U_at(s + 1)) : nullptr;
+        nf.V = (s + 1 < S) ? c.f(w.V_at(s + 1)) : nullptr;
+        nf.w3a = c.pk(PK_W3A);
+        nf.wo1c = c.pk(PK_WO1C);
+        nf.wo1a = c.pk(PK_WO1A);
+        nf.wo1p = c.pk(PK_WO1P);
+        nf.wo2 = c.pk(PK_WO2);
+        nf.w1b = c.pk(PK_W1B);
+        nf.w1c = c.pk(PK_W1C);
+        nf.bo1 = c.pk(PB_O1);
+        nf.bo2p = c.pk(PB_O2P);
+        SPW_CHECK(launch_node_fwd(nf, st));
+    }
+    return SPWGNN_OK;
+}
+
+struct WgSpec {
+    int xmode = XM_ROW, ymode = YM_ROW;
+    const float* x = nullptr;
+    int x_ld = 0, x_width = 0, x_ones = -1;
+    int64_t x_count = 1, x_stride = 0;
+    const float* y = nullptr;
+    int y_ld = 0, y_width = 0;
+    int64_t y_count = 1, y_stride = 0;
+    int64_t rows = 0;
+    int kx_pad = 0, ny_pad = 0;
+    // reduce target
+    int tk = -1, tb = -1, k_rows = 0, k_row0 = 0, bias_row = -1, perm = 0;
+};
+
+static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, hipStream_t st,
+                         int64_t U_off, int64_t V_off, int64_t G3_off, int64_t m2_off) {
+    const Ws& w = c.w;
+    if (g.rows <= 0) return SPWGNN_OK;
+    int64_t chunks = (g.rows + 32 * 8 - 1) / (32 * 8);
+    chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, kMaxChunks));
+    int64_t rpc = up((g.rows + chunks - 1) / chunks, 32);
+    chunks = (g.rows + rpc - 1) / rpc;
+    WgradArgs a{};
+    a.rows = g.rows;
+    a.rows_per_chunk = rpc;
+    a.xmode = g.xmode;
+    a.ymode = g.ymode;
+    a.kx_pad = g.kx_pad;
+    a.ny_pad = g.ny_pad;
+    a.x_ptr = g.x;
+    a.x_ld = g.x_ld;
+    a.x_width = g.x_width;
+    a.x_ones = g.x_ones;
+    a.x_count = g.x_count;
+    a.x_stride = g.x_stride;
+    a.y_ptr = g.y;
+    a.y_ld = g.y_ld;
+    a.y_width = g.y_width;
+    a.y_count = g.y_count;
+    a.y_stride = g.y_stride;
+    a.pos = b->pos;
+    a.esrc = b->edge_src;
+    a.edst = b->edge_dst;
+    a.A = c.f(w.A);
+    a.U = c.f(U_off);
+    a.V = c.f(V_off);
+    a.G3 = c.f(G3_off);
+    a.mask2 = c.u(m2_off);
+    a.RE = w.RE;
+    a.RN = w.RN;
+    a.slab = c.f(w.slab);
+    SPW_CHECK(launch_wgrad(a, (int)chunks, st));
+    const ParamTable& pt = param_table();
+    ReduceArgs ra{};
+    ra.slab = c.f(w.slab);
+    ra.chunks = (int)chunks;
+    ra.kx_pad = g.kx_pad;
+    ra.ny_pad = g.ny_pad;
+    ra.out = grads;
+    ra.kernel_off = g.tk >= 0 ? pt.t[g.tk].offset : -1;
+    ra.kernel_rows = g.k_rows;
+    ra.kernel_cols = g.tk >= 0 ? pt.t[g.tk].cols : pt.t[g.tb].cols;
+    ra.kernel_row0 = g.k_row0;
+    ra.bias_off = g.tb >= 0 ? pt.t[g.tb].offset : -1;
+    ra.bias_row = g.bias_row;
+    ra.perm = g.perm;
+    SPW_CHECK(launch_wgrad_reduce(ra, st));
+    return SPWGNN_OK;
+}
+
+int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w, char* base,
+                     const float* dlogits, float* grads, float* dprop, hipStream_t st) {
+    (void)params;  // the packed copies made by the forward on this workspace are used
+    Ctx c{w, base};
+    const int S = r->mp_steps;
+    const int64_t nN = b->n_nodes;
+    const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
+    SPW_CHECK(hipMemsetAsync(grads, 0, param_table().total * sizeof(float), st));
+
+    for (int s = S - 1; s >= 0; --s) {
+        const bool first = (s == S - 1);
+        NodeBwdArgs nb{};
+        nb.n_nodes = b->n_nodes;
+        nb.first = first;
+        nb.tail = 0;
+        nb.dPin = first ? nullptr : c.f(w.dP_at(s + 1));
+        nb.dU = first ? nullptr : c.f(w.dU_at(s + 1));
+        nb.dV = first ? nullptr : c.f(w.dV_at(s + 1));
+        nb.Pn = c.f(w.P_at(s + 1));
+        nb.o1 = c.f(w.o1_at(s));
+        nb.a = c.f(w.a_at(s));
+        nb.dlogits = dlogits;
+        nb.dx = c.f(w.dx_at(s));
+        nb.do1 = c.f(w.do1_at(s));
+        nb.g = c.f(w.g_at(s));
+        nb.G3 = c.f(w.G3_at(s));
+        nb.dPout = c.f(w.dP_at(s));
+        nb.dco = c.f(w.dco);
+        nb.dco_accumulate = !first;
+        nb.w1bt = c.pk(PK_W1BT);
+        nb.w1ct = c.pk(PK_W1CT);
+        nb.wo2t = c.pk(PK_WO2T);
+        nb.wo1ct = c.pk(PK_WO1CT);
+        nb.wo1at = c.pk(PK_WO1AT);
+        nb.wo1pt = c.pk(PK_WO1PT);
+        nb.w3t = c.pk(PK_W3T);
+        SPW_CHECK(launch_node_bwd(nb, st));
+
+        EdgeBwdArgs eb{};
+        eb.n_wtiles = b->n_wtiles;
+        eb.nw_max = b->nw_max;
+        eb.wpg = edge_wpg(edge_bwd_lds_per_wave(b->nw_max));
+        eb.dA_accumulate = !first;
+        eb.wtile = b->wtile;
+        eb.esrc = b->edge_src;
+        eb.edst = b->edge_dst;
+        eb.csr = reinterpret_cast<const uint32_t*>(b->blk_csr);
+        eb.mask1 = c.u(w.m1_at(s));
+        eb.mask2 = c.u(w.m2_at(s));
+        eb.G3 = c.f(w.G3_at(s));
+        eb.w2t = c.pk(PK_W2T);
+        eb.dA = c.f(w.dA);
+        eb.dU = c.f(w.dU_at(s));
+        eb.dV = c.f(w.dV_at(s));
+        SPW_CHECK(launch_edge_bwd(eb, st));
+    }
+    if (dprop) {
+        NodeBwdArgs nb{};
+        nb.n_nodes = b->n_nodes;
+        nb.first = 0;
+        nb.tail = 1;
+        nb.dPin = c.f(w.dP_at(0));
+        nb.dU = c.f(w.dU_at(0));
+        nb.dV = c.f(w.dV_at(0));
+        nb.dprop = dprop;
+        nb.w1bt = c.pk(PK_W1BT);
+        nb.w1ct = c.pk(PK_W1CT);
+        SPW_CHECK(launch_node_bwd(nb, st));
+    }
+    EncEdgeBwdArgs eeb{};
+    eeb.n_eblocks = b->n_eblocks;
+    eeb.dA = c.f(w.dA);
+    eeb.cr = c.f(w.cr);
+    eeb.z3 = c.f(w.z3);
+    eeb.z2 = c.f(w.z2);
+    eeb.z1 = c.f(w.z1);
+    eeb.w1at = c.pk(PK_W1AT);
+    eeb.rm3t = c.pk(PK_RM3T);
+    eeb.rm2t = c.pk(PK_RM2T);
+    eeb.rm1t = c.pk(PK_RM1T);
+    eeb.dz4 = c.f(w.dz4);
+    eeb.dz3 = c.f(w.dz3);
+    eeb.dz2 = c.f(w.dz2);
+    eeb.dz1 = c.f(w.dz1);
+    eeb.scale = scale;
+    SPW_CHECK(launch_enc_edge_bwd(eeb, st));
+
+    EncNodeBwdArgs enb{};
+    enb.n_nodes = b->n_nodes;
+    enb.dco = c.f(w.dco);
+    enb.co = c.f(w.co);
+    enb.zo1 = c.f(w.zo1);
+    enb.om1t = c.pk(PK_OM1T);
+    enb.dzo2 = c.f(w.dzo2);
+    enb.dzo1 = c.f(w.dzo1);
+    enb.scale = scale;
+    SPW_CHECK(launch_enc_node_bwd(enb, st));
+
+    // ---- weight gradients ----
+    const int64_t RE = w.RE, RN = w.RN;
+    auto edge_row = [&](WgSpec& g, int64_t xoff, int64_t yoff, int tk, int tb) {
+        g.x = c.f(xoff); g.x_ld = kLdE; g.x_width = kFE; g.x_ones = kFE; g.x_count = RE; g.x_stride = 0;
+        g.y = c.f(yoff); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE; g.y_stride = 0;
+        g.rows = RE; g.kx_pad = 160; g.ny_pad = 160;
+        g.tk = tk; g.tb = tb; g.k_rows = kFE; g.k_row0 = 0; g.bias_row = kFE;
+    };
+    int32_t e;
+    {   // rm.0: X = [d | 1]
+        WgSpec g; g.xmode = XM_EDGE_D; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
+        g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
+        g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
+    {   // rmp.1 (W2, b2): X = [h1 | 1] recomputed, Y = dh2pre, over all steps
+        WgSpec g; g.xmode = XM_EDGE_H1; g.ymode = YM_EDGE_DH2; g.kx_pad = 160; g.ny_pad = 160; g.rows = RE * S;
+        g.tk = T_RMP1K; g.tb = T_RMP1B; g.k_rows = kFE; g.bias_row = kFE;
+        if ((e = run_wgrad(c, b, g, grads, st, w.U, w.V, w.G3, w.mask2))) return e;
+    }
+    auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
+                       int yw, int kxp, int nyp) {
+        g.x = c.f(xoff); g.x_ld = xld; g.x_width = xw; g.x_ones = xones; g.x_count = nN; g.x_stride = xstride;
+        g.y = c.f(yoff); g.y_ld = yld; g.y_width = yw; g.y_count = nN; g.y_stride = RN;
+        g.rows = nN * S; g.kx_pad = kxp; g.ny_pad = nyp;
+    };
+    {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
+        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // rmp.0 rows 250..349 (W1c)
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
+        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // rmp.2 (W3, b3): X = [H2s | deg]
+        WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
+        g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
+        WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // omp.0 rows 100..199 (effect part)
+        WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // omp.0 rows 200..299 (P part)
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // omp.1 (Wo2, bo2), x' column order → Keras order
+        WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
+        g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // om.0: X = [y, w | 1]
+        WgSpec g; g.xmode = XM_NODE_O; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
+        g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
+        g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    {   // om.1
+        WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
+        g.rows = nN; g.y_stride = 0;
+        g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
+        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+    }
+    return SPWGNN_OK;
+}
+
+}  // namespace spw
+
+using namespace spw;
+
+extern "C" {
+
+int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training) {
+    if (n_nodes < 1 || n_eblocks < 1 || mp_steps < 1) return -1;
+    return make_ws(n_nodes, n_eblocks, mp_steps, training ? 1 : 0).total;
+}
+
+int32_t spwgnn_forward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run, void* workspace,
+                       int64_t workspace_bytes, float* logits, spwgnn_stream_t stream) {
+    int32_t stt = validate(batch, run);
+    if (stt) return stt;
+    if (!params || !workspace || !logits) return SPWGNN_E_ARG;
+    Ws w = make_ws(batch->n_nodes, batch->n_eblocks, run->mp_steps, run->training ? 1 : 0);
+    if (workspace_bytes < w.total) return SPWGNN_E_WORKSPACE;
+    return run_forward(params, batch, run, w, static_cast<char*>(workspace), logits,
+                       static_cast<hipStream_t>(stream));
+}
+
+int32_t spwgnn_backward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run, void* workspace,
+                        int64_t workspace_bytes, const float* dlogits, float* grads, float* dprop,
+                        spwgnn_stream_t stream) {
+    int32_t stt = validate(batch, run);
+    if (stt) return stt;
+    if (!run->training) return SPWGNN_E_NOTRAIN;
+    if (!params || !workspace || !dlogits || !grads) return SPWGNN_E_ARG;
+    Ws w = make_ws(batch->n_nodes, batch->n_eblocks, run->mp_steps, 1);
+    if (workspace_bytes < w.total) return SPWGNN_E_WORKSPACE;
+    return run_backward(params, batch, run, w, static_cast<char*>(workspace), dlogits, grads, dprop,
+                        static_cast<hipStream_t>(stream));
+}
+
+int64_t spwgnn_bce_scratch_bytes(int64_t n) {
+    (void)n;
+    return 256 * 2 * sizeof(float);
+}
+
+int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* out3, float* dlogits, void* scratch,
+                   spwgnn_stream_t stream) {
+    if (!logits || !targets || !out3 || !scratch || n < 1) return SPWGNN_E_ARG;
+    BceArgs a{};
+    a.logits = logits;
+    a.targets = targets;
+    a.n = n;
+    a.dlogits = dlogits;
+    a.partial = static_cast<float*>(scratch);
+    a.out3 = out3;
+    a.blocks = (int)std::min<int64_t>(256, (n + 255) / 256);
+    hipError_t e = launch_bce(a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
+int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64_t n, int32_t step, float lr,
+                    float beta1, float beta2, float eps, float l2, float grad_scale, spwgnn_stream_t stream) {
+    if (!params || !grads || !m || !v || n < 1 || step < 1) return SPWGNN_E_ARG;
+    AdamArgs a{};
+    a.p = params;
+    a.g = grads;
+    a.m = m;
+    a.v = v;
+    a.n = n;
+    const double t = step;
+    a.lr_t = (float)(lr * std::sqrt(1.0 - std::pow((double)beta2, t)) / (1.0 - std::pow((double)beta1, t)));
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.l2 = l2;
+    a.gscale = grad_scale;
+    hipError_t e = launch_adam(a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
+int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream) {
+    if (!logits || !probs || n < 1) return SPWGNN_E_ARG;
+    hipError_t e = launch_sigmoid(logits, probs, n, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+// Device helpers shared by the gfx950 kernels of libspwgnn_hip.
+//
+// MFMA: v_mfma_f32_32x32x2_f32 (exact fp32, one rounding per product, fmaf-chain order).
+//   A operand, lane l: A[i = l&31][k = l>>5];  B operand: B[k = l>>5][j = l&31]
+//   C/D: 16 regs, reg r of lane l holds C[row = rho(r, l>>5)][col = l&31],
+//        rho(r,h) = (r&3) + 8(r>>2) + 4h.
+// Two orientations are used:
+//   natural     rows (edges/nodes) on the A lanes, features on the C lanes — segment sums run
+//               over the C registers;
+//   transposed  features on the A lanes (weights), rows on the B/C lanes — an MLP chains layer to
+//               layer in registers (C of layer n is the B operand of layer n+1, k-step = C reg).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "spwgnn_layout.h"
+
+namespace spw {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ constexpr int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    return z;
+}
+
+// Orders this wave's LDS writes before its later LDS reads (single wavefront, no WG barrier:
+// waves of a workgroup run independent tiles).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+// ---------------------------------------------------------------------------------------------
+// Dropout key (our own counter-based RNG; Keras' TF draws cannot be reproduced — DESIGN.md §6).
+// keep(seed, kind, tower, a, b, feature) = mix(...) >= rate·2^32.  Restated bit-exactly in
+// tests (oracle helper) to build the oracle's multiplicative masks.
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t drop_row_key(uint64_t seed, uint32_t kind, uint32_t tower,
+                                                          uint32_t a, uint32_t b) {
+    uint32_t h = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + kind));
+    h = mix32(h ^ tower);
+    h = mix32(h ^ ((a << 16) | (b & 0xffffu)));
+    return h;
+}
+__host__ __device__ __forceinline__ bool drop_keep(uint32_t rowkey, uint32_t feature, uint32_t thresh) {
+    return mix32(rowkey ^ feature) >= thresh;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Packed (zero-padded) weight copies built by k_prep_weights at the start of every call.
+enum PackId : int {
+    PK_RM1 = 0, PK_RM2, PK_RM3, PK_W1A,       // [160][160] [in][out]
+    PK_OM1,                                    // [128][128]
+    PK_W1B, PK_W1C,                            // [128][160] [P feature][U/V feature]
+    PK_W2,                                     // [160][160] rmp.1 [in][out]
+    PK_W3A,                                    // [160][128] rmp.2 rows 0..149, row 150 = rmp.2 bias
+    PK_WO1C, PK_WO1A, PK_WO1P,                 // [128][128] omp.0 rows 0-99 / 100-199 / 200-299
+    PK_WO2,                                    // [128][128] omp.1 with permuted columns (x' order)
+    PK_W2T,                                    // [160][160] W2T[k][j] = W2[j][k]
+    PK_W1BT, PK_W1CT,                          // [160][128] W1bT[k][p] = W1b[p][k]
+    PK_WO2T,                                   // [128][128] Wo2pT[k][i] = Wo2p[i][k]
+    PK_WO1CT, PK_WO1AT, PK_WO1PT,              // [128][128] Wo1T_p[k][i] = Wo1[off_p+i][k]
+    PK_W3T,                                    // [128][160] W3T[k][i] = W3[i][k]
+    PK_W1AT, PK_RM3T, PK_RM2T, PK_RM1T,        // [160][160] transposes
+    PK_OM1T,                                   // [128][128]
+    // biases, padded vectors
+    PB_RM1, PB_RM2, PB_RM3, PB_W1A, PB_W2,     // [160]
+    PB_OM1, PB_O1, PB_O2P,                     // [128]  (PB_O2P permuted like PK_WO2)
+    PK_RM0,                                    // [2][160] rm.0 kernel
+    PK_OM0,                                    // [2][128] om.0 kernel
+    PB_RM0, PB_OM0,                            // [160], [128]
+    PK_COUNT
+};
+
+struct PackSlots {
+    int64_t off[PK_COUNT];
+    int64_t total;
+};
+
+__host__ __device__ inline int pack_rows(int id) {
+    switch (id) {
+        case PK_RM1: case PK_RM2: case PK_RM3: case PK_W1A: case PK_W2: case PK_W2T:
+        case PK_W1AT: case PK_RM3T: case PK_RM2T: case PK_RM1T: case PK_W3A: case PK_W1BT: case PK_W1CT:
+            return 160;
+        case PB_RM1: case PB_RM2: case PB_RM3: case PB_W1A: case PB_W2: case PB_OM1: case PB_O1: case PB_O2P:
+        case PB_RM0: case PB_OM0:
+            return 1;
+        case PK_RM0: case PK_OM0:
+            return 2;
+        default:
+            return 128;
+    }
+}
+__host__ __device__ inline int pack_cols(int id) {
+    switch (id) {
+        case PK_RM1: case PK_RM2: case PK_RM3: case PK_W1A: case PK_W2: case PK_W2T:
+        case PK_W1AT: case PK_RM3T: case PK_RM2T: case PK_RM1T: case PK_W1B: case PK_W1C: case PK_W3T:
+        case PB_RM1: case PB_RM2: case PB_RM3: case PB_W1A: case PB_W2:
+        case PK_RM0: case PB_RM0:
+            return 160;
+        default:
+            return 128;
+    }
+}
+
+// x' (permuted omp.1 output) column f' ↔ Keras column: state f' < 100 ↔ col f'+1, logit ↔ col 0.
+__host__ __device__ __forceinline__ int wo2_perm(int fp) { return fp < 100 ? fp + 1 : (fp == 100 ? 0 : -1); }
+
+}  // namespace spw

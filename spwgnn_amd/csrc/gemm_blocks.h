@@ -1,0 +1,128 @@
+// Register-level MFMA building blocks (fp32, v_mfma_f32_32x32x2_f32) used by every kernel.
+#pragma once
+#include "device_common.h"
+
+namespace spw {
+
+// ---- row I/O for the transposed orientation (lane (j, h) owns row j; C reg r of tile t is
+//      feature rho(r,h) + 32t, and regs 4q..4q+3 are the 4 consecutive features 8q + 4h + 32t + 0..3).
+template <int NT>
+__device__ __forceinline__ void store_rho(float* __restrict__ row, const f32x16 (&X)[NT], int h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float4 v = make_float4(X[t][4 * q], X[t][4 * q + 1], X[t][4 * q + 2], X[t][4 * q + 3]);
+            *reinterpret_cast<float4*>(row + 32 * t + 8 * q + 4 * h) = v;
+        }
+}
+template <int NT>
+__device__ __forceinline__ void store_rho_masked(float* __restrict__ row, const f32x16 (&X)[NT], int h, bool valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float4 v = valid ? make_float4(X[t][4 * q], X[t][4 * q + 1], X[t][4 * q + 2], X[t][4 * q + 3])
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(row + 32 * t + 8 * q + 4 * h) = v;
+        }
+}
+template <int NT>
+__device__ __forceinline__ void load_rho(const float* __restrict__ row, f32x16 (&X)[NT], int h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float4 v = *reinterpret_cast<const float4*>(row + 32 * t + 8 * q + 4 * h);
+            X[t][4 * q] = v.x;
+            X[t][4 * q + 1] = v.y;
+            X[t][4 * q + 2] = v.z;
+            X[t][4 * q + 3] = v.w;
+        }
+}
+
+// ---- split-halves row chunk: lane half h holds features [KH*h, KH*h+KH) of its row.
+template <int KH>
+__device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh, float (&x)[KH]) {
+    static_assert(KH % 4 == 0, "KH multiple of 4");
+    const float4* p = reinterpret_cast<const float4*>(row_plus_khh);
+#pragma unroll
+    for (int q = 0; q < KH / 4; ++q) {
+        float4 v = p[q];
+        x[4 * q] = v.x;
+        x[4 * q + 1] = v.y;
+        x[4 * q + 2] = v.z;
+        x[4 * q + 3] = v.w;
+    }
+}
+
+// ---- transposed orientation: out[t] += Wᵀ·in over register k-steps.
+// in: C layout of the previous layer (feature rho(r,h)+32tp on the lane's row); the k-steps are
+// (tp, r) for tp < NT_IN, with r < LAST_R in the last input tile (rows beyond are zero padding).
+// W: [in][out] row-major with row stride LDW; the A operand of lane (i,h) is W[k(h)][32t + i].
+template <int NT_OUT, int NT_IN, int LAST_R, int LDW>
+__device__ __forceinline__ void tchain_acc(const f32x16 (&in)[NT_IN], f32x16 (&out)[NT_OUT],
+                                           const float* __restrict__ W, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    const float* wbase = W + (4 * h) * LDW + i;
+#pragma unroll
+    for (int tp = 0; tp < NT_IN; ++tp) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (tp == NT_IN - 1 && r >= LAST_R) continue;
+            const float* wrow = wbase + (rho(r, 0) + 32 * tp) * LDW;
+            const float b = in[tp][r];
+#pragma unroll
+            for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wrow[32 * t], b, out[t]);
+        }
+    }
+}
+
+// ---- transposed orientation, B operand from a split-halves row chunk x (features KH*h + s).
+template <int NT_OUT, int KH, int LDW>
+__device__ __forceinline__ void tgemm_half_acc(const float (&x)[KH], f32x16 (&out)[NT_OUT],
+                                               const float* __restrict__ W, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    const float* wbase = W + (KH * h) * LDW + i;
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+        const float* wrow = wbase + s * LDW;
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wrow[32 * t], x[s], out[t]);
+    }
+}
+
+// ---- natural orientation: acc[t] += A·W, A operand = this lane's row chunk a (features KH*h+s),
+// W: [k][col] row stride LDW; B operand of lane (j,h) is W[KH*h + s][32t + j].
+template <int NT_OUT, int KH, int LDW>
+__device__ __forceinline__ void ngemm_acc(const float (&a)[KH], f32x16 (&acc)[NT_OUT],
+                                          const float* __restrict__ W, int lane) {
+    const int j = lane & 31, h = lane >> 5;
+    const float* wbase = W + (KH * h) * LDW + j;
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+        const float* wrow = wbase + s * LDW;
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) acc[t] = mfma32(a[s], wrow[32 * t], acc[t]);
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void zero_tiles(f32x16 (&X)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) X[t] = zero16();
+}
+
+// bias (padded vector, feature rho(r,h)+32t) + optional relu, in place (transposed C layout).
+template <int NT, bool RELU>
+__device__ __forceinline__ void bias_act_rho(f32x16 (&X)[NT], const float* __restrict__ b, int h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float v = X[t][r] + b[rho(r, 0) + 4 * h + 32 * t];
+            X[t][r] = RELU ? relu(v) : v;
+        }
+}
+
+}  // namespace spw

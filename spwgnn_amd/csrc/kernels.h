@@ -1,0 +1,184 @@
+// Kernel argument structs and declarations (libspwgnn_hip).
+#pragma once
+#include "gemm_blocks.h"
+
+namespace spw {
+
+struct PackDesc {
+    int64_t dst_off;   // floats into the pack buffer
+    int64_t src_off;   // floats into the flat params
+    int32_t rows, cols;          // destination dims
+    int32_t src_rows, src_cols;  // valid source extent (in destination orientation before transpose)
+    int32_t src_ld, src_row0;
+    int32_t transpose, perm;
+};
+struct PrepArgs {
+    const float* params;
+    float* pk;
+    PackDesc desc[PK_COUNT];  // by value (kernel-argument memory): no host→device copy, capturable
+};
+
+struct EncNodeArgs {
+    int n_nodes;
+    const float* pos;
+    const float* prop;
+    const int32_t* node_tower;
+    const int32_t* node_local;
+    const float *w_om0, *b_om0, *w_om1, *b_om1, *w1b, *w1c;
+    float *zo1, *co, *P0, *U0, *V0;
+    int dropout_on;
+    uint32_t thresh;
+    float scale;
+    uint64_t seed;
+};
+
+struct EncEdgeArgs {
+    int n_eblocks;
+    const float* pos;
+    const int32_t *esrc, *edst, *node_tower, *node_local;
+    const float *w_rm0, *b_rm0, *w_rm1, *b_rm1, *w_rm2, *b_rm2, *w_rm3, *b_rm3, *w_w1a, *b_w1a;
+    float *z1, *z2, *z3, *cr, *A;
+    int dropout_on;
+    uint32_t thresh;
+    float scale;
+    uint64_t seed;
+};
+
+struct EdgeFwdArgs {
+    int n_wtiles, nw_max, wpg;
+    const int32_t *wtile, *esrc, *edst;
+    const uint32_t* csr;
+    const float *A, *U, *V, *w2, *b2;
+    float* H2s;
+    uint32_t *mask1, *mask2;
+};
+
+struct NodeFwdArgs {
+    int n_nodes;
+    const float *H2s, *P, *co;
+    float *a_out, *o1_out, *Pn, *logits, *U, *V;
+    const float *w3a, *wo1c, *wo1a, *wo1p, *wo2, *w1b, *w1c, *bo1, *bo2p;
+};
+
+struct NodeBwdArgs {
+    int n_nodes;
+    int first;      // 1 for the last propagation step (no incoming dP, dlogits present)
+    int tail;       // 1: only compute dP0 = dPpart + dU·W1bᵀ + dV·W1cᵀ into dprop (ld 100)
+    const float *dPin, *dU, *dV;   // from step s+1 (null when first)
+    const float *Pn, *o1, *a;      // P_{s+1}, o1_s, a_s
+    const float* dlogits;
+    float *dx, *do1, *g, *G3, *dPout, *dco, *dprop;
+    int dco_accumulate;
+    const float *w1bt, *w1ct, *wo2t, *wo1ct, *wo1at, *wo1pt, *w3t;
+};
+
+struct EdgeBwdArgs {
+    int n_wtiles, nw_max, wpg;
+    int dA_accumulate;
+    const int32_t *wtile, *esrc, *edst;
+    const uint32_t* csr;
+    const uint32_t *mask1, *mask2;
+    const float *G3, *w2t;
+    float *dA, *dU, *dV;
+};
+
+struct EncEdgeBwdArgs {
+    int n_eblocks;
+    const float *dA, *cr, *z3, *z2, *z1;
+    const float *w1at, *rm3t, *rm2t, *rm1t;
+    float *dz4, *dz3, *dz2, *dz1;
+    float scale;   // dropout 1/(1-p) (1 when off)
+};
+
+struct EncNodeBwdArgs {
+    int n_nodes;
+    const float *dco, *co, *zo1, *om1t;
+    float *dzo2, *dzo1;
+    float scale;
+};
+
+// ---- weight gradients: dW = Σ_rows X[row]ᵀ·Y[row] (deterministic split-row slabs) ----
+enum XMode : int {
+    XM_ROW = 0,     // ptr[(row % bcast_rows) * ld + f], f < width; f == ones_col → 1
+    XM_EDGE_D,      // (pos[dst] - pos[src])[f] for f < 2, f == 2 → 1; padding edge → 0
+    XM_NODE_O,      // pos[n][1 + f] for f < 2, f == 2 → 1
+    XM_EDGE_H1,     // relu(A[e] + U_s[src] + V_s[dst])[f] for f < 150, f == 150 → 1 (row = s*RE + e)
+};
+enum YMode : int {
+    YM_ROW = 0,
+    YM_EDGE_DH2,    // G3_s[dst][f] * bit(mask2_s) for f < 150 (row = s*RE + e)
+};
+struct WgradArgs {
+    int64_t rows;          // logical rows L = s*count + n
+    int64_t rows_per_chunk;
+    int xmode, ymode;
+    int kx_pad, ny_pad;    // multiples of 32, <= 160
+    // X (ROW mode): physical row = (stride ? (L / count) * stride : 0) + L % count
+    const float* x_ptr;
+    int x_ld, x_width, x_ones;
+    int64_t x_count, x_stride;
+    // Y (ROW mode)
+    const float* y_ptr;
+    int y_ld, y_width;
+    int64_t y_count, y_stride;
+    // edge/node context
+    const float* pos;
+    const int32_t *esrc, *edst;
+    const float *A, *U, *V, *G3;
+    const uint32_t* mask2;
+    int64_t RE, RN;        // edge rows, node rows (per step strides)
+    float* slab;           // [chunks][kx_pad][ny_pad]
+};
+struct ReduceArgs {
+    const float* slab;
+    int chunks, kx_pad, ny_pad;
+    float* out;            // flat grads base
+    int64_t kernel_off;    // tensor offset (kernel), -1 none
+    int kernel_rows, kernel_cols, kernel_row0;  // write rows [0, kernel_rows) of slab → tensor rows kernel_row0+
+    int64_t bias_off;      // tensor offset (bias), -1 none
+    int bias_row;          // slab row holding the bias (ones column)
+    int perm;              // 1: omp.1 column permutation (slab col f' → tensor col wo2_perm(f'))
+};
+
+struct BceArgs {
+    const float *logits, *targets;
+    int64_t n;
+    float* dlogits;
+    float* partial;   // [blocks][2]
+    float* out3;
+    int blocks;
+};
+struct AdamArgs {
+    float *p, *m, *v;
+    const float* g;
+    int64_t n;
+    float lr_t, b1, b2, eps, l2, gscale;
+};
+
+// Host launchers (defined next to their kernels; each returns hipGetLastError()).
+hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st);
+hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st);
+hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st);
+hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st);
+hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st);
+hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);
+hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st);
+hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st);
+hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
+hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st);
+hipError_t launch_wgrad_reduce(const ReduceArgs& a, hipStream_t st);
+hipError_t launch_bce(const BceArgs& a, hipStream_t st);
+hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
+hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);
+
+// LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
+inline size_t edge_fwd_lds_per_wave(int nw_max) { return (size_t)(2112 + nw_max * kLdE) * 4; }
+inline size_t edge_bwd_lds_per_wave(int nw_max) { return (size_t)(2112 + 2 * nw_max * kLdE) * 4; }
+inline int edge_wpg(size_t lds_per_wave) {
+    // waves per workgroup: keep a workgroup's LDS <= 80 KiB so two workgroups share a CU
+    if (4 * lds_per_wave <= 80 * 1024) return 4;
+    if (2 * lds_per_wave <= 80 * 1024) return 2;
+    return 1;
+}
+
+}  // namespace spw

@@ -1,0 +1,346 @@
+// Backward kernels of the propagation network (replaces TF autodiff of Networks.py:121-186).
+//
+// Per step s (reverse order):
+//   k_node_bwd   dP_{s+1} = dPpart + dU_{s+1}·W1bᵀ + dV_{s+1}·W1cᵀ;  dx' = [dP ⊙ (1-P²) | dlogit];
+//                do1 = dx'·Wo2'ᵀ ⊙ [o1>0];  [dc_o | da | dP_omp] = do1·Wo1ᵀ;  g = da ⊙ (1-a²);
+//                G3 = g·W3ᵀ (the per-edge dh2 is G3[receiver] — rmp layer 3 sits behind the sum)
+//   k_edge_bwd   dh2pre = G3[r] ⊙ [h2>0];  dh1pre = dh2pre·W2ᵀ ⊙ [h1>0];  dA += dh1pre;
+//                dU = Σ_sender dh1pre, dV = Σ_receiver dh1pre (deterministic LDS segment sums)
+// Once:
+//   k_enc_edge_bwd   dc_r = dA·W1aᵀ → rm backward chain (dz4..dz1, pre-activation grads)
+//   k_enc_node_bwd   dc_o → om backward chain
+#include "kernels.h"
+
+namespace spw {
+
+// B operand streamed from a split-halves global row (transposed orientation), KH/4 float4 chunks.
+template <int NT_OUT, int KH, int LDW>
+__device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_khh, f32x16 (&out)[NT_OUT],
+                                                 const float* __restrict__ W, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    const float4* x4 = reinterpret_cast<const float4*>(row_khh);
+    const float* wbase = W + (KH * h) * LDW + i;
+    float4 nxt = x4[0];
+#pragma unroll 1
+    for (int q = 0; q < KH / 4; ++q) {
+        const float4 cur = nxt;
+        if (q + 1 < KH / 4) nxt = x4[q + 1];
+        const float xv[4] = {cur.x, cur.y, cur.z, cur.w};
+        const float* wrow = wbase + (4 * q) * LDW;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wrow[c * LDW + 32 * t], xv[c], out[t]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_node_bwd(NodeBwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nb * 32 >= a.n_nodes) return;
+    const int n = nb * 32 + j;
+    const bool valid = n < a.n_nodes;
+    const int64_t nc = valid ? n : a.n_nodes - 1;
+    const int64_t rowN = (int64_t)n * kLdN;
+
+    f32x16 D[4];
+    if (a.first) {
+        zero_tiles(D);
+    } else {
+        load_rho<4>(a.dPin + nc * kLdN, D, h);
+        tgemm_stream_acc<4, kKhE, kLdN>(a.dU + nc * kLdE + kKhE * h, D, a.w1bt, lane);
+        tgemm_stream_acc<4, kKhE, kLdN>(a.dV + nc * kLdE + kKhE * h, D, a.w1ct, lane);
+    }
+    if (a.tail) {  // dP0 = d/d 'propagation' (ld 100)
+        if (valid) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int f0 = 32 * t + 8 * q + 4 * h;
+                    if (f0 < kFN)
+                        *reinterpret_cast<float4*>(a.dprop + (int64_t)n * kFN + f0) =
+                            make_float4(D[t][4 * q], D[t][4 * q + 1], D[t][4 * q + 2], D[t][4 * q + 3]);
+                }
+        }
+        return;
+    }
+    {
+        f32x16 Pn[4];
+        load_rho<4>(a.Pn + nc * kLdN, Pn, h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                const float p = Pn[t][r];
+                D[t][r] = f < kFN ? D[t][r] * (1.f - p * p) : 0.f;  // tanh' (Networks.py:181)
+            }
+    }
+    // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
+    store_rho_masked<4>(a.dPout + rowN, D, h, valid);
+    if (a.first && h == 1) D[3][0] = valid ? a.dlogits[n] : 0.f;  // x' row 100 = logit
+    store_rho_masked<4>(a.dx + rowN, D, h, valid);
+
+    f32x16 G[4];
+    zero_tiles(G);
+    tchain_acc<4, 4, 4, kLdN>(D, G, a.wo2t, lane);
+    {
+        f32x16 O1[4];
+        load_rho<4>(a.o1 + nc * kLdN, O1, h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) G[t][r] = O1[t][r] > 0.f ? G[t][r] : 0.f;
+    }
+    store_rho_masked<4>(a.do1 + rowN, G, h, valid);
+
+    // P part of omp's input → dP_s
+    zero_tiles(D);
+    tchain_acc<4, 4, 4, kLdN>(G, D, a.wo1pt, lane);
+    {
+        f32x16 T[4];
+        load_rho<4>(a.dPout + nc * kLdN, T, h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) D[t] += T[t];
+    }
+    store_rho_masked<4>(a.dPout + rowN, D, h, valid);
+    // c_o part → dc_o (accumulated over steps in step order S-1..0)
+    zero_tiles(D);
+    tchain_acc<4, 4, 4, kLdN>(G, D, a.wo1ct, lane);
+    if (a.dco_accumulate) {
+        f32x16 T[4];
+        load_rho<4>(a.dco + nc * kLdN, T, h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) D[t] = T[t] + D[t];
+    }
+    store_rho_masked<4>(a.dco + rowN, D, h, valid);
+    // effect part → g = da ⊙ (1 - a²) → G3 = g·W3ᵀ
+    zero_tiles(D);
+    tchain_acc<4, 4, 4, kLdN>(G, D, a.wo1at, lane);
+    {
+        f32x16 Aa[4];
+        load_rho<4>(a.a + nc * kLdN, Aa, h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = Aa[t][r];
+                D[t][r] = D[t][r] * (1.f - v * v);
+            }
+    }
+    store_rho_masked<4>(a.g + rowN, D, h, valid);
+    f32x16 H[5];
+    zero_tiles(H);
+    tchain_acc<5, 4, 4, kLdE>(D, H, a.w3t, lane);
+    store_rho_masked<5>(a.G3 + (int64_t)n * kLdE, H, h, valid);
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int WORD_BASE>
+__device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint32_t csrw, int t, bool tv, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    float sum = 0.f;
+#pragma unroll 1
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + (k >> 2));
+        const int nd = (nw >> (8 * (k & 3))) & 255;
+        if (nd == 255) break;
+        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
+        const int eo = (ow >> (8 * (k & 3))) & 255;
+        sum += st[h * 1056 + eo * 33 + i];
+        int ndn = 255;
+        if (k < 31) {
+            const uint32_t nw2 = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + ((k + 1) >> 2));
+            ndn = (nw2 >> (8 * ((k + 1) & 3))) & 255;
+        }
+        if (ndn != nd) {
+            if (tv) nacc[nd * kLdE + 32 * t + i] += sum;
+            sum = 0.f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void k_edge_bwd(EdgeBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int wave = threadIdx.x >> 6;
+    const int wt = blockIdx.x * a.wpg + wave;
+    if (wt >= a.n_wtiles) return;
+    float* st = smem + wave * (2112 + 2 * a.nw_max * kLdE);
+    float* naccR = st + 2112;
+    float* naccS = naccR + a.nw_max * kLdE;
+    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    for (int idx = lane; idx < nn * kLdE; idx += 64) {
+        naccR[idx] = 0.f;
+        naccS[idx] = 0.f;
+    }
+    for (int bb = 0; bb < nb; ++bb) {
+        const int blk = fb + bb;
+        const int64_t e = (int64_t)blk * 32 + i;
+        const int d = a.edst[e];
+        const bool valid = d >= 0;
+        const int dc = valid ? d : n0;
+        // dh2pre (A operand, lane = edge, split halves): G3[receiver] ⊙ [h2 > 0]
+        const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
+        uint32_t w[5];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) w[t] = m2[32 * t];
+        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + (int64_t)dc * kLdE + kKhE * h);
+        f32x16 acc[5];
+        zero_tiles(acc);
+        const float* wbase = a.w2t + (kKhE * h) * kLdE + i;
+        float4 nxt = G4[0];
+#pragma unroll 1
+        for (int q = 0; q < kKhE / 4; ++q) {
+            const float4 cur = nxt;
+            if (q + 1 < kKhE / 4) nxt = G4[q + 1];
+            // 4 features f0..f0+3 (f0 = 76h + 4q) share one mask word (f0 % 4 == 0)
+            const int f0 = kKhE * h + 4 * q;
+            const int wi = f0 >> 5;
+            const uint32_t wd = wi == 0 ? w[0] : wi == 1 ? w[1] : wi == 2 ? w[2] : wi == 3 ? w[3] : w[4];
+            const uint32_t bits = valid ? (wd >> (f0 & 31)) : 0u;
+            float xv[4];
+            xv[0] = (bits & 1u) ? cur.x : 0.f;
+            xv[1] = (bits & 2u) ? cur.y : 0.f;
+            xv[2] = (bits & 4u) ? cur.z : 0.f;
+            xv[3] = (bits & 8u) ? cur.w : 0.f;
+            const float* wrow = wbase + (4 * q) * kLdE;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wrow[c * kLdE + 32 * t], acc[t]);
+        }
+        // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
+        const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
+        float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const uint32_t mw = m1[32 * t];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rho(r, 0) + 4 * h;
+                float v = ((mw >> row) & 1u) ? acc[t][r] : 0.f;
+                float* p = dArow + row * kLdE + 32 * t;
+                if (a.dA_accumulate) v = *p + v;
+                *p = v;
+                acc[t][r] = ((mw >> row) & 1u) ? acc[t][r] : 0.f;
+            }
+        }
+        // segment sums: receiver → dV, sender → dU
+        const uint32_t csrw = reinterpret_cast<const uint32_t*>(a.csr)[(int64_t)blk * 32 + i];
+#pragma unroll
+        for (int rd = 0; rd < 3; ++rd) {
+#pragma unroll
+            for (int slot = 0; slot < 2; ++slot) {
+                const int t = 2 * rd + slot;
+                if (t >= 5) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = acc[t][r];
+            }
+            wave_lds_sync();
+            const int t = 2 * rd + h;
+            segsum_walk_b<0>(st, naccR, csrw, t, t < 5, lane);
+            segsum_walk_b<16>(st, naccS, csrw, t, t < 5, lane);
+            wave_lds_sync();
+        }
+    }
+    float* oU = a.dU + (int64_t)n0 * kLdE;
+    float* oV = a.dV + (int64_t)n0 * kLdE;
+    for (int idx = lane; idx < nn * kLdE; idx += 64) {
+        oU[idx] = naccS[idx];
+        oV[idx] = naccR[idx];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blk >= a.n_eblocks) return;
+    const int64_t e = (int64_t)blk * 32 + j;
+    const int64_t row = e * kLdE;
+    f32x16 D[5], E[5], Z[5];
+    zero_tiles(D);
+    tgemm_stream_acc<5, kKhE, kLdE>(a.dA + row + kKhE * h, D, a.w1at, lane);  // dc_r = dA·W1aᵀ
+    load_rho<5>(a.cr + row, Z, h);
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) D[t][r] = Z[t][r] > 0.f ? D[t][r] * a.scale : 0.f;  // relu + dropout
+    store_rho<5>(a.dz4 + row, D, h);
+    zero_tiles(E);
+    tchain_acc<5, 5, 12, kLdE>(D, E, a.rm3t, lane);
+    load_rho<5>(a.z3 + row, Z, h);
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) E[t][r] = Z[t][r] > 0.f ? E[t][r] : 0.f;
+    store_rho<5>(a.dz3 + row, E, h);
+    zero_tiles(D);
+    tchain_acc<5, 5, 12, kLdE>(E, D, a.rm2t, lane);
+    load_rho<5>(a.z2 + row, Z, h);
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) D[t][r] = Z[t][r] > 0.f ? D[t][r] : 0.f;
+    store_rho<5>(a.dz2 + row, D, h);
+    zero_tiles(E);
+    tchain_acc<5, 5, 12, kLdE>(D, E, a.rm1t, lane);
+    load_rho<5>(a.z1 + row, Z, h);
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) E[t][r] = Z[t][r] > 0.f ? E[t][r] : 0.f;
+    store_rho<5>(a.dz1 + row, E, h);
+}
+
+__global__ __launch_bounds__(256, 2) void k_enc_node_bwd(EncNodeBwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nb * 32 >= a.n_nodes) return;
+    const int n = nb * 32 + j;
+    const bool valid = n < a.n_nodes;
+    const int64_t nc = valid ? n : a.n_nodes - 1;
+    f32x16 D[4], Z[4], E[4];
+    load_rho<4>(a.dco + nc * kLdN, D, h);
+    load_rho<4>(a.co + nc * kLdN, Z, h);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) D[t][r] = Z[t][r] > 0.f ? D[t][r] * a.scale : 0.f;
+    store_rho_masked<4>(a.dzo2 + (int64_t)n * kLdN, D, h, valid);
+    zero_tiles(E);
+    tchain_acc<4, 4, 4, kLdN>(D, E, a.om1t, lane);
+    load_rho<4>(a.zo1 + nc * kLdN, Z, h);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) E[t][r] = Z[t][r] > 0.f ? E[t][r] : 0.f;
+    store_rho_masked<4>(a.dzo1 + (int64_t)n * kLdN, E, h, valid);
+}
+
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
+    const int waves = (a.n_nodes + 31) / 32;
+    hipLaunchKernelGGL(k_node_bwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st) {
+    const size_t lds = edge_bwd_lds_per_wave(a.nw_max) * a.wpg;
+    hipLaunchKernelGGL(k_edge_bwd, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_enc_edge_bwd, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st) {
+    const int waves = (a.n_nodes + 31) / 32;
+    hipLaunchKernelGGL(k_enc_node_bwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace spw

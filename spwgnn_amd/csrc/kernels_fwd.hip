@@ -1,0 +1,394 @@
+// Forward kernels of the propagation network (Networks.py:121-186) for gfx950.
+//
+//   k_prep_weights   zero-padded / transposed / permuted copies of the 22 Keras tensors
+//   k_enc_node       om encoder (Networks.py:166,168) + P0 copy + first U/V projections
+//   k_enc_edge       rm encoder (Networks.py:165,167) + step-invariant part of rmp layer 1
+//   k_edge_fwd       per step: h1 = relu(A + U[s] + V[r]) → h2 = relu(h1·W2 + b2) → receiver
+//                    segment sum (Networks.py:174-178, with rmp layer 3 moved behind the sum)
+//   k_node_fwd       per step: rmp layer 3 on the summed messages, tanh, omp, state update,
+//                    readout, next-step U/V (Networks.py:178-186)
+#include "kernels.h"
+
+namespace spw {
+
+// ------------------------------------------------------------------------------------------------
+__global__ void k_prep_weights(PrepArgs a) {
+    const int id = blockIdx.y;
+    const PackDesc& d = a.desc[id];
+    const int total = d.rows * d.cols;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const int r = idx / d.cols, c = idx - r * d.cols;
+        int sa = d.transpose ? c : r;  // source row (before row0)
+        int sb = d.transpose ? r : c;  // source col (before perm)
+        float v = 0.f;
+        if (d.perm) sb = wo2_perm(sb);
+        if (sa >= 0 && sa < d.src_rows && sb >= 0 && sb < d.src_cols)
+            v = a.params[d.src_off + (int64_t)(sa + d.src_row0) * d.src_ld + sb];
+        a.pk[d.dst_off + idx] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// om encoder: c_o = dropout(relu(om(y, w))), P0, U0 = P0·W1b, V0 = P0·W1c (transposed orientation,
+// 32 nodes per wave).
+__global__ __launch_bounds__(256, 2) void k_enc_node(EncNodeArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int n = nb * 32 + j;
+    if (nb * 32 >= a.n_nodes) return;
+    const bool valid = n < a.n_nodes;
+    const int nc = valid ? n : a.n_nodes - 1;
+    const float4 p = reinterpret_cast<const float4*>(a.pos)[nc];
+    const float o0 = p.y, o1 = p.z;  // Networks.py:155-161: (y, width)
+
+    f32x16 Z[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * t;
+            Z[t][r] = relu(o0 * a.w_om0[f] + o1 * a.w_om0[128 + f] + a.b_om0[f]);
+        }
+    if (a.zo1) store_rho_masked<4>(a.zo1 + (int64_t)n * kLdN, Z, h, valid);
+
+    f32x16 C[4];
+    zero_tiles(C);
+    tchain_acc<4, 4, 4, kLdN>(Z, C, a.w_om1, lane);
+    bias_act_rho<4, true>(C, a.b_om1, h);  // relu(om(.)) — Networks.py:166
+    if (a.dropout_on) {                    // Networks.py:168
+        const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                C[t][r] = drop_keep(key, (uint32_t)f, a.thresh) ? C[t][r] * a.scale : 0.f;
+            }
+    }
+    store_rho_masked<4>(a.co + (int64_t)n * kLdN, C, h, valid);
+
+    // P0: the 'propagation' input (Networks.py:119,169), ld 100 → workspace ld 128
+    f32x16 P[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.prop && f0 < kFN && valid) v = *reinterpret_cast<const float4*>(a.prop + (int64_t)n * kFN + f0);
+            P[t][4 * q] = v.x;
+            P[t][4 * q + 1] = v.y;
+            P[t][4 * q + 2] = v.z;
+            P[t][4 * q + 3] = v.w;
+        }
+    store_rho_masked<4>(a.P0 + (int64_t)n * kLdN, P, h, valid);
+
+    f32x16 U[5];
+    zero_tiles(U);
+    tchain_acc<5, 4, 4, kLdE>(P, U, a.w1b, lane);
+    store_rho_masked<5>(a.U0 + (int64_t)n * kLdE, U, h, valid);
+    zero_tiles(U);
+    tchain_acc<5, 4, 4, kLdE>(P, U, a.w1c, lane);
+    store_rho_masked<5>(a.V0 + (int64_t)n * kLdE, U, h, valid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// rm encoder (transposed orientation, one 32-edge block per wave): d = pos[r]-pos[s] (2 feats)
+// → 150 → 150 → 150 → 150 (+relu, dropout) = c_r; A = c_r·W1a + b1 (step-invariant first-layer
+// term of rmp: W1·[c_r|P_s|P_r] = (c_r·W1a + b1) + P_s·W1b + P_r·W1c).
+__global__ __launch_bounds__(256, 2) void k_enc_edge(EncEdgeArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blk >= a.n_eblocks) return;
+    const int64_t e = (int64_t)blk * 32 + j;
+    const int s = a.esrc[e], d = a.edst[e];
+    const bool valid = s >= 0;
+    float dx = 0.f, dy = 0.f;
+    if (valid) {
+        const float4 ps = reinterpret_cast<const float4*>(a.pos)[s];
+        const float4 pd = reinterpret_cast<const float4*>(a.pos)[d];
+        dx = pd.x - ps.x;  // Networks.py:148-152 (receiver − sender), (x, y)
+        dy = pd.y - ps.y;
+    }
+    f32x16 X[5], Y[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * t;
+            X[t][r] = relu(dx * a.w_rm0[f] + dy * a.w_rm0[160 + f] + a.b_rm0[f]);
+        }
+    float* zrow = nullptr;
+    if (a.z1) store_rho_masked<5>(a.z1 + e * kLdE, X, h, valid);
+    zero_tiles(Y);
+    tchain_acc<5, 5, 12, kLdE>(X, Y, a.w_rm1, lane);
+    bias_act_rho<5, true>(Y, a.b_rm1, h);
+    if (a.z2) store_rho_masked<5>(a.z2 + e * kLdE, Y, h, valid);
+    zero_tiles(X);
+    tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_rm2, lane);
+    bias_act_rho<5, true>(X, a.b_rm2, h);
+    if (a.z3) store_rho_masked<5>(a.z3 + e * kLdE, X, h, valid);
+    zero_tiles(Y);
+    tchain_acc<5, 5, 12, kLdE>(X, Y, a.w_rm3, lane);
+    bias_act_rho<5, true>(Y, a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:165
+    if (a.dropout_on && valid) {           // Networks.py:167
+        const uint32_t tw = (uint32_t)a.node_tower[s];
+        const uint32_t key = drop_row_key(a.seed, 1u, tw, (uint32_t)a.node_local[s], (uint32_t)a.node_local[d]);
+#pragma unroll
+        for (int t = 0; t < 5; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                Y[t][r] = drop_keep(key, (uint32_t)f, a.thresh) ? Y[t][r] * a.scale : 0.f;
+            }
+    }
+    if (a.cr) store_rho_masked<5>(a.cr + e * kLdE, Y, h, valid);
+    zero_tiles(X);
+    tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_w1a, lane);
+    bias_act_rho<5, false>(X, a.b_w1a, h);
+    store_rho_masked<5>(a.A + e * kLdE, X, h, valid);
+    (void)zrow;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Segment sum of a C-layout tile pair through a per-wave LDS stage (deterministic: each node's
+// edges are summed in csr order, blocks in order). st: [2][32][33]; csrw = this lane's word of
+// the block's 128-byte csr; word_base 0 = receiver tables, 16 = sender tables.
+template <int WORD_BASE>
+__device__ __forceinline__ void segsum_walk(const float* st, float* nacc, uint32_t csrw, int t, bool tv, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    float sum = 0.f;
+#pragma unroll 1
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + (k >> 2));
+        const int nd = (nw >> (8 * (k & 3))) & 255;
+        if (nd == 255) break;
+        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
+        const int eo = (ow >> (8 * (k & 3))) & 255;
+        sum += st[h * 1056 + eo * 33 + i];
+        int ndn = 255;
+        if (k < 31) {
+            const uint32_t nw2 = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + ((k + 1) >> 2));
+            ndn = (nw2 >> (8 * ((k + 1) & 3))) & 255;
+        }
+        if (ndn != nd) {
+            if (tv) nacc[nd * kLdE + 32 * t + i] += sum;
+            sum = 0.f;
+        }
+    }
+}
+
+__device__ __forceinline__ void stage_pair(float* st, const f32x16 (&acc)[5], int t0, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int slot = 0; slot < 2; ++slot) {
+        const int t = t0 + slot;
+        if (t >= 5) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = acc[t][r];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// One propagation step, edge side (natural orientation, one wave-tile of whole towers per wave).
+__global__ __launch_bounds__(256, 2) void k_edge_fwd(EdgeFwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int wave = threadIdx.x >> 6;
+    const int wt = blockIdx.x * a.wpg + wave;
+    if (wt >= a.n_wtiles) return;
+    float* st = smem + wave * (2112 + a.nw_max * kLdE);
+    float* nacc = st + 2112;
+    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    for (int idx = lane; idx < nn * kLdE; idx += 64) nacc[idx] = 0.f;
+
+    for (int bb = 0; bb < nb; ++bb) {
+        const int blk = fb + bb;
+        const int64_t e = (int64_t)blk * 32 + i;
+        const int s = a.esrc[e], d = a.edst[e];
+        const bool valid = s >= 0;
+        const int sc = valid ? s : n0, dc = valid ? d : n0;
+        // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:174-177), lane = edge, split
+        // halves, streamed 4 features at a time straight into h2 = h1·W2 (rmp layer 2).
+        const uint64_t vmask = __ballot(valid);
+        const float4* A4 = reinterpret_cast<const float4*>(a.A + e * kLdE + kKhE * h);
+        const float4* U4 = reinterpret_cast<const float4*>(a.U + (int64_t)sc * kLdE + kKhE * h);
+        const float4* V4 = reinterpret_cast<const float4*>(a.V + (int64_t)dc * kLdE + kKhE * h);
+        uint32_t* m1row = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
+        f32x16 acc[5];
+        zero_tiles(acc);
+        float4 pa = A4[0], pu = U4[0], pv = V4[0];
+        const float* wbase = a.w2 + (kKhE * h) * kLdE + i;
+#pragma unroll 1
+        for (int q = 0; q < kKhE / 4; ++q) {
+            const float4 ca = pa, cu = pu, cv = pv;
+            if (q + 1 < kKhE / 4) {
+                pa = A4[q + 1];
+                pu = U4[q + 1];
+                pv = V4[q + 1];
+            }
+            float xv[4];
+            xv[0] = valid ? relu(ca.x + cu.x + cv.x) : 0.f;
+            xv[1] = valid ? relu(ca.y + cu.y + cv.y) : 0.f;
+            xv[2] = valid ? relu(ca.z + cu.z + cv.z) : 0.f;
+            xv[3] = valid ? relu(ca.w + cu.w + cv.w) : 0.f;
+            if (m1row) {  // h1 > 0 bits: word per (block, feature), bit = edge
+                uint32_t word = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint64_t bal = __ballot(xv[c] > 0.f);
+                    if (lane == c) word = (uint32_t)bal;
+                    if (lane == 4 + c) word = (uint32_t)(bal >> 32);
+                }
+                if (lane < 8) m1row[(lane < 4 ? 4 * q + lane : kKhE + 4 * q + lane - 4)] = word;
+            }
+            const float* wrow = wbase + (4 * q) * kLdE;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wrow[c * kLdE + 32 * t], acc[t]);
+        }
+        if (m1row && lane < 8) m1row[152 + lane] = 0u;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const float b = a.b2[32 * t + i];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = relu(acc[t][r] + b);
+                if (t == 4 && i == kDegCol - 128) v = 1.f;  // degree column (multiplies b3)
+                const bool rv = (vmask >> (rho(r, 0) + 4 * h)) & 1;
+                acc[t][r] = rv ? v : 0.f;
+            }
+        }
+        if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
+            uint32_t* m2row = a.mask2 + (int64_t)blk * 160;
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint64_t bal = __ballot(acc[t][r] > 0.f);
+                    if (lane == rho(r, 0)) word = (uint32_t)bal;
+                    if (lane == rho(r, 1)) word = (uint32_t)(bal >> 32);
+                }
+                if (lane < 32) m2row[t * 32 + lane] = word;
+            }
+        }
+        // receiver segment sum (Networks.py:178 dot(receiver_relations, x)) into LDS node rows
+        const uint32_t csrw = a.csr[(int64_t)blk * 32 + i];
+#pragma unroll
+        for (int rd = 0; rd < 3; ++rd) {
+            stage_pair(st, acc, 2 * rd, lane);
+            wave_lds_sync();
+            const int t = 2 * rd + h;
+            segsum_walk<0>(st, nacc, csrw, t, t < 5, lane);
+            wave_lds_sync();
+        }
+    }
+    // write the wave-tile's node rows (each node is owned by exactly one wave-tile)
+    float* out = a.H2s + (int64_t)n0 * kLdE;
+    for (int idx = lane; idx < nn * kLdE; idx += 64) out[idx] = nacc[idx];
+}
+
+// ------------------------------------------------------------------------------------------------
+// One propagation step, node side (transposed orientation, 32 nodes per wave).
+//   a  = tanh([H2s | deg]·[W3; b3])              (Networks.py:178, layer 3 after the sum)
+//   o1 = relu([c_o | a | P]·Wo1 + bo1)            (Networks.py:179-180, omp layer 1)
+//   x' = o1·Wo2' + bo2'   (x' = x with the logit moved to column 100)
+//   P' = tanh(x'[0:100] + P); logit = x'[100]     (Networks.py:181, 184)
+//   U' = P'·W1b, V' = P'·W1c for the next step
+__global__ __launch_bounds__(256, 2) void k_node_fwd(NodeFwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nb * 32 >= a.n_nodes) return;
+    const int n = nb * 32 + j;
+    const bool valid = n < a.n_nodes;
+    const int64_t nc = valid ? n : a.n_nodes - 1;
+
+    f32x16 E[4];
+    zero_tiles(E);
+    {
+        float xb[kKhE];
+        load_half<kKhE>(a.H2s + nc * kLdE + kKhE * h, xb);
+        tgemm_half_acc<4, kKhE, kLdN>(xb, E, a.w3a, lane);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * t;
+            E[t][r] = f < kFN ? tanhf(E[t][r]) : 0.f;
+        }
+    if (a.a_out) store_rho_masked<4>(a.a_out + (int64_t)n * kLdN, E, h, valid);
+
+    f32x16 O[4];
+    zero_tiles(O);
+    {
+        float xb[kKhN];
+        load_half<kKhN>(a.co + nc * kLdN + kKhN * h, xb);
+        tgemm_half_acc<4, kKhN, kLdN>(xb, O, a.wo1c, lane);
+    }
+    tchain_acc<4, 4, 4, kLdN>(E, O, a.wo1a, lane);
+    {
+        float xb[kKhN];
+        load_half<kKhN>(a.P + nc * kLdN + kKhN * h, xb);
+        tgemm_half_acc<4, kKhN, kLdN>(xb, O, a.wo1p, lane);
+    }
+    bias_act_rho<4, true>(O, a.bo1, h);
+    if (a.o1_out) store_rho_masked<4>(a.o1_out + (int64_t)n * kLdN, O, h, valid);
+
+    f32x16 X[4];
+    zero_tiles(X);
+    tchain_acc<4, 4, 4, kLdN>(O, X, a.wo2, lane);
+    bias_act_rho<4, false>(X, a.bo2p, h);
+    {
+        f32x16 P[4];
+        load_rho<4>(a.P + nc * kLdN, P, h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                E[t][r] = f < kFN ? tanhf(X[t][r] + P[t][r]) : 0.f;  // E := P'
+            }
+    }
+    if (a.logits && h == 1 && valid) a.logits[n] = X[3][0];  // x' row 100 = rho(0,1) + 96
+    store_rho_masked<4>(a.Pn + (int64_t)n * kLdN, E, h, valid);
+    if (a.U) {
+        f32x16 U[5];
+        zero_tiles(U);
+        tchain_acc<5, 4, 4, kLdE>(E, U, a.w1b, lane);
+        store_rho_masked<5>(a.U + (int64_t)n * kLdE, U, h, valid);
+        zero_tiles(U);
+        tchain_acc<5, 4, 4, kLdE>(E, U, a.w1c, lane);
+        store_rho_masked<5>(a.V + (int64_t)n * kLdE, U, h, valid);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_prep_weights, dim3(32, PK_COUNT), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st) {
+    const int waves = (a.n_nodes + 31) / 32;
+    hipLaunchKernelGGL(k_enc_node, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_enc_edge, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st) {
+    const size_t lds = edge_fwd_lds_per_wave(a.nw_max) * a.wpg;
+    hipLaunchKernelGGL(k_edge_fwd, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st) {
+    const int waves = (a.n_nodes + 31) / 32;
+    hipLaunchKernelGGL(k_node_fwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace spw

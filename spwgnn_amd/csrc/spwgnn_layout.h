@@ -1,0 +1,40 @@
+// Shared host/device constants and the parameter table of libspwgnn_hip.
+#pragma once
+#include <cstdint>
+#include <cstdio>
+
+namespace spw {
+
+// ---- model widths (Networks.py:119,136-140) ----
+constexpr int kFE = 150;    // relation widths (rm hidden/out, rmp hidden)
+constexpr int kFN = 100;    // object / state widths (om, effect, P, omp hidden)
+constexpr int kLdE = 160;   // row stride (floats) of every 150/151-wide array  (5 MFMA tiles of 32)
+constexpr int kLdN = 128;   // row stride (floats) of every 100/101-wide array  (4 MFMA tiles of 32)
+constexpr int kKhE = 76;    // split-halves contraction: features [76h, 76h+76), h = lane/32 (152 = 150 + 2 zero)
+constexpr int kKhN = 52;    // split-halves contraction for 100-wide inputs (104 = 100 + 4 zero)
+constexpr int kNwMaxLimit = 32;   // max nodes per wave-tile (LDS node accumulators)
+constexpr int kDegCol = 150;      // H2s column 150 holds the in-degree (multiplies the rmp.2 bias)
+
+constexpr int kNumTensors = 22;
+
+struct TensorDesc {
+    const char* name;
+    int64_t offset;
+    int32_t rows, cols;
+};
+struct ParamTable {
+    TensorDesc t[kNumTensors];
+    int64_t total;  // padded
+    int64_t real;
+};
+const ParamTable& param_table();
+
+// Tensor indices in the flat buffer (order of param_table: rm.0..3, om.0..1, rmp.0..2, omp.0..1; kernel, bias)
+enum TensorId : int {
+    T_RM0K = 0, T_RM0B, T_RM1K, T_RM1B, T_RM2K, T_RM2B, T_RM3K, T_RM3B,
+    T_OM0K, T_OM0B, T_OM1K, T_OM1B,
+    T_RMP0K, T_RMP0B, T_RMP1K, T_RMP1B, T_RMP2K, T_RMP2B,
+    T_OMP0K, T_OMP0B, T_OMP1K, T_OMP1B,
+};
+
+}  // namespace spw

@@ -1,0 +1,137 @@
+"""Input builders: synthetic Jenga towers, relation matrices, stability labels, JSON trajectories.
+
+Mirrors the reference's data producers and driver preprocessing (no physics):
+  * tower geometry ........ src/JengaBuilder.py:50-61 (constants), :137-192 (create_world),
+                            :223-233 (remove_object) — positions of the first recorded frame
+  * relation matrices ..... src/main.py:66-81 (raw-pixel distance < 170, sender-major slots) and
+                            src/JengaBuilder.py:309-326 (normalised coords vs 170 → fully connected)
+  * stability labels ...... src/main.py:8-23 (Σ‖Δpos‖ over frames < 0.5 px ⇒ stable)
+  * trajectories on disk .. src/JengaBuilder.py:128-135, :366-371 (JSON [traj][obj][frame][x,y,w]),
+                            src/main.py:39-63 (load, drop empty, pad frames with the last frame)
+  * normalisation ......... src/main.py:91 (boxes / 170)
+"""
+from __future__ import annotations
+
+import json
+import random
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+RELATION_THRESHOLD = 170.0        # main.py:71
+# JengaBuilder.py:50-61
+BOTTOM_EDGE = 70
+LEFT_MOST = 400
+RIGHT_MOST = 1500 - 400
+RECT_HEIGHT = 80
+RECT_WIDTH_MIN = 50
+RECT_WIDTH_RANGE = 250
+RECT_WIDTH_AVERAGE = (RECT_WIDTH_MIN + RECT_WIDTH_RANGE) / 2
+MAX_SPACE_RECTS = 50
+
+
+def jenga_tower(n: int, rng: random.Random) -> np.ndarray:
+    """One tower of n boxes [x, y, w] in pixels, laid out like JengaBuilder.create_world."""
+    boxes: List[List[Tuple[float, float, float]]] = []
+    layer = -1
+    while n > 0:
+        layer += 1
+        boxes.append([])
+        if layer == 0:
+            right_edge, left_edge = RIGHT_MOST, LEFT_MOST
+        else:
+            xs = [b[0] for b in boxes[layer - 1]]
+            right_edge, left_edge = max(xs), min(xs)
+        y = BOTTOM_EDGE + RECT_HEIGHT / 2 + RECT_HEIGHT * layer
+        if right_edge == left_edge:  # previous layer holds one box (JengaBuilder.py:159-167)
+            x = rng.randint(int(left_edge - RECT_WIDTH_MIN / 2), int(left_edge + RECT_WIDTH_MIN / 2))
+            w = rng.randint(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE)
+            boxes[layer].append((float(x), BOTTOM_EDGE + int(RECT_HEIGHT / 2) + RECT_HEIGHT * layer, float(w)))
+            n -= 1
+            continue
+        left_edge -= (layer > 0) * int(RECT_WIDTH_AVERAGE / 2)   # :172
+        w = rng.randint(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE)
+        left_edge += w
+        while left_edge - w / 2 < right_edge and n > 0:          # :175-185
+            boxes[layer].append((left_edge - w / 2, y, float(w)))
+            n -= 1
+            left_edge += rng.randint(0, MAX_SPACE_RECTS)
+            w = rng.randint(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE)
+            left_edge += w
+    return np.array([b for layer_boxes in boxes for b in layer_boxes], dtype=np.float64)
+
+
+def synthetic_towers(n_towers: int, n_objects: int, seed: int = 0, remove_one: bool = True) -> np.ndarray:
+    """(B, N, 3) raw-pixel [x, y, w]: build N+1 boxes and remove one at random (the Jenga
+    trajectory records the tower after remove_object, JengaBuilder.py:223-233)."""
+    rng = random.Random(seed)
+    out = np.zeros((n_towers, n_objects, 3))
+    for b in range(n_towers):
+        t = jenga_tower(n_objects + (1 if remove_one else 0), rng)
+        if remove_one:
+            t = np.delete(t, rng.randint(0, len(t) - 1), axis=0)
+        out[b] = t
+    return out
+
+
+def relation_matrices(boxes_raw: np.ndarray, threshold: Optional[float] = RELATION_THRESHOLD):
+    """Dense sender/receiver one-hot matrices (B, N, E), E = N(N-1), exactly as main.py:66-81
+    (threshold on raw-pixel frame-0 distance) — vectorised over towers and slots.
+    threshold=None → fully connected (the inference path of JengaBuilder.py:309-326)."""
+    B, N = boxes_raw.shape[:2]
+    m_idx, j_idx = np.nonzero(~np.eye(N, dtype=bool))          # sender-major slot order
+    E = len(m_idx)
+    if threshold is None:
+        active = np.ones((B, E), dtype=bool)
+    else:
+        d = np.linalg.norm(boxes_raw[:, m_idx, 0:2] - boxes_raw[:, j_idx, 0:2], axis=2)
+        active = d < threshold
+    Rs = np.zeros((B, N, E), dtype=np.float32)
+    Rr = np.zeros((B, N, E), dtype=np.float32)
+    bb, kk = np.nonzero(active)
+    Rs[bb, m_idx[kk], kk] = 1.0
+    Rr[bb, j_idx[kk], kk] = 1.0
+    return Rs, Rr
+
+
+def calculate_stability(boxes: np.ndarray, threshold: float = 0.5) -> np.ndarray:
+    """main.py:8-23: boxes (T, F, N, >=2) → y (T, N, 1); stable iff Σ_f ‖pos_f − pos_{f+1}‖ < 0.5."""
+    step = np.linalg.norm(boxes[:, 1:, :, 0:2] - boxes[:, :-1, :, 0:2], axis=3)   # (T, F-1, N)
+    return (step.sum(axis=1) < threshold).astype(np.float64)[..., None]
+
+
+def load_trajectories(path: str, n_objects: int, object_dim: int = 3) -> np.ndarray:
+    """main.py:39-63: JSON [traj][obj][frame][x,y,(w)] → (T, F, N, object_dim), frames padded
+    with each object's last frame; empty trajectories dropped."""
+    with open(path) as f:
+        data = json.load(f)
+    data = [d for d in data if len(d) != 0]
+    n_frame = max(len(t[0]) for t in data)
+    boxes = np.zeros((len(data), n_frame, n_objects, object_dim))
+    for t, traj in enumerate(data):
+        for o in range(n_objects):
+            fr = np.asarray(traj[o], dtype=np.float64)[:, :object_dim]
+            boxes[t, :len(fr), o] = fr
+            boxes[t, len(fr):, o] = fr[-1]
+    return boxes
+
+
+def training_arrays(boxes: np.ndarray, threshold: float = RELATION_THRESHOLD):
+    """The dicts main.py:92-93 passes to fit: relations from raw frame 0, then /170."""
+    Rs, Rr = relation_matrices(boxes[:, 0], threshold)
+    y = calculate_stability(boxes)
+    objects = (boxes[:, 0] / RELATION_THRESHOLD).astype(np.float32)
+    prop = np.zeros(objects.shape[:2] + (100,), np.float32)
+    return ({"objects": objects, "sender_relations": Rs, "receiver_relations": Rr, "propagation": prop},
+            {"target": y.astype(np.float32)})
+
+
+def synthetic_batch(n_towers: int, n_objects: int, seed: int = 0, fully_connected: bool = True):
+    """Synthetic (objects /170, Rs, Rr, prop, target) for benchmarks: Jenga geometry, Bernoulli labels."""
+    raw = synthetic_towers(n_towers, n_objects, seed)
+    Rs, Rr = relation_matrices(raw, None if fully_connected else RELATION_THRESHOLD)
+    rng = np.random.default_rng(seed + 1)
+    target = rng.integers(0, 2, size=(n_towers, n_objects)).astype(np.float32)
+    objects = (raw / RELATION_THRESHOLD).astype(np.float32)
+    prop = np.zeros((n_towers, n_objects, 100), np.float32)
+    return objects, Rs, Rr, prop, target

@@ -1,0 +1,133 @@
+"""Thin host wrapper over the C-ABI: workspace management and the per-call entry points.
+
+torch provides device memory (caching allocator) and the current HIP stream; every byte of
+arithmetic happens in libspwgnn_hip.so. Nothing here falls back to CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib, params as P
+from .batch import TowerBatch
+
+REF_MP_STEPS = 5       # Networks.py:173
+REF_DROPOUT = 0.1      # Networks.py:167-168
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_gpu(t: torch.Tensor, what: str):
+    if t.device.type != "cuda":
+        raise _lib.SpwgnnError(f"{what} must be a HIP device tensor (got {t.device}); the HIP path has no CPU fallback")
+
+
+@dataclass
+class RunConfig:
+    mp_steps: int = REF_MP_STEPS
+    training: bool = False
+    dropout: float = 0.0
+    seed: int = 0
+
+    def cstruct(self) -> _lib.RunC:
+        r = _lib.RunC()
+        r.mp_steps = int(self.mp_steps)
+        r.training = 1 if self.training else 0
+        r.dropout = float(self.dropout)
+        r.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        return r
+
+
+class Workspace:
+    """Device scratch for one forward (+ its backward). Sized by spwgnn_workspace_bytes."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = None
+            self.buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+def workspace_bytes(batch: TowerBatch, run: RunConfig) -> int:
+    n = int(_lib.lib().spwgnn_workspace_bytes(batch.n_nodes, batch.n_eblocks, run.mp_steps, 1 if run.training else 0))
+    if n < 0:
+        raise _lib.SpwgnnError("invalid batch shape for workspace")
+    return n
+
+
+def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Workspace,
+            logits: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _require_gpu(flat_params, "params")
+    if flat_params.dtype != torch.float32 or not flat_params.is_contiguous() or flat_params.numel() != P.flat_size():
+        raise ValueError("params must be a contiguous fp32 flat buffer of spwgnn_param_count() floats")
+    nbytes = workspace_bytes(batch, run)
+    buf = ws.get(nbytes)
+    if logits is None:
+        logits = torch.empty(batch.n_nodes, dtype=torch.float32, device=batch.device)
+    b = batch.cstruct()
+    r = run.cstruct()
+    st = _lib.lib().spwgnn_forward(flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(),
+                                   logits.data_ptr(), _stream(batch.device))
+    _lib.check(st, "spwgnn_forward")
+    return logits
+
+
+def backward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Workspace, dlogits: torch.Tensor,
+             grads: Optional[torch.Tensor] = None, want_dprop: bool = False):
+    if not run.training:
+        raise _lib.SpwgnnError("backward needs a training forward on the same workspace")
+    dlogits = dlogits.contiguous().to(torch.float32)
+    _require_gpu(dlogits, "dlogits")
+    if grads is None:
+        grads = torch.empty_like(flat_params)
+    dprop = torch.empty(batch.n_nodes, 100, dtype=torch.float32, device=batch.device) if want_dprop else None
+    b = batch.cstruct()
+    r = run.cstruct()
+    buf = ws.buf
+    st = _lib.lib().spwgnn_backward(flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(),
+                                    dlogits.data_ptr(), grads.data_ptr(), dprop.data_ptr() if dprop is not None else None,
+                                    _stream(batch.device))
+    _lib.check(st, "spwgnn_backward")
+    return grads, dprop
+
+
+class BceScratch:
+    def __init__(self, device):
+        n = int(_lib.lib().spwgnn_bce_scratch_bytes(1))
+        self.scratch = torch.empty(n, dtype=torch.uint8, device=device)
+        self.out3 = torch.empty(3, dtype=torch.float32, device=device)
+
+
+def bce(logits: torch.Tensor, targets: torch.Tensor, scratch: BceScratch, dlogits: Optional[torch.Tensor] = None):
+    """Keras binary_crossentropy (+ binary_accuracy numerator) and d loss / d logit on device.
+    Returns out3 = [loss, n_correct, n] (device) and dlogits."""
+    targets = targets.reshape(-1).to(torch.float32).contiguous()
+    if dlogits is None:
+        dlogits = torch.empty_like(logits)
+    st = _lib.lib().spwgnn_bce(logits.data_ptr(), targets.data_ptr(), logits.numel(), scratch.out3.data_ptr(),
+                               dlogits.data_ptr(), scratch.scratch.data_ptr(), _stream(logits.device))
+    _lib.check(st, "spwgnn_bce")
+    return scratch.out3, dlogits
+
+
+def adam(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr=5e-4,
+         beta1=0.9, beta2=0.999, eps=1e-7, l2=0.0, grad_scale=1.0):
+    st = _lib.lib().spwgnn_adam(params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), params.numel(),
+                                int(step), lr, beta1, beta2, eps, l2, grad_scale, _stream(params.device))
+    _lib.check(st, "spwgnn_adam")
+
+
+def sigmoid(logits: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(logits)
+    st = _lib.lib().spwgnn_sigmoid(logits.data_ptr(), out.data_ptr(), logits.numel(), _stream(logits.device))
+    _lib.check(st, "spwgnn_sigmoid")
+    return out

@@ -1,0 +1,193 @@
+"""Keras-shaped front end: PropagationNetwork.getModel(...) → model.fit / model.predict.
+
+Mirrors the reference call sites one-to-one so a driver written against the reference drops in:
+  * PropagationNetwork().getModel(n_objects, object_dim=3, relation_dim=1)  — Networks.py:102-194
+    (one model per n_objects, cached; all models share rm/om/rmp/omp weights, :107-108, :130-146)
+  * model.fit(x_dict, {'target': y}, batch_size=32, epochs=10, validation_split=0.2, shuffle=True,
+    verbose=1)                                                            — main.py:92-98
+  * model.predict(x_dict) → (B, N, 1) probabilities                       — JengaBuilder.py:328-329
+Compile semantics (Networks.py:191-192): Adam(lr=5e-4, decay=0) per model, binary_crossentropy,
+binary_accuracy. Every step runs through libspwgnn_hip (forward, BCE, backward, Adam).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import engine as E
+from . import params as P
+from .batch import TowerBatch
+from .network import GraphNetwork
+
+
+class CompactDataset:
+    """Host-side compact copy of a dense dataset: per-tower node rows and active edges."""
+
+    def __init__(self, objects, Rs, Rr, propagation=None):
+        objects = np.asarray(objects, np.float32)
+        self.B, self.N = objects.shape[:2]
+        full = TowerBatch.from_dense(objects[:1], np.asarray(Rs)[:1], np.asarray(Rr)[:1], device="cpu")  # validates layout
+        del full
+        # one C++ conversion for the whole set
+        import ctypes as C
+        from . import _lib
+        Rs = np.ascontiguousarray(Rs, np.float32)
+        Rr = np.ascontiguousarray(Rr, np.float32)
+        E_ = self.N * (self.N - 1)
+        cap = self.B * E_
+        src = np.zeros(max(cap, 1), np.int32)
+        dst = np.zeros(max(cap, 1), np.int32)
+        tec = np.zeros(self.B, np.int32)
+        ne = C.c_int64(0)
+        _lib.check(_lib.lib().spwgnn_dense_to_edges(Rs.ctypes.data, Rr.ctypes.data, self.B, self.N, src.ctypes.data,
+                                                    dst.ctypes.data, None, cap, C.byref(ne), tec.ctypes.data),
+                   "dense_to_edges")
+        n = int(ne.value)
+        self.objects = objects
+        self.src = src[:n] - np.repeat(np.arange(self.B, dtype=np.int32) * self.N, tec)   # tower-local
+        self.dst = dst[:n] - np.repeat(np.arange(self.B, dtype=np.int32) * self.N, tec)
+        self.edge_off = np.concatenate([[0], np.cumsum(tec)]).astype(np.int64)
+        self.tower_edges = tec
+        self.prop = None if propagation is None or not np.any(np.asarray(propagation)) else \
+            np.asarray(propagation, np.float32)
+
+    def subset(self, idx: np.ndarray, device) -> TowerBatch:
+        idx = np.asarray(idx)
+        n = len(idx)
+        pieces_s, pieces_d = [], []
+        for k, b in enumerate(idx):
+            e0, e1 = self.edge_off[b], self.edge_off[b + 1]
+            pieces_s.append(self.src[e0:e1] + k * self.N)
+            pieces_d.append(self.dst[e0:e1] + k * self.N)
+        src = np.concatenate(pieces_s) if pieces_s else np.zeros(0, np.int32)
+        dst = np.concatenate(pieces_d) if pieces_d else np.zeros(0, np.int32)
+        prop = None if self.prop is None else self.prop[idx].reshape(n * self.N, 100)
+        return TowerBatch.from_edges(self.objects[idx].reshape(n * self.N, 3), np.full(n, self.N, np.int32), src, dst,
+                                     self.tower_edges[idx], prop, device, node_shape=(n, self.N))
+
+
+class KerasModel:
+    """One compiled per-N model of the reference (Networks.py:189-194); weights shared via ``net``."""
+
+    def __init__(self, net: GraphNetwork, n_objects: int, object_dim: int = 3, lr: float = 5e-4,
+                 l2: float = 0.0):
+        if object_dim != 3:
+            # Networks.py:160-163 + main.py:28-31/59-63: the object_dim=2 path of the reference is
+            # broken (om gets 1 feature, boxes[...,2] is out of range); only the Jenga layout runs.
+            raise ValueError("only object_dim=3 ([x, y, width]) is supported, as in the working reference path")
+        self.net = net
+        self.n_objects = n_objects
+        self.lr, self.l2 = lr, l2
+        self.beta1, self.beta2, self.eps = 0.9, 0.999, 1e-7
+        dev = net.device
+        self.m = torch.zeros_like(net.flat.data)
+        self.v = torch.zeros_like(net.flat.data)
+        self.iterations = 0
+        self._ws = E.Workspace(dev)
+        self._bce = E.BceScratch(dev)
+        self._grads = torch.empty_like(net.flat.data)
+        self.history: Dict[str, List[float]] = {}
+
+    # ---------------------------------------------------------------- inference
+    def predict(self, x: Dict[str, np.ndarray], batch_size: int = 32768) -> np.ndarray:
+        objects = np.asarray(x["objects"], np.float32)
+        B, N = objects.shape[:2]
+        out = np.zeros((B, N, 1), np.float32)
+        run = E.RunConfig(self.net.mp_steps, training=False)
+        for b0 in range(0, B, batch_size):
+            sl = slice(b0, min(B, b0 + batch_size))
+            prop = x.get("propagation")
+            batch = TowerBatch.from_dense(objects[sl], np.asarray(x["sender_relations"])[sl],
+                                          np.asarray(x["receiver_relations"])[sl],
+                                          None if prop is None else np.asarray(prop)[sl], device=self.net.device)
+            with torch.no_grad():
+                z = E.forward(self.net.flat.detach(), batch, run, self._ws)
+                p = E.sigmoid(z)
+            out[sl, :, 0] = p.reshape(-1, N).cpu().numpy()
+        return out
+
+    # ---------------------------------------------------------------- training
+    def train_on_batch(self, batch: TowerBatch, target: torch.Tensor):
+        """One Keras step: forward (dropout on), BCE, backward, Adam. Returns (loss, accuracy) tensors."""
+        net = self.net
+        net._step_seed += 1
+        run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed=net._step_seed)
+        z = E.forward(net.flat.data, batch, run, self._ws)
+        out3, dz = E.bce(z, target, self._bce)
+        E.backward(net.flat.data, batch, run, self._ws, dz, grads=self._grads)
+        self.iterations += 1
+        E.adam(net.flat.data, self._grads, self.m, self.v, self.iterations, self.lr, self.beta1, self.beta2,
+               self.eps, self.l2)
+        return out3
+
+    def evaluate_batch(self, batch: TowerBatch, target: torch.Tensor):
+        run = E.RunConfig(self.net.mp_steps, training=False)
+        z = E.forward(self.net.flat.data, batch, run, self._ws)
+        out3, _ = E.bce(z, target, self._bce)
+        return out3
+
+    def fit(self, x: Dict[str, np.ndarray], y: Dict[str, np.ndarray], batch_size: int = 32, epochs: int = 10,
+            validation_split: float = 0.0, shuffle: bool = True, verbose: int = 1, seed: int = 0):
+        objects = np.asarray(x["objects"], np.float32)
+        target = np.asarray(y["target"], np.float32).reshape(objects.shape[0], -1)
+        B = objects.shape[0]
+        # Keras: validation = the LAST fraction of the samples, taken before shuffling
+        n_val = int(B * validation_split) if validation_split else 0
+        n_tr = B - n_val
+        ds = CompactDataset(objects, x["sender_relations"], x["receiver_relations"], x.get("propagation"))
+        rng = np.random.default_rng(seed)
+        dev = self.net.device
+        tgt = torch.as_tensor(target, device=dev)
+        hist = {"loss": [], "binary_accuracy": []}
+        if n_val:
+            hist.update({"val_loss": [], "val_binary_accuracy": []})
+            vbatch = ds.subset(np.arange(n_tr, B), dev)
+            vtgt = tgt[n_tr:].reshape(-1).contiguous()
+        for ep in range(epochs):
+            order = rng.permutation(n_tr) if shuffle else np.arange(n_tr)
+            tot_l = tot_c = tot_n = 0.0
+            for b0 in range(0, n_tr, batch_size):
+                idx = order[b0:b0 + batch_size]
+                batch = ds.subset(idx, dev)
+                o3 = self.train_on_batch(batch, tgt[torch.as_tensor(idx, device=dev)].reshape(-1).contiguous())
+                l, c, n = o3.tolist()
+                tot_l += l * len(idx)
+                tot_c += c
+                tot_n += n
+            hist["loss"].append(tot_l / max(n_tr, 1))
+            hist["binary_accuracy"].append(tot_c / max(tot_n, 1))
+            if n_val:
+                vl, vc, vn = self.evaluate_batch(vbatch, vtgt).tolist()
+                hist["val_loss"].append(vl)
+                hist["val_binary_accuracy"].append(vc / vn)
+            if verbose:
+                msg = f"Epoch {ep + 1}/{epochs} - loss: {hist['loss'][-1]:.4f} - binary_accuracy: {hist['binary_accuracy'][-1]:.4f}"
+                if n_val:
+                    msg += f" - val_loss: {hist['val_loss'][-1]:.4f} - val_binary_accuracy: {hist['val_binary_accuracy'][-1]:.4f}"
+                print(msg)
+        for k, v in hist.items():
+            self.history.setdefault(k, []).extend(v)
+        return hist
+
+
+class PropagationNetwork:
+    """Networks.py:102-194: getModel caches one compiled model per n_objects, all sharing the
+    weights of the first one built (set_weights / reuse_model, Networks.py:130-146)."""
+
+    def __init__(self, device="cuda", seed: int = 0, mp_steps: int = E.REF_MP_STEPS, dropout: float = E.REF_DROPOUT):
+        self.Nets: Dict[int, KerasModel] = {}
+        self.set_weights = False
+        self._net: Optional[GraphNetwork] = None
+        self._device, self._seed, self._mp, self._drop = device, seed, mp_steps, dropout
+
+    def getModel(self, n_objects: int, object_dim: int = 3, relation_dim: int = 1) -> KerasModel:  # noqa: N802
+        if n_objects in self.Nets:
+            return self.Nets[n_objects]
+        if not self.set_weights:
+            self._net = GraphNetwork(self._mp, self._drop, self._seed, device=self._device)
+            self.set_weights = True
+        model = KerasModel(self._net, n_objects, object_dim)
+        self.Nets[n_objects] = model
+        return model

@@ -1,0 +1,81 @@
+"""HIP path vs the CPU oracle (fp64) — the parity gate. Runs on an MI355X only (-m gpu).
+
+Tolerances (fp32 kernels vs fp64 oracle): logits |Δ| <= 1e-5 + 1e-5·|z| (north_star: "outputs match
+the CPU reference logits within 1e-5 fp32"); gradients |Δ| <= 1e-5·max|g| + 1e-7 per tensor.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model as O
+from spwgnn_amd import TowerBatch, data as D, engine as E, params as P
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_ATOL = 1e-5
+LOGIT_RTOL = 1e-5
+
+
+def _oracle_logits(params, obj, Rs, Rr, prop, S):
+    tp = O.to_torch(params)
+    z = O.forward_dense(tp, torch.tensor(obj, dtype=torch.float64), torch.tensor(Rs, dtype=torch.float64),
+                        torch.tensor(Rr, dtype=torch.float64), torch.tensor(prop, dtype=torch.float64), S)
+    return z.numpy()
+
+
+def _gpu_forward(params, batch, S, training=False):
+    flat = P.to_flat(params, device="cuda")
+    ws = E.Workspace("cuda")
+    z = E.forward(flat, batch, E.RunConfig(S, training=training), ws)
+    torch.cuda.synchronize()
+    return flat, ws, z
+
+
+@pytest.mark.parametrize("S", [1, 3, 5])
+@pytest.mark.parametrize("fully", [True, False])
+def test_forward_parity_small(S, fully):
+    params = O.random_params(seed=3)
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(8, 6, seed=11, fully_connected=fully)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    _, _, z = _gpu_forward(params, batch, S)
+    ref = _oracle_logits(params, obj, Rs, Rr, prop, S)
+    got = z.cpu().numpy().reshape(ref.shape)
+    err = np.abs(got - ref)
+    print(f"S={S} fully={fully} max|dz|={err.max():.3e} max|z|={np.abs(ref).max():.3f}")
+    assert np.all(err <= LOGIT_ATOL + LOGIT_RTOL * np.abs(ref))
+
+
+@pytest.mark.parametrize("N", [3, 5, 9, 12, 16])
+def test_forward_parity_sizes(N):
+    params = O.random_params(seed=5)
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(5, N, seed=N, fully_connected=False)
+    rng = np.random.default_rng(N)
+    prop = rng.normal(0, 0.3, size=prop.shape).astype(np.float32)   # non-zero propagation input
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    _, _, z = _gpu_forward(params, batch, 5)
+    ref = _oracle_logits(params, obj, Rs, Rr, prop, 5)
+    got = z.cpu().numpy().reshape(ref.shape)
+    assert np.all(np.abs(got - ref) <= LOGIT_ATOL + LOGIT_RTOL * np.abs(ref)), np.abs(got - ref).max()
+
+
+def test_backward_parity_small():
+    params = O.random_params(seed=7)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(6, 6, seed=2, fully_connected=False)
+    S = 5
+    loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, S)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    flat, ws, z = _gpu_forward(params, batch, S, training=True)
+    scratch = E.BceScratch("cuda")
+    out3, dz = E.bce(z, torch.tensor(tgt, device="cuda").reshape(-1), scratch)
+    grads, _ = E.backward(flat, batch, E.RunConfig(S, training=True), ws, dz)
+    torch.cuda.synchronize()
+    assert abs(float(out3[0]) - loss_ref) < 1e-5
+    got = P.from_flat(grads)
+    worst = 0.0
+    for name, ref in g_ref.items():
+        scale = np.abs(ref).max()
+        err = np.abs(got[name] - ref).max()
+        worst = max(worst, err / (scale + 1e-30))
+        print(f"{name:14s} max|g|={scale:.3e} max|dg|={err:.3e}")
+        assert err <= 1e-5 * scale + 1e-7, name
+    print("worst relative", worst)
