@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark: towers/s of one full training step (forward + BCE + backward [+ RCCL all-reduce] +
+Adam) on synthetic 6-block Jenga towers, 65,536 towers per GPU, 5 propagation steps, fp32.
+
+Contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run, one
+rank per GPU). Prints ONE JSON line on rank 0. See DESIGN.md §7 for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from spwgnn_amd import _lib, params as P  # noqa: E402
+from spwgnn_amd import data as D  # noqa: E402
+from spwgnn_amd.batch import TowerBatch  # noqa: E402
+from spwgnn_amd.trainer import Trainer  # noqa: E402
+
+METRIC = "towers/sec fwd+bwd, 6-block batch=65k, 1/2/4/8 MI355X; achieved HBM GB/s"
+PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: fp32 MFMA (= vector) peak
+PEAK_HBM_GBS = 8000.0
+
+# algorithmic FLOPs per launch of each timed kernel, as f(real edges, nodes, S)
+KERNELS = {
+    "edge_fwd": (_lib.K_EDGE_FWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne),
+    "edge_bwd": (_lib.K_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne),
+    "wgrad_w2": (_lib.K_WGRAD_W2, lambda Ne, Nn, S: 2.0 * 151 * 150 * Ne * S),
+    "enc_edge": (_lib.K_ENC_EDGE, lambda Ne, Nn, S: 2.0 * (2 * 150 + 4 * 150 * 150) * Ne),
+    "enc_edge_bwd": (_lib.K_ENC_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 4 * 150 * 150 * Ne),
+}
+LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "wgrad_w2": 1, "enc_edge": 1, "enc_edge_bwd": 1}
+
+
+def step_flops(Ne: int, Nn: int, S: int) -> float:
+    """Algorithmic FLOPs of one fwd+bwd training step in the form the kernels compute."""
+    fwd = Ne * (2 * 150 + 4 * 150 * 150) + Nn * (2 * 100 + 100 * 100) \
+        + S * (Ne * 150 * 150 + Nn * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150)) - Nn * 2 * 100 * 150
+    bwd_edge = Ne * (4 * 150 * 150 + 4 * 151 * 150 + 3 * 100) + S * Ne * (150 * 150 + 151 * 150)
+    bwd_node = Nn * (100 * 100 + 101 * 100 + 3 * 100) + S * Nn * (
+        2 * 150 * 100 + 101 * 100 + 300 * 100 + 150 * 100     # activation grads
+        + 2 * 100 * 150 + 151 * 100 + 301 * 100 + 101 * 101)  # weight grads
+    return 2.0 * (fwd + bwd_edge + bwd_node)
+
+
+class HipEvents:
+    def __init__(self, n):
+        self.hip = C.CDLL("libamdhip64.so")
+        self.ev = []
+        for _ in range(n):
+            e = C.c_void_p()
+            if self.hip.hipEventCreate(C.byref(e)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+            self.ev.append(e.value)
+
+    def elapsed_ms(self, a, b) -> float:
+        ms = C.c_float()
+        self.hip.hipEventSynchronize(C.c_void_p(self.ev[b]))
+        st = self.hip.hipEventElapsedTime(C.byref(ms), C.c_void_p(self.ev[a]), C.c_void_p(self.ev[b]))
+        if st != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed ({st})")
+        return ms.value
+
+    def close(self):
+        for e in self.ev:
+            self.hip.hipEventDestroy(C.c_void_p(e))
+
+
+def cpu_baseline(n_objects: int, S: int, seconds: float):
+    """The oracle (torch-CPU restatement of Networks.py, literal dense one-hot form, fp32 like
+    Keras floatx) timed fwd+bwd on a bounded sample on this host's cores."""
+    from oracle import model as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    B = 256
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, n_objects, seed=123, fully_connected=True)
+    p = O.to_torch(O.glorot_uniform_params(0), dtype=torch.float32, requires_grad=True)
+    ts = [torch.tensor(a, dtype=torch.float32) for a in (obj, Rs, Rr, prop)]
+    t = torch.tensor(tgt, dtype=torch.float32)
+
+    def one():
+        for v in p.values():
+            v.grad = None
+        z = O.forward_dense(p, *ts, S)
+        O.keras_bce_from_logits(z, t).backward()
+
+    one()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        n += 1
+        el = time.perf_counter() - t0
+        if (el > seconds and n >= 3) or n >= 200:
+            break
+    return {"value": B * n / el, "unit": "towers/s", "cores": threads, "kind": "port",
+            "sample": f"oracle.forward_dense fp32 fwd+bwd, {B} towers x {n} iters, N={n_objects}, S={S}, "
+                      f"{el:.1f}s, torch CPU threads={threads}"}
+
+
+def load_pmc(kernel: str):
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--towers", type=int, default=65536, help="towers per GPU")
+    ap.add_argument("--nodes", type=int, default=6)
+    ap.add_argument("--mp-steps", type=int, default=5)
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--roofline-kernel", default="edge_bwd", choices=sorted(KERNELS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    B, N, S = args.towers, args.nodes, args.mp_steps
+    raw = D.synthetic_towers(B, N, seed=1000 + rank)
+    objects = (raw / D.RELATION_THRESHOLD).astype(np.float32)
+    batch = TowerBatch.fully_connected(objects, device=device)
+    rng = np.random.default_rng(rank)
+    target = torch.tensor(rng.integers(0, 2, size=B * N).astype(np.float32), device=device)
+    params = P.to_flat(P.glorot_uniform(0), device=device)
+    if world > 1:
+        dist.broadcast(params, 0)
+    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7)
+
+    for _ in range(args.warmup):
+        trainer.step(batch, target)
+    torch.cuda.synchronize()
+
+    kid, flops_fn = KERNELS[args.roofline_kernel]
+    per = LAUNCHES_PER_STEP[args.roofline_kernel]
+    nl = (S if per == "S" else per) * args.steps
+    ev = HipEvents(2 * nl)
+    trainer.prof_kernel = kid
+    trainer.prof_events = ev.ev
+    # the library fills events in launch order; re-offset the array every step
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    per_step = nl // args.steps
+    for k in range(args.steps):
+        trainer.prof_events = ev.ev[2 * per_step * k: 2 * per_step * (k + 1)]
+        out3 = trainer.step(batch, target)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    kern_ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(nl)]
+    ev.close()
+    loss = float(out3[0].item())
+
+    Ne, Nn = batch.n_edges, batch.n_nodes
+    avg_ms = float(np.mean(kern_ms))
+    kflops = flops_fn(Ne, Nn, S)
+    achieved = kflops / (avg_ms * 1e-3) / 1e12
+    value = world * B * args.steps / el
+    total_flops = step_flops(Ne, Nn, S)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "towers/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
+        "config": {"workload": f"train step fwd+BCE+bwd+{'allreduce+' if world > 1 else ''}Adam, "
+                               f"{N}-block towers fully connected (E={N*(N-1)}), {B} towers/GPU, "
+                               f"{S} MP steps, dropout {args.dropout}",
+                   "towers_per_gpu": B, "global_batch": B * world, "nodes_per_tower": N, "mp_steps": S,
+                   "parallelism": f"dp{world}"},
+        "step_tflops": round(total_flops * world * args.steps / el / 1e12, 2),
+        "loss": round(loss, 5),
+        "roofline": {"kernel": args.roofline_kernel, "bound": "mfma", "achieved": round(achieved, 2),
+                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                     "avg_launch_ms": round(avg_ms, 4), "launches": nl, "flop_per_launch": kflops,
+                     "traffic": load_pmc(args.roofline_kernel)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, S, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -106,7 +106,22 @@ typedef struct spwgnn_run {
     float dropout;      /* Dropout rate on the two encodings (Networks.py:167-168); 0 = off      */
     int32_t pad0;
     uint64_t seed;      /* dropout mask key                                                       */
+    /* Optional timing hook (bench/profiling): for each launch of kernel `prof_kernel`
+     * (SPWGNN_K_*), the library records caller-created hipEvent_t prof_events[2k] before and
+     * prof_events[2k+1] after launch k (k < prof_count) on the call's stream. 0 = off. */
+    int32_t prof_kernel;
+    int32_t prof_count;
+    void** prof_events;
 } spwgnn_run;
+
+#define SPWGNN_K_NONE 0
+#define SPWGNN_K_EDGE_FWD 1
+#define SPWGNN_K_NODE_FWD 2
+#define SPWGNN_K_EDGE_BWD 3
+#define SPWGNN_K_NODE_BWD 4
+#define SPWGNN_K_ENC_EDGE 5
+#define SPWGNN_K_ENC_EDGE_BWD 6
+#define SPWGNN_K_WGRAD_W2 7
 
 /* Workspace bytes for (n_nodes, n_eblocks, mp_steps, training). */
 int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training);

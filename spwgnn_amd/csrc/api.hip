@@ -42,7 +42,8 @@ struct Ws {
     int64_t dP_at(int k) const { return dP + (int64_t)(k & 1) * RN * kLdN; }
 };
 
-static constexpr int kMaxChunks = 1024;
+static constexpr int kMaxChunks = 768;
+static constexpr int kReduceGroups = 32;
 
 static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     Ws w;
@@ -97,7 +98,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.dz3 = take(eE);
         w.dz2 = take(eE);
         w.dz1 = take(eE);
-        w.slab_floats = (int64_t)kMaxChunks * 160 * 160;
+        w.slab_floats = (int64_t)(kMaxChunks + kReduceGroups) * 160 * 160;
         w.slab = take(w.slab_floats);
     } else {
         w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = -1;
@@ -189,6 +190,22 @@ static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
     return SPWGNN_OK;
 }
 
+struct Prof {
+    const spwgnn_run* r;
+    hipStream_t st;
+    mutable int k = 0;
+    hipError_t before(int kid) const {
+        if (r->prof_kernel != kid || !r->prof_events || k >= r->prof_count) return hipSuccess;
+        return hipEventRecord(static_cast<hipEvent_t>(r->prof_events[2 * k]), st);
+    }
+    hipError_t after(int kid) const {
+        if (r->prof_kernel != kid || !r->prof_events || k >= r->prof_count) return hipSuccess;
+        hipError_t e = hipEventRecord(static_cast<hipEvent_t>(r->prof_events[2 * k + 1]), st);
+        ++k;
+        return e;
+    }
+};
+
 #define SPW_CHECK(x)                                  \
     do {                                              \
         hipError_t e_ = (x);                          \
@@ -259,9 +276,15 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.thresh = thresh;
     ee.scale = scale;
     ee.seed = r->seed;
-    SPW_CHECK(launch_enc_edge(ee, st));
+    {
+        Prof p0{r, st};
+        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
+        SPW_CHECK(launch_enc_edge(ee, st));
+        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
+    }
 
     const int S = r->mp_steps;
+    Prof prof{r, st};
     for (int s = 0; s < S; ++s) {
         EdgeFwdArgs ef{};
         ef.n_wtiles = b->n_wtiles;
@@ -279,7 +302,9 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.H2s = c.f(w.H2s_at(s));
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
+        SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
         SPW_CHECK(launch_edge_fwd(ef, st));
+        SPW_CHECK(prof.after(SPWGNN_K_EDGE_FWD));
 
         NodeFwdArgs nf{};
         nf.n_nodes = b->n_nodes;
@@ -301,7 +326,9 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         nf.w1c = c.pk(PK_W1C);
         nf.bo1 = c.pk(PB_O1);
         nf.bo2p = c.pk(PB_O2P);
+        SPW_CHECK(prof.before(SPWGNN_K_NODE_FWD));
         SPW_CHECK(launch_node_fwd(nf, st));
+        SPW_CHECK(prof.after(SPWGNN_K_NODE_FWD));
     }
     return SPWGNN_OK;
 }
@@ -321,10 +348,10 @@ struct WgSpec {
 };
 
 static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, hipStream_t st,
-                         int64_t U_off, int64_t V_off, int64_t G3_off, int64_t m2_off) {
+                         int64_t U_off, int64_t V_off, int64_t G3_off, int64_t m2_off, const Prof* prof = nullptr) {
     const Ws& w = c.w;
     if (g.rows <= 0) return SPWGNN_OK;
-    int64_t chunks = (g.rows + 32 * 8 - 1) / (32 * 8);
+    int64_t chunks = (g.rows + 32 * 16 - 1) / (32 * 16);
     chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, kMaxChunks));
     int64_t rpc = up((g.rows + chunks - 1) / chunks, 32);
     chunks = (g.rows + rpc - 1) / rpc;
@@ -357,7 +384,9 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     a.RE = w.RE;
     a.RN = w.RN;
     a.slab = c.f(w.slab);
+    if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
     SPW_CHECK(launch_wgrad(a, (int)chunks, st));
+    if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     const ParamTable& pt = param_table();
     ReduceArgs ra{};
     ra.slab = c.f(w.slab);
@@ -372,7 +401,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     ra.bias_off = g.tb >= 0 ? pt.t[g.tb].offset : -1;
     ra.bias_row = g.bias_row;
     ra.perm = g.perm;
-    SPW_CHECK(launch_wgrad_reduce(ra, st));
+    SPW_CHECK(launch_wgrad_reduce(ra, c.f(w.slab) + (int64_t)kMaxChunks * 160 * 160, kReduceGroups, st));
     return SPWGNN_OK;
 }
 
@@ -384,6 +413,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     const int64_t nN = b->n_nodes;
     const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
     SPW_CHECK(hipMemsetAsync(grads, 0, param_table().total * sizeof(float), st));
+    Prof prof{r, st};
 
     for (int s = S - 1; s >= 0; --s) {
         const bool first = (s == S - 1);
@@ -412,7 +442,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         nb.wo1at = c.pk(PK_WO1AT);
         nb.wo1pt = c.pk(PK_WO1PT);
         nb.w3t = c.pk(PK_W3T);
+        SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
         SPW_CHECK(launch_node_bwd(nb, st));
+        SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
 
         EdgeBwdArgs eb{};
         eb.n_wtiles = b->n_wtiles;
@@ -430,7 +462,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.dA = c.f(w.dA);
         eb.dU = c.f(w.dU_at(s));
         eb.dV = c.f(w.dV_at(s));
+        SPW_CHECK(prof.before(SPWGNN_K_EDGE_BWD));
         SPW_CHECK(launch_edge_bwd(eb, st));
+        SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
     }
     if (dprop) {
         NodeBwdArgs nb{};
@@ -461,7 +495,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     eeb.dz2 = c.f(w.dz2);
     eeb.dz1 = c.f(w.dz1);
     eeb.scale = scale;
+    SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
     SPW_CHECK(launch_enc_edge_bwd(eeb, st));
+    SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
 
     EncNodeBwdArgs enb{};
     enb.n_nodes = b->n_nodes;
@@ -496,7 +532,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.1 (W2, b2): X = [h1 | 1] recomputed, Y = dh2pre, over all steps
         WgSpec g; g.xmode = XM_EDGE_H1; g.ymode = YM_EDGE_DH2; g.kx_pad = 160; g.ny_pad = 160; g.rows = RE * S;
         g.tk = T_RMP1K; g.tb = T_RMP1B; g.k_rows = kFE; g.bias_row = kFE;
-        if ((e = run_wgrad(c, b, g, grads, st, w.U, w.V, w.G3, w.mask2))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st, w.U, w.V, w.G3, w.mask2, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {

@@ -40,6 +40,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
+// Put a wave-uniform 32-bit value into lane `ln` of `old` (v_cmp + v_cndmask; no exec branch).
+__device__ __forceinline__ uint32_t writelane(uint32_t val, int ln, uint32_t old) {
+    return ((int)(threadIdx.x & 63) == ln) ? val : old;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Dropout key (our own counter-based RNG; Keras' TF draws cannot be reproduced — DESIGN.md §6).
 // keep(seed, kind, tower, a, b, feature) = mix(...) >= rate·2^32.  Restated bit-exactly in

@@ -166,7 +166,7 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st);
-hipError_t launch_wgrad_reduce(const ReduceArgs& a, hipStream_t st);
+hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);

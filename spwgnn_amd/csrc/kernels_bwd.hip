@@ -20,17 +20,32 @@ __device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_k
     const int i = lane & 31, h = lane >> 5;
     const float4* x4 = reinterpret_cast<const float4*>(row_khh);
     const float* wbase = W + (KH * h) * LDW + i;
+    float wc[4][NT_OUT], wn[4][NT_OUT];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) wc[c][t] = wbase[c * LDW + 32 * t];
     float4 nxt = x4[0];
 #pragma unroll 1
     for (int q = 0; q < KH / 4; ++q) {
         const float4 cur = nxt;
-        if (q + 1 < KH / 4) nxt = x4[q + 1];
+        if (q + 1 < KH / 4) {
+            const float* wrow = wbase + (4 * q + 4) * LDW;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int t = 0; t < NT_OUT; ++t) wn[c][t] = wrow[c * LDW + 32 * t];
+            nxt = x4[q + 1];
+        }
         const float xv[4] = {cur.x, cur.y, cur.z, cur.w};
-        const float* wrow = wbase + (4 * q) * LDW;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wrow[c * LDW + 32 * t], xv[c], out[t]);
+            for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wc[c][t], xv[c], out[t]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < NT_OUT; ++t) wc[c][t] = wn[c][t];
     }
 }
 
@@ -141,15 +156,21 @@ __global__ __launch_bounds__(256, 2) void k_node_bwd(NodeBwdArgs a) {
 template <int WORD_BASE>
 __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint32_t csrw, int t, bool tv, int lane) {
     const int i = lane & 31, h = lane >> 5;
+    // all LDS reads first (independent, pipelined), then the ordered per-node sums
+    float vals[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
+        const int eo = (ow >> (8 * (k & 3))) & 31;
+        vals[k] = st[h * 1056 + eo * 33 + i];
+    }
     float sum = 0.f;
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + (k >> 2));
         const int nd = (nw >> (8 * (k & 3))) & 255;
         if (nd == 255) break;
-        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
-        const int eo = (ow >> (8 * (k & 3))) & 255;
-        sum += st[h * 1056 + eo * 33 + i];
+        sum += vals[k];
         int ndn = 255;
         if (k < 31) {
             const uint32_t nw2 = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + ((k + 1) >> 2));
@@ -192,11 +213,23 @@ __global__ __launch_bounds__(256, 2) void k_edge_bwd(EdgeBwdArgs a) {
         f32x16 acc[5];
         zero_tiles(acc);
         const float* wbase = a.w2t + (kKhE * h) * kLdE + i;
+        float wc[4][5], wn[4][5];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < 5; ++t) wc[c][t] = wbase[c * kLdE + 32 * t];
         float4 nxt = G4[0];
 #pragma unroll 1
         for (int q = 0; q < kKhE / 4; ++q) {
             const float4 cur = nxt;
-            if (q + 1 < kKhE / 4) nxt = G4[q + 1];
+            if (q + 1 < kKhE / 4) {
+                const float* wrow = wbase + (4 * q + 4) * kLdE;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int t = 0; t < 5; ++t) wn[c][t] = wrow[c * kLdE + 32 * t];
+                nxt = G4[q + 1];
+            }
             // 4 features f0..f0+3 (f0 = 76h + 4q) share one mask word (f0 % 4 == 0)
             const int f0 = kKhE * h + 4 * q;
             const int wi = f0 >> 5;
@@ -207,11 +240,14 @@ __global__ __launch_bounds__(256, 2) void k_edge_bwd(EdgeBwdArgs a) {
             xv[1] = (bits & 2u) ? cur.y : 0.f;
             xv[2] = (bits & 4u) ? cur.z : 0.f;
             xv[3] = (bits & 8u) ? cur.w : 0.f;
-            const float* wrow = wbase + (4 * q) * kLdE;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
-                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wrow[c * kLdE + 32 * t], acc[t]);
+                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wc[c][t], acc[t]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int t = 0; t < 5; ++t) wc[c][t] = wn[c][t];
         }
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
         const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;

@@ -157,15 +157,21 @@ __global__ __launch_bounds__(256, 2) void k_enc_edge(EncEdgeArgs a) {
 template <int WORD_BASE>
 __device__ __forceinline__ void segsum_walk(const float* st, float* nacc, uint32_t csrw, int t, bool tv, int lane) {
     const int i = lane & 31, h = lane >> 5;
+    // all LDS reads first (independent, pipelined), then the ordered per-node sums
+    float vals[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
+        const int eo = (ow >> (8 * (k & 3))) & 31;
+        vals[k] = st[h * 1056 + eo * 33 + i];
+    }
     float sum = 0.f;
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + (k >> 2));
         const int nd = (nw >> (8 * (k & 3))) & 255;
         if (nd == 255) break;
-        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
-        const int eo = (ow >> (8 * (k & 3))) & 255;
-        sum += st[h * 1056 + eo * 33 + i];
+        sum += vals[k];
         int ndn = 255;
         if (k < 31) {
             const uint32_t nw2 = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + ((k + 1) >> 2));
@@ -211,45 +217,68 @@ __global__ __launch_bounds__(256, 2) void k_edge_fwd(EdgeFwdArgs a) {
         const int sc = valid ? s : n0, dc = valid ? d : n0;
         // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:174-177), lane = edge, split
         // halves, streamed 4 features at a time straight into h2 = h1·W2 (rmp layer 2).
+        // W2 fragments are double-buffered in registers one chunk ahead (no load→MFMA stall).
         const uint64_t vmask = __ballot(valid);
+        const float vf = valid ? 1.f : 0.f;
         const float4* A4 = reinterpret_cast<const float4*>(a.A + e * kLdE + kKhE * h);
         const float4* U4 = reinterpret_cast<const float4*>(a.U + (int64_t)sc * kLdE + kKhE * h);
         const float4* V4 = reinterpret_cast<const float4*>(a.V + (int64_t)dc * kLdE + kKhE * h);
-        uint32_t* m1row = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
+        const bool want_m1 = a.mask1 != nullptr;
+        uint32_t mw0 = 0, mw1 = 0, mw2 = 0;
         f32x16 acc[5];
         zero_tiles(acc);
-        float4 pa = A4[0], pu = U4[0], pv = V4[0];
         const float* wbase = a.w2 + (kKhE * h) * kLdE + i;
+        float wc[4][5], wn[4][5];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < 5; ++t) wc[c][t] = wbase[c * kLdE + 32 * t];
+        float4 pa = A4[0], pu = U4[0], pv = V4[0];
 #pragma unroll 1
         for (int q = 0; q < kKhE / 4; ++q) {
             const float4 ca = pa, cu = pu, cv = pv;
             if (q + 1 < kKhE / 4) {
+                const float* wrow = wbase + (4 * q + 4) * kLdE;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int t = 0; t < 5; ++t) wn[c][t] = wrow[c * kLdE + 32 * t];
                 pa = A4[q + 1];
                 pu = U4[q + 1];
                 pv = V4[q + 1];
             }
             float xv[4];
-            xv[0] = valid ? relu(ca.x + cu.x + cv.x) : 0.f;
-            xv[1] = valid ? relu(ca.y + cu.y + cv.y) : 0.f;
-            xv[2] = valid ? relu(ca.z + cu.z + cv.z) : 0.f;
-            xv[3] = valid ? relu(ca.w + cu.w + cv.w) : 0.f;
-            if (m1row) {  // h1 > 0 bits: word per (block, feature), bit = edge
-                uint32_t word = 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const uint64_t bal = __ballot(xv[c] > 0.f);
-                    if (lane == c) word = (uint32_t)bal;
-                    if (lane == 4 + c) word = (uint32_t)(bal >> 32);
-                }
-                if (lane < 8) m1row[(lane < 4 ? 4 * q + lane : kKhE + 4 * q + lane - 4)] = word;
-            }
-            const float* wrow = wbase + (4 * q) * kLdE;
+            xv[0] = relu(ca.x + cu.x + cv.x) * vf;
+            xv[1] = relu(ca.y + cu.y + cv.y) * vf;
+            xv[2] = relu(ca.z + cu.z + cv.z) * vf;
+            xv[3] = relu(ca.w + cu.w + cv.w) * vf;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
-                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wrow[c * kLdE + 32 * t], acc[t]);
+                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wc[c][t], acc[t]);
+            if (want_m1) {  // h1 > 0 bits: word per (block, feature), bit = edge; feature f → lane f&63
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint64_t bal = __ballot(xv[c] > 0.f);
+                    const int f0 = 4 * q + c, f1 = kKhE + 4 * q + c;
+                    const uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
+                    if (f0 < 64) mw0 = writelane(lo, f0, mw0);
+                    else mw1 = writelane(lo, f0 - 64, mw1);
+                    if (f1 < 128) mw1 = writelane(hi, f1 - 64, mw1);
+                    else mw2 = writelane(hi, f1 - 128, mw2);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int t = 0; t < 5; ++t) wc[c][t] = wn[c][t];
         }
-        if (m1row && lane < 8) m1row[152 + lane] = 0u;
+        if (want_m1) {
+            uint32_t* mrow = a.mask1 + (int64_t)blk * kLdE;
+            mrow[lane] = mw0;
+            mrow[64 + lane] = mw1;
+            if (lane < 32) mrow[128 + lane] = lane < 24 ? mw2 : 0u;
+        }
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const float b = a.b2[32 * t + i];
@@ -263,17 +292,19 @@ __global__ __launch_bounds__(256, 2) void k_edge_fwd(EdgeFwdArgs a) {
         }
         if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
             uint32_t* m2row = a.mask2 + (int64_t)blk * 160;
+            uint32_t mw[3] = {0u, 0u, 0u};
 #pragma unroll
-            for (int t = 0; t < 5; ++t) {
-                uint32_t word = 0;
+            for (int t = 0; t < 5; ++t)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const uint64_t bal = __ballot(acc[t][r] > 0.f);
-                    if (lane == rho(r, 0)) word = (uint32_t)bal;
-                    if (lane == rho(r, 1)) word = (uint32_t)(bal >> 32);
+                    const int w0 = t * 32 + rho(r, 0), w1 = t * 32 + rho(r, 1);
+                    mw[w0 >> 6] = writelane((uint32_t)bal, w0 & 63, mw[w0 >> 6]);
+                    mw[w1 >> 6] = writelane((uint32_t)(bal >> 32), w1 & 63, mw[w1 >> 6]);
                 }
-                if (lane < 32) m2row[t * 32 + lane] = word;
-            }
+            m2row[lane] = mw[0];
+            m2row[64 + lane] = mw[1];
+            if (lane < 32) m2row[128 + lane] = mw[2];
         }
         // receiver segment sum (Networks.py:178 dot(receiver_relations, x)) into LDS node rows
         const uint32_t csrw = a.csr[(int64_t)blk * 32 + i];

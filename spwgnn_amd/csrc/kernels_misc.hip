@@ -5,96 +5,139 @@
 namespace spw {
 
 constexpr int kWgThreads = 320;   // 5 waves: wave w owns output row tile w (32 x-features × all y tiles)
-constexpr int kWgLd = 161;        // LDS row stride (odd: conflict-free column reads)
 
 __device__ __forceinline__ int64_t wg_phys(int64_t L, int64_t count, int64_t stride) {
     const int64_t s = L / count, n = L - s * count;
     return (stride ? s * stride : 0) + n;
 }
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void f4set(float4& v, int k, float x) {
+    if (k == 0) v.x = x; else if (k == 1) v.y = x; else if (k == 2) v.z = x; else if (k == 3) v.w = x;
+}
+__device__ __forceinline__ float4 f4relu(float4 v) {
+    return make_float4(relu(v.x), relu(v.y), relu(v.z), relu(v.w));
+}
+__device__ __forceinline__ float4 f4add3(float4 a, float4 b, float4 c) {
+    return make_float4(a.x + b.x + c.x, a.y + b.y + c.y, a.z + b.z + c.z, a.w + b.w + c.w);
+}
 
-__device__ __forceinline__ float wg_x(const WgradArgs& a, int64_t L, int f) {
-    switch (a.xmode) {
-        case XM_ROW: {
-            if (f < a.x_width) return a.x_ptr[wg_phys(L, a.x_count, a.x_stride) * a.x_ld + f];
-            return f == a.x_ones ? 1.f : 0.f;
+// 4 consecutive X features [f0, f0+4) of logical row L (all producers write zero padding up to ld)
+template <int XM>
+__device__ __forceinline__ float4 wg_x4(const WgradArgs& a, int64_t L, int f0) {
+    if (XM == XM_ROW) {
+        const int64_t r = wg_phys(L, a.x_count, a.x_stride);
+        float4 v = f0 < a.x_ld ? *reinterpret_cast<const float4*>(a.x_ptr + r * a.x_ld + f0) : f4zero();
+        if (a.x_ones >= f0 && a.x_ones < f0 + 4) f4set(v, a.x_ones - f0, 1.f);
+        return v;
+    } else if (XM == XM_EDGE_D) {
+        const int sidx = a.esrc[L];
+        float4 v = f4zero();
+        if (sidx >= 0 && f0 == 0) {
+            const float4 ps = reinterpret_cast<const float4*>(a.pos)[sidx];
+            const float4 pd = reinterpret_cast<const float4*>(a.pos)[a.edst[L]];
+            v = make_float4(pd.x - ps.x, pd.y - ps.y, 1.f, 0.f);
         }
-        case XM_EDGE_D: {
-            const int64_t e = L;
-            const int sidx = a.esrc[e];
-            if (sidx < 0) return 0.f;
-            if (f < 2) return a.pos[(int64_t)a.edst[e] * 4 + f] - a.pos[(int64_t)sidx * 4 + f];
-            return f == 2 ? 1.f : 0.f;
+        return v;
+    } else if (XM == XM_NODE_O) {
+        float4 v = f4zero();
+        if (f0 == 0) {
+            const float4 p = reinterpret_cast<const float4*>(a.pos)[L];
+            v = make_float4(p.y, p.z, 1.f, 0.f);
         }
-        case XM_NODE_O: {
-            if (f < 2) return a.pos[L * 4 + 1 + f];
-            return f == 2 ? 1.f : 0.f;
-        }
-        default: {  // XM_EDGE_H1, L = s*RE + e
-            const int64_t s = L / a.RE, e = L - s * a.RE;
-            const int sidx = a.esrc[e];
-            if (sidx < 0) return 0.f;
-            if (f < kFE) {
-                const int didx = a.edst[e];
-                const float v = a.A[e * kLdE + f] + a.U[(s * a.RN + sidx) * kLdE + f] + a.V[(s * a.RN + didx) * kLdE + f];
-                return relu(v);
-            }
-            return f == kFE ? 1.f : 0.f;
-        }
+        return v;
+    } else {  // XM_EDGE_H1
+        const int64_t s = L / a.RE, e = L - s * a.RE;
+        const int sidx = a.esrc[e];
+        if (sidx < 0) return f4zero();
+        const int didx = a.edst[e];
+        const float4 x = *reinterpret_cast<const float4*>(a.A + e * kLdE + f0);
+        const float4 u = *reinterpret_cast<const float4*>(a.U + (s * a.RN + sidx) * kLdE + f0);
+        const float4 w = *reinterpret_cast<const float4*>(a.V + (s * a.RN + didx) * kLdE + f0);
+        float4 v = f4relu(f4add3(x, u, w));
+        if (f0 == 148) { v.z = 1.f; v.w = 0.f; }        // feature 150 = ones (b2), 151 = 0
+        else if (f0 >= 152) v = f4zero();
+        return v;
     }
 }
 
-__device__ __forceinline__ float wg_y(const WgradArgs& a, int64_t L, int f) {
-    if (a.ymode == YM_ROW) return f < a.y_width ? a.y_ptr[wg_phys(L, a.y_count, a.y_stride) * a.y_ld + f] : 0.f;
-    // YM_EDGE_DH2
-    const int64_t s = L / a.RE, e = L - s * a.RE;
-    const int didx = a.edst[e];
-    if (didx < 0 || f >= kFE) return 0.f;
-    const uint32_t word = a.mask2[(s * (a.RE / 32) + (e >> 5)) * 160 + (f >> 5) * 32 + (e & 31)];
-    return ((word >> (f & 31)) & 1u) ? a.G3[(s * a.RN + didx) * kLdE + f] : 0.f;
+template <int YM>
+__device__ __forceinline__ float4 wg_y4(const WgradArgs& a, int64_t L, int f0) {
+    if (YM == YM_ROW) {
+        const int64_t r = wg_phys(L, a.y_count, a.y_stride);
+        return f0 < a.y_ld ? *reinterpret_cast<const float4*>(a.y_ptr + r * a.y_ld + f0) : f4zero();
+    } else {  // YM_EDGE_DH2
+        const int64_t s = L / a.RE, e = L - s * a.RE;
+        const int didx = a.edst[e];
+        if (didx < 0 || f0 >= 152) return f4zero();
+        const uint32_t word = a.mask2[(s * (a.RE / 32) + (e >> 5)) * 160 + (f0 >> 5) * 32 + (e & 31)];
+        const uint32_t bits = word >> (f0 & 31);
+        const float4 g = *reinterpret_cast<const float4*>(a.G3 + (s * a.RN + didx) * kLdE + f0);
+        return make_float4((bits & 1u) ? g.x : 0.f, (bits & 2u) ? g.y : 0.f, (bits & 4u) ? g.z : 0.f,
+                           (bits & 8u) ? g.w : 0.f);
+    }
 }
 
-__global__ __launch_bounds__(kWgThreads) void k_wgrad(WgradArgs a) {
-    __shared__ float Xs[32 * kWgLd];
-    __shared__ float Ys[32 * kWgLd];
+// dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n]
+template <int XM, int YM, int KXP, int NYP>
+__global__ __launch_bounds__(kWgThreads) void k_wgrad_t(WgradArgs a) {
+    constexpr int TX = KXP / 32, TY = NYP / 32;
+    constexpr int LDX = KXP + 4, LDY = NYP + 4;   // 16-B aligned rows; MFMA reads are conflict-free
+    constexpr int GX = KXP / 4, GY = NYP / 4;
+    __shared__ __attribute__((aligned(16))) float Xs[32 * LDX];
+    __shared__ __attribute__((aligned(16))) float Ys[32 * LDY];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
     const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
-    const int TX = a.kx_pad / 32, TY = a.ny_pad / 32;
-    f32x16 acc[5];
-    zero_tiles(acc);
+    f32x16 acc[TY];
+#pragma unroll
+    for (int t = 0; t < TY; ++t) acc[t] = zero16();
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
-        for (int idx = tid; idx < 32 * a.kx_pad; idx += kWgThreads) {
-            const int rr = idx / a.kx_pad, f = idx - rr * a.kx_pad;
+#pragma unroll
+        for (int g = tid; g < 32 * GX; g += kWgThreads) {
+            const int rr = g / GX, c4 = g - rr * GX;
             const int64_t L = r0 + rr;
-            Xs[rr * kWgLd + f] = L < r_end ? wg_x(a, L, f) : 0.f;
+            const float4 v = L < r_end ? wg_x4<XM>(a, L, 4 * c4) : f4zero();
+            *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = v;
         }
-        for (int idx = tid; idx < 32 * a.ny_pad; idx += kWgThreads) {
-            const int rr = idx / a.ny_pad, f = idx - rr * a.ny_pad;
+#pragma unroll
+        for (int g = tid; g < 32 * GY; g += kWgThreads) {
+            const int rr = g / GY, c4 = g - rr * GY;
             const int64_t L = r0 + rr;
-            Ys[rr * kWgLd + f] = L < r_end ? wg_y(a, L, f) : 0.f;
+            const float4 v = L < r_end ? wg_y4<YM>(a, L, 4 * c4) : f4zero();
+            *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = v;
         }
         __syncthreads();
         if (wave < TX) {
-#pragma unroll 4
+#pragma unroll
             for (int k2 = 0; k2 < 16; ++k2) {
                 const int rr = 2 * k2 + h;
-                const float av = Xs[rr * kWgLd + 32 * wave + i];
+                const float av = Xs[rr * LDX + 32 * wave + i];
 #pragma unroll
-                for (int ty = 0; ty < 5; ++ty)
-                    if (ty < TY) acc[ty] = mfma32(av, Ys[rr * kWgLd + 32 * ty + i], acc[ty]);
+                for (int ty = 0; ty < TY; ++ty) acc[ty] = mfma32(av, Ys[rr * LDY + 32 * ty + i], acc[ty]);
             }
         }
     }
     if (wave < TX) {
-        float* out = a.slab + (int64_t)blockIdx.x * a.kx_pad * a.ny_pad;
+        float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
 #pragma unroll
-        for (int ty = 0; ty < 5; ++ty) {
-            if (ty >= TY) continue;
+        for (int ty = 0; ty < TY; ++ty)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) out[(int64_t)(32 * wave + rho(r, 0) + 4 * h) * a.ny_pad + 32 * ty + i] = acc[ty][r];
-        }
+            for (int r = 0; r < 16; ++r) out[(int64_t)(32 * wave + rho(r, 0) + 4 * h) * NYP + 32 * ty + i] = acc[ty][r];
     }
+}
+
+// stage 1: partial[g][idx] = Σ_{c in group g} slab[c][idx] (contiguous chunk ranges, fixed order)
+__global__ void k_wgrad_reduce1(ReduceArgs a, float* partial, int groups) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = a.kx_pad * a.ny_pad;
+    if (idx >= n) return;
+    const int g = blockIdx.y;
+    const int per = (a.chunks + groups - 1) / groups;
+    const int c0 = g * per, c1 = min(a.chunks, c0 + per);
+    float s = 0.f;
+    for (int c = c0; c < c1; ++c) s += a.slab[(int64_t)c * n + idx];
+    partial[(int64_t)g * n + idx] = s;
 }
 
 __global__ void k_wgrad_reduce(ReduceArgs a) {
@@ -173,12 +216,33 @@ __global__ void k_sigmoid(const float* z, float* p, int64_t n) {
 
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
-    hipLaunchKernelGGL(k_wgrad, dim3(chunks), dim3(kWgThreads), 0, st, a);
-    return hipGetLastError();
+    const dim3 g(chunks), b(kWgThreads);
+#define SPW_WG(XM, YM, KX, NY)                                                               \
+    if (a.xmode == XM && a.ymode == YM && a.kx_pad == KX && a.ny_pad == NY) {                 \
+        hipLaunchKernelGGL((k_wgrad_t<XM, YM, KX, NY>), g, b, 0, st, a);                      \
+        return hipGetLastError();                                                             \
+    }
+    SPW_WG(XM_ROW, YM_ROW, 160, 160)
+    SPW_WG(XM_ROW, YM_ROW, 128, 160)
+    SPW_WG(XM_ROW, YM_ROW, 160, 128)
+    SPW_WG(XM_ROW, YM_ROW, 128, 128)
+    SPW_WG(XM_EDGE_D, YM_ROW, 32, 160)
+    SPW_WG(XM_NODE_O, YM_ROW, 32, 128)
+    SPW_WG(XM_EDGE_H1, YM_EDGE_DH2, 160, 160)
+#undef SPW_WG
+    return hipErrorInvalidValue;
 }
-hipError_t launch_wgrad_reduce(const ReduceArgs& a, hipStream_t st) {
+hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st) {
     const int n = a.kx_pad * a.ny_pad;
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, st, a);
+    if (groups > 1 && a.chunks > groups) {
+        hipLaunchKernelGGL(k_wgrad_reduce1, dim3((n + 255) / 256, groups), dim3(256), 0, st, a, partial, groups);
+        ReduceArgs b = a;
+        b.slab = partial;
+        b.chunks = groups;
+        hipLaunchKernelGGL(k_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, st, b);
+    } else {
+        hipLaunchKernelGGL(k_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, st, a);
+    }
     return hipGetLastError();
 }
 hipError_t launch_bce(const BceArgs& a, hipStream_t st) {

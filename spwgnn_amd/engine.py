@@ -33,6 +33,8 @@ class RunConfig:
     training: bool = False
     dropout: float = 0.0
     seed: int = 0
+    prof_kernel: int = 0                 # SPWGNN_K_* to bracket with HIP events (bench only)
+    prof_events: Optional[list] = None   # raw hipEvent_t handles, 2 per launch
 
     def cstruct(self) -> _lib.RunC:
         r = _lib.RunC()
@@ -40,6 +42,12 @@ class RunConfig:
         r.training = 1 if self.training else 0
         r.dropout = float(self.dropout)
         r.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        if self.prof_kernel and self.prof_events:
+            arr = (C.c_void_p * len(self.prof_events))(*self.prof_events)
+            self._prof_arr = arr   # keep alive for the call
+            r.prof_kernel = int(self.prof_kernel)
+            r.prof_count = len(self.prof_events) // 2
+            r.prof_events = C.cast(arr, C.c_void_p)
         return r
 
 
