@@ -101,8 +101,9 @@ def calculate_stability(boxes: np.ndarray, threshold: float = 0.5) -> np.ndarray
 
 
 def load_trajectories(path: str, n_objects: int, object_dim: int = 3) -> np.ndarray:
-    """main.py:39-63: JSON [traj][obj][frame][x,y,(w)] → (T, F, N, object_dim), frames padded
-    with each object's last frame; empty trajectories dropped."""
+    """main.py:39-63: JSON [traj][obj][frame][x,y,(w)] → (T, F, N, object_dim); F = max over
+    trajectories of object 0's frame count (main.py:46-47); each object is truncated to F or
+    padded with its last frame; empty trajectories dropped (main.py:44)."""
     with open(path) as f:
         data = json.load(f)
     data = [d for d in data if len(d) != 0]
@@ -110,7 +111,7 @@ def load_trajectories(path: str, n_objects: int, object_dim: int = 3) -> np.ndar
     boxes = np.zeros((len(data), n_frame, n_objects, object_dim))
     for t, traj in enumerate(data):
         for o in range(n_objects):
-            fr = np.asarray(traj[o], dtype=np.float64)[:, :object_dim]
+            fr = np.asarray(traj[o], dtype=np.float64)[:n_frame, :object_dim]   # main.py:55-63 truncates/pads
             boxes[t, :len(fr), o] = fr
             boxes[t, len(fr):, o] = fr[-1]
     return boxes

@@ -1,0 +1,210 @@
+"""GPU: committed golden vectors (incl. dropout), determinism, full-size property checks, ragged
+batches, the optimizer step, and the Keras-shaped front end — all through the C-ABI.
+
+Tolerances as in test_gpu_parity.py (logits 1e-5 abs + 1e-5 rel; grads 1e-5 of each tensor's max).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dropout as DR
+from oracle import model as O
+from spwgnn_amd import PropagationNetwork, TowerBatch, data as D, engine as E, params as P
+from spwgnn_amd.trainer import Trainer
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _params():
+    return dict(np.load(os.path.join(GOLDEN, "golden_params.npz")))
+
+
+def _fwd_bwd(params, batch, tgt, S, dropout=0.0, seed=0):
+    flat = P.to_flat(params, device="cuda")
+    ws = E.Workspace("cuda")
+    run = E.RunConfig(S, training=True, dropout=dropout, seed=seed)
+    z = E.forward(flat, batch, run, ws)
+    out3, dz = E.bce(z, torch.as_tensor(tgt, device="cuda").reshape(-1), E.BceScratch("cuda"))
+    grads, dprop = E.backward(flat, batch, run, ws, dz, want_dprop=True)
+    torch.cuda.synchronize()
+    return z.cpu().numpy(), float(out3[0]), P.from_flat(grads), dprop.cpu().numpy()
+
+
+def _check_grads(got, ref_full=None, g=None):
+    for k in got:
+        if ref_full is not None:
+            ref = ref_full[k]
+            assert np.abs(got[k] - ref).max() <= 1e-5 * np.abs(ref).max() + 1e-7, k
+        else:
+            sel = got[k].reshape(-1)[g["gidx/" + k]]
+            ref = g["gval/" + k]
+            assert np.abs(sel - ref).max() <= 1e-5 * max(np.abs(ref).max(), 1e-3) + 1e-7, k
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "golden_N*.npz"))))
+def test_golden_vectors(path):
+    g = np.load(path)
+    S = int(g["mp_steps"])
+    prop = g["prop"] if np.any(g["prop"]) else None
+    batch = TowerBatch.from_dense(g["objects"], g["Rs"], g["Rr"], prop, device="cuda")
+    z, loss, grads, _ = _fwd_bwd(_params(), batch, g["target"], S)
+    ref = g["logits"]
+    assert np.all(np.abs(z.reshape(ref.shape) - ref) <= 1e-5 + 1e-5 * np.abs(ref))
+    assert abs(loss - float(g["loss"])) < 1e-5
+    full = {k[5:]: g[k] for k in g.files if k.startswith("grad/")}
+    _check_grads(grads, full if full else None, None if full else g)
+
+
+def test_golden_dropout():
+    g = np.load(os.path.join(GOLDEN, "golden_dropout_N6_B2_S5.npz"))
+    batch = TowerBatch.from_dense(g["objects"], g["Rs"], g["Rr"], None, device="cuda")
+    z, loss, grads, _ = _fwd_bwd(_params(), batch, g["target"], int(g["mp_steps"]), float(g["rate"]), int(g["seed"]))
+    ref = g["logits"]
+    assert np.all(np.abs(z.reshape(ref.shape) - ref) <= 1e-5 + 1e-5 * np.abs(ref))
+    _check_grads(grads, {k[5:]: g[k] for k in g.files if k.startswith("grad/")})
+
+
+def test_dprop_gradient_matches_oracle():
+    params = O.random_params(8)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(3, 5, seed=4, fully_connected=False)
+    prop = np.random.default_rng(1).normal(0, 0.3, prop.shape).astype(np.float32)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    _, _, _, dprop = _fwd_bwd(params, batch, tgt, 4)
+    tp = O.to_torch(params)
+    pt = torch.tensor(prop, dtype=torch.float64, requires_grad=True)
+    z = O.forward_dense(tp, torch.tensor(obj, dtype=torch.float64), torch.tensor(Rs, dtype=torch.float64),
+                        torch.tensor(Rr, dtype=torch.float64), pt, 4)
+    O.keras_bce_from_logits(z, torch.tensor(tgt, dtype=torch.float64)).backward()
+    ref = pt.grad.numpy().reshape(-1, 100)
+    assert np.abs(dprop - ref).max() <= 1e-5 * np.abs(ref).max() + 1e-8
+
+
+def test_bitwise_deterministic():
+    params = O.random_params(2)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(64, 6, seed=5, fully_connected=False)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    a = _fwd_bwd(params, batch, tgt, 5, 0.1, 99)
+    b = _fwd_bwd(params, batch, tgt, 5, 0.1, 99)
+    assert np.array_equal(a[0], b[0])
+    for k in a[2]:
+        assert np.array_equal(a[2][k], b[2][k]), k
+
+
+def test_full_size_towers_are_independent():
+    """B = 65,536 towers (the bench config): every tower's logits equal the oracle on that tower
+    alone (sampled), and are identical to a run of the same tower in a small batch."""
+    B, N, S = 65536, 6, 5
+    params = O.random_params(6)
+    raw = D.synthetic_towers(B, N, seed=17)
+    obj = (raw / 170).astype(np.float32)
+    big = TowerBatch.fully_connected(obj, device="cuda")
+    flat = P.to_flat(params, device="cuda")
+    z = E.forward(flat, big, E.RunConfig(S), E.Workspace("cuda")).cpu().numpy().reshape(B, N)
+    pick = np.random.default_rng(0).choice(B, 24, replace=False)
+    Rs, Rr = O.relation_matrices(raw[pick], None)
+    tp = O.to_torch(params)
+    ref = O.forward_dense(tp, torch.tensor(obj[pick], dtype=torch.float64), torch.tensor(Rs, dtype=torch.float64),
+                          torch.tensor(Rr, dtype=torch.float64), torch.zeros(24, N, 100, dtype=torch.float64), S).numpy()
+    assert np.all(np.abs(z[pick] - ref) <= 1e-5 + 1e-5 * np.abs(ref))
+    small = TowerBatch.fully_connected(obj[pick], device="cuda")
+    zs = E.forward(flat, small, E.RunConfig(S), E.Workspace("cuda")).cpu().numpy().reshape(24, N)
+    assert np.array_equal(zs, z[pick])
+
+
+def test_gradient_linearity_over_shards():
+    """Σ over tower shards of (shard-mean loss grads × shard size) = full-batch grads × B."""
+    params = O.random_params(3)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(96, 6, seed=8, fully_connected=False)
+    full = TowerBatch.from_dense(obj, Rs, Rr, None, device="cuda")
+    _, _, gf, _ = _fwd_bwd(params, full, tgt, 5)
+    acc = {k: np.zeros_like(v) for k, v in gf.items()}
+    for sl in (slice(0, 40), slice(40, 96)):
+        b = TowerBatch.from_dense(obj[sl], Rs[sl], Rr[sl], None, device="cuda")
+        _, _, g, _ = _fwd_bwd(params, b, tgt[sl], 5)
+        for k in acc:
+            acc[k] += g[k] * (sl.stop - sl.start)
+    for k in acc:
+        assert np.abs(acc[k] / 96 - gf[k]).max() <= 1e-5 * np.abs(gf[k]).max() + 1e-8, k
+
+
+@pytest.mark.parametrize("nw", [None, 32])
+def test_ragged_batch_equals_per_size_runs(nw):
+    """Mixed 4–16-node towers in one batch (config 4's shape) = each size run on its own."""
+    params = O.random_params(4)
+    rng = np.random.default_rng(2)
+    sizes = rng.integers(4, 17, size=20)
+    towers = [D.synthetic_towers(1, int(n), seed=100 + i)[0] for i, n in enumerate(sizes)]
+    objs = [(t / 170).astype(np.float32) for t in towers]
+    rag = TowerBatch.ragged(objs, relation_threshold=170.0, raw_positions_list=towers, device="cuda", nw_max=nw)
+    flat = P.to_flat(params, device="cuda")
+    z = E.forward(flat, rag, E.RunConfig(5), E.Workspace("cuda")).cpu().numpy()
+    off = 0
+    tp = O.to_torch(params)
+    for t, o in zip(towers, objs):
+        Rs, Rr = O.relation_matrices(t[None], 170.0)
+        ref = O.forward_dense(tp, torch.tensor(o[None], dtype=torch.float64), torch.tensor(Rs, dtype=torch.float64),
+                              torch.tensor(Rr, dtype=torch.float64), torch.zeros(1, len(o), 100, dtype=torch.float64),
+                              5).numpy()[0]
+        got = z[off:off + len(o)]
+        assert np.all(np.abs(got - ref) <= 1e-5 + 1e-5 * np.abs(ref))
+        off += len(o)
+
+
+def test_trainer_step_matches_oracle_adam():
+    params = O.random_params(12)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(16, 6, seed=21, fully_connected=False)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, None, device="cuda")
+    flat = P.to_flat(params, device="cuda")
+    tr = Trainer(flat, mp_steps=5, dropout=0.0)
+    opt = O.KerasAdam()
+    ref = P.to_flat(params, dtype=torch.float64).numpy()
+    for _ in range(3):
+        tr.step(batch, torch.tensor(tgt.reshape(-1), device="cuda"))
+        _, _, g = O.loss_and_grads(P.from_flat(torch.tensor(ref)), obj, Rs, Rr, prop, tgt, 5)
+        ref = opt.step(ref, P.to_flat(g, dtype=torch.float64).numpy())
+    torch.cuda.synchronize()
+    got = flat.cpu().numpy()
+    assert np.abs(got - ref).max() < 2e-6     # 3 Adam steps of 5e-4-sized updates, fp32
+
+
+def test_keras_front_end_fit_and_predict():
+    """PropagationNetwork.getModel → fit/predict, the main.py:92-98 / JengaBuilder.py:328 call shapes."""
+    raw = D.synthetic_towers(96, 6, seed=31)
+    boxes = np.repeat(raw[:, None], 3, axis=1)
+    boxes[:48, 2, :, 1] -= 5.0               # half the towers move → unstable labels
+    x, y = D.training_arrays(boxes)
+    pn = PropagationNetwork(seed=0)
+    model = pn.getModel(n_objects=6, object_dim=3)
+    assert pn.getModel(6) is model
+    h = model.fit(x, y, batch_size=32, epochs=4, validation_split=0.25, shuffle=True, verbose=0)
+    assert len(h["loss"]) == 4 and h["loss"][-1] < h["loss"][0]
+    probs = model.predict({"objects": x["objects"][:5], "sender_relations": x["sender_relations"][:5],
+                           "receiver_relations": x["receiver_relations"][:5], "propagation": x["propagation"][:5]})
+    assert probs.shape == (5, 6, 1)
+    tp = O.to_torch(pn._net.keras_weights())
+    ref = O.forward_dense(tp, torch.tensor(x["objects"][:5], dtype=torch.float64),
+                          torch.tensor(x["sender_relations"][:5], dtype=torch.float64),
+                          torch.tensor(x["receiver_relations"][:5], dtype=torch.float64),
+                          torch.zeros(5, 6, 100, dtype=torch.float64), 5).numpy()
+    assert np.abs(probs[..., 0] - 1 / (1 + np.exp(-ref))).max() < 1e-5
+    m9 = pn.getModel(9)                      # a second size shares the weights (Networks.py:130-146)
+    assert m9.net is model.net
+
+
+def test_graph_network_module_autograd():
+    from spwgnn_amd import GraphNetwork
+    params = O.random_params(9)
+    net = GraphNetwork(mp_steps=3, dropout=0.0, params=params)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(4, 5, seed=2, fully_connected=False)
+    probs = net(obj, Rs, Rr, prop)
+    assert probs.shape == (4, 5, 1)
+    loss = torch.nn.functional.binary_cross_entropy(probs[..., 0], torch.tensor(tgt, device="cuda"))
+    loss.backward()
+    _, _, g = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, 3)
+    got = P.from_flat(net.flat.grad)
+    for k in g:
+        assert np.abs(got[k] - g[k]).max() <= 1e-5 * np.abs(g[k]).max() + 1e-7, k

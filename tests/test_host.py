@@ -1,0 +1,168 @@
+"""CPU: the C-ABI library loads and exports every declared symbol; host-side input builders
+(dense→edge conversion, wave-tile plan), parameter layout, and data builders vs the reference
+semantics (main.py:8-23, 66-81; JengaBuilder.py:137-192)."""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import model as O
+from spwgnn_amd import _lib, data as D, params as P
+from spwgnn_amd.batch import TowerBatch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "spwgnn.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(spwgnn_\w+)\s*\(", hdr, re.M))
+    assert len(declared) >= 15
+    lib = _lib.lib()
+    for name in sorted(declared):
+        assert hasattr(lib, name), name
+    assert lib.spwgnn_version() == 1
+    assert b"workspace" in lib.spwgnn_strerror(-4)
+
+
+def test_param_table_matches_reference_layout():
+    shapes = dict(O.param_shapes())
+    lay = P.layout()
+    assert [n for n, _, _ in lay] == [n for n, _ in O.param_shapes()]
+    for name, off, shape in lay:
+        assert tuple(shape) == tuple(shapes[name]), name
+        assert off % 64 == 0
+    assert P.real_size() == 209501  # rm 68,400 + om 10,400 + rmp 90,400 + omp 40,301
+    p = O.random_params(0)
+    back = P.from_flat(P.to_flat(p))
+    for k in p:
+        assert np.array_equal(back[k].astype(np.float32), p[k])
+
+
+def _c_dense_to_edges(Rs, Rr):
+    B, N, E = Rs.shape
+    Rs = np.ascontiguousarray(Rs, np.float32)
+    Rr = np.ascontiguousarray(Rr, np.float32)
+    src = np.zeros(B * E + 1, np.int32)
+    dst = np.zeros(B * E + 1, np.int32)
+    slot = np.zeros(B * E + 1, np.int32)
+    tec = np.zeros(B, np.int32)
+    n = C.c_int64()
+    st = _lib.lib().spwgnn_dense_to_edges(Rs.ctypes.data, Rr.ctypes.data, B, N, src.ctypes.data, dst.ctypes.data,
+                                          slot.ctypes.data, B * E, C.byref(n), tec.ctypes.data)
+    return st, src[:n.value], dst[:n.value], slot[:n.value], tec
+
+
+@pytest.mark.parametrize("fully", [True, False])
+def test_dense_to_edges_matches_reference_enumeration(fully):
+    raw = D.synthetic_towers(16, 7, seed=3)
+    Rs, Rr = O.relation_matrices(raw, None if fully else 170.0)
+    st, src, dst, slot, tec = _c_dense_to_edges(Rs, Rr)
+    assert st == 0
+    ref = O.dense_to_edges(Rs, Rr)
+    assert len(ref) == len(src) == tec.sum()
+    for (b, k, s, r), cs, cd, ck in zip(ref, src, dst, slot):
+        assert (cs, cd, ck) == (b * 7 + s, b * 7 + r, k)
+
+
+def test_dense_to_edges_rejects_non_onehot():
+    Rs, Rr = O.relation_matrices(D.synthetic_towers(2, 4, seed=1), None)
+    bad = Rs.copy()
+    bad[0, 1, 0] = 1.0            # two senders in one column
+    assert _c_dense_to_edges(bad, Rr)[0] == -3
+    bad = Rs.copy()
+    bad[0, :, 2] = 0.0            # receiver without sender
+    assert _c_dense_to_edges(bad, Rr)[0] == -3
+    half = Rr.copy()
+    half[1, :, 3] = 0.0           # sender without receiver: never summed → dropped
+    st, src, _, _, tec = _c_dense_to_edges(Rs, half)
+    assert st == 0 and tec[1] == 11 and tec[0] == 12
+
+
+@pytest.mark.parametrize("N,nw", [(6, None), (12, None), (4, 16), (3, 10)])
+def test_plan_invariants(N, nw):
+    B = 11
+    raw = D.synthetic_towers(B, N, seed=N)
+    Rs, Rr = O.relation_matrices(raw, 170.0)
+    b = TowerBatch.from_dense((raw / 170).astype(np.float32), Rs, Rr, device="cpu", nw_max=nw)
+    wt = b.wtile.numpy()
+    esrc, edst = b.edge_src.numpy(), b.edge_dst.numpy()
+    csr = b.blk_csr.numpy()
+    assert wt[:, 1].sum() == b.n_eblocks
+    seen = []
+    tower_of = np.repeat(np.arange(B), N)
+    node_cover = np.zeros(B * N, int)
+    for fb, nb, n0, nn in wt:
+        node_cover[n0:n0 + nn] += 1
+        assert nn <= b.nw_max
+        towers = set(tower_of[n0:n0 + nn])
+        assert all((tower_of == t).sum() == (tower_of[n0:n0 + nn] == t).sum() for t in towers)  # whole towers
+        for blk in range(fb, fb + nb):
+            s = esrc[blk * 32:(blk + 1) * 32]
+            d = edst[blk * 32:(blk + 1) * 32]
+            valid = s >= 0
+            assert np.all(valid[:valid.sum()])            # padding only at the end
+            assert np.all((s[valid] >= n0) & (s[valid] < n0 + nn)) and np.all((d[valid] >= n0) & (d[valid] < n0 + nn))
+            seen += list(zip(s[valid], d[valid]))
+            for base, key in ((0, d), (64, s)):
+                order = csr[blk, base:base + 32]
+                nodes = csr[blk, base + 32:base + 64]
+                assert sorted(order) == list(range(32))
+                nv = valid.sum()
+                assert np.all(nodes[nv:] == 255)
+                assert np.all(nodes[:nv] == key[order[:nv]] - n0)
+                assert np.all(np.diff(nodes[:nv].astype(int)) >= 0)
+    assert np.all(node_cover == 1)
+    assert sorted(seen) == sorted(zip(b.src, b.dst))
+
+
+def test_relation_matrices_vectorised_equals_reference_loop():
+    raw = D.synthetic_towers(9, 6, seed=5)
+    for thr in (None, 170.0, 120.0):
+        a = D.relation_matrices(raw, thr)
+        b = O.relation_matrices(raw, thr)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_synthetic_tower_geometry():
+    raw = D.synthetic_towers(200, 6, seed=0)
+    assert raw.shape == (200, 6, 3)
+    assert np.all((raw[..., 2] >= 50) & (raw[..., 2] <= 300))             # JengaBuilder.py:57-58
+    assert np.all(((raw[..., 1] - 110) % 80) == 0)                        # y = 70 + 40 + 80·layer
+    assert np.all(raw[..., 0] > 0)
+
+
+def test_calculate_stability_matches_reference_loop():
+    rng = np.random.default_rng(0)
+    boxes = rng.normal(0, 0.1, size=(5, 7, 4, 3)).cumsum(axis=1)
+    boxes[:, :, 0] = 3.0                   # a static object → stable
+    y = D.calculate_stability(boxes)
+    ref = np.zeros((5, 4, 1))
+    for o in range(4):                     # main.py:16-22
+        for t in range(5):
+            pc = sum(np.linalg.norm(boxes[t, f, o, 0:2] - boxes[t, f + 1, o, 0:2]) for f in range(0, 6))
+            ref[t, o, 0] = 1.0 if pc < 0.5 else 0.0
+    assert np.array_equal(y, ref)
+    assert np.all(y[:, 0, 0] == 1.0)
+
+
+def test_json_loader_pads_with_last_frame(tmp_path):
+    data = [[[[1, 2, 50], [1, 3, 50]], [[5, 6, 70]]], [], [[[0, 0, 60]], [[9, 9, 80], [9, 8, 80], [9, 7, 80]]]]
+    p = tmp_path / "jenga_model_3_2_x.txt"
+    p.write_text(json.dumps(data))
+    boxes = D.load_trajectories(str(p), 2)
+    assert boxes.shape == (2, 2, 2, 3)               # empty dropped; F = max len of object 0 (main.py:46-47)
+    assert np.array_equal(boxes[0, 1, 1], [5, 6, 70])  # padded with last frame (main.py:56-59)
+    assert np.array_equal(boxes[1, :, 1, 1], [9, 8])   # truncated to F frames
+    assert np.array_equal(boxes[1, 1, 0], [0, 0, 60])
+
+
+def test_training_arrays_layout():
+    boxes = np.repeat(D.synthetic_towers(3, 5, seed=2)[:, None], 4, axis=1)
+    x, y = D.training_arrays(boxes)
+    assert set(x) == {"objects", "sender_relations", "receiver_relations", "propagation"}   # main.py:92
+    assert x["objects"].shape == (3, 5, 3) and x["sender_relations"].shape == (3, 5, 20)
+    assert np.all(y["target"] == 1.0)                 # static trajectories are stable
+    assert np.allclose(x["objects"] * 170, boxes[:, 0])
