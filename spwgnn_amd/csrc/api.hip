@@ -42,7 +42,7 @@ struct Ws {
     int64_t dP_at(int k) const { return dP + (int64_t)(k & 1) * RN * kLdN; }
 };
 
-static constexpr int kMaxChunks = 768;
+static constexpr int kMaxChunks = 1024;
 static constexpr int kReduceGroups = 32;
 
 static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {

@@ -60,35 +60,55 @@ __device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh
 // in: C layout of the previous layer (feature rho(r,h)+32tp on the lane's row); the k-steps are
 // (tp, r) for tp < NT_IN, with r < LAST_R in the last input tile (rows beyond are zero padding).
 // W: [in][out] row-major with row stride LDW; the A operand of lane (i,h) is W[k(h)][32t + i].
-template <int NT_OUT, int NT_IN, int LAST_R, int LDW>
+// The weight fragments run PF k-steps ahead in a register ring (hipcc otherwise serialises each
+// load with its MFMA under register pressure — see DESIGN.md §3).
+template <int NT_OUT, int NT_IN, int LAST_R, int LDW, int PF = 3>
 __device__ __forceinline__ void tchain_acc(const f32x16 (&in)[NT_IN], f32x16 (&out)[NT_OUT],
                                            const float* __restrict__ W, int lane) {
     const int i = lane & 31, h = lane >> 5;
     const float* wbase = W + (4 * h) * LDW + i;
+    constexpr int NK = (NT_IN - 1) * 16 + LAST_R;
+    float w[PF + 1][NT_OUT];
 #pragma unroll
-    for (int tp = 0; tp < NT_IN; ++tp) {
+    for (int k = 0; k < PF; ++k) {
+        if (k >= NK) break;
+        const float* wrow = wbase + (rho(k & 15, 0) + 32 * (k >> 4)) * LDW;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (tp == NT_IN - 1 && r >= LAST_R) continue;
-            const float* wrow = wbase + (rho(r, 0) + 32 * tp) * LDW;
-            const float b = in[tp][r];
+        for (int t = 0; t < NT_OUT; ++t) w[k][t] = wrow[32 * t];
+    }
 #pragma unroll
-            for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wrow[32 * t], b, out[t]);
+    for (int k = 0; k < NK; ++k) {
+        if (k + PF < NK) {
+            const int kk = k + PF;
+            const float* wrow = wbase + (rho(kk & 15, 0) + 32 * (kk >> 4)) * LDW;
+#pragma unroll
+            for (int t = 0; t < NT_OUT; ++t) w[kk % (PF + 1)][t] = wrow[32 * t];
         }
+        const float b = in[k >> 4][k & 15];
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(w[k % (PF + 1)][t], b, out[t]);
     }
 }
 
 // ---- transposed orientation, B operand from a split-halves row chunk x (features KH*h + s).
-template <int NT_OUT, int KH, int LDW>
+template <int NT_OUT, int KH, int LDW, int PF = 3>
 __device__ __forceinline__ void tgemm_half_acc(const float (&x)[KH], f32x16 (&out)[NT_OUT],
                                                const float* __restrict__ W, int lane) {
     const int i = lane & 31, h = lane >> 5;
     const float* wbase = W + (KH * h) * LDW + i;
+    float w[PF + 1][NT_OUT];
+#pragma unroll
+    for (int k = 0; k < PF; ++k)
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) w[k][t] = wbase[k * LDW + 32 * t];
 #pragma unroll
     for (int s = 0; s < KH; ++s) {
-        const float* wrow = wbase + s * LDW;
+        if (s + PF < KH) {
 #pragma unroll
-        for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wrow[32 * t], x[s], out[t]);
+            for (int t = 0; t < NT_OUT; ++t) w[(s + PF) % (PF + 1)][t] = wbase[(s + PF) * LDW + 32 * t];
+        }
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(w[s % (PF + 1)][t], x[s], out[t]);
     }
 }
 

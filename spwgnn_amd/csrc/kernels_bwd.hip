@@ -50,7 +50,7 @@ __device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_k
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_node_bwd(NodeBwdArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node_bwd(NodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (nb * 32 >= a.n_nodes) return;
@@ -183,7 +183,7 @@ __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint
     }
 }
 
-__global__ __launch_bounds__(256, 2) void k_edge_bwd(EdgeBwdArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd(EdgeBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = threadIdx.x >> 6;
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(256, 2) void k_edge_bwd(EdgeBwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (blk >= a.n_eblocks) return;
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
     store_rho<5>(a.dz1 + row, E, h);
 }
 
-__global__ __launch_bounds__(256, 2) void k_enc_node_bwd(EncNodeBwdArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_node_bwd(EncNodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (nb * 32 >= a.n_nodes) return;

@@ -31,7 +31,7 @@ __global__ void k_prep_weights(PrepArgs a) {
 // ------------------------------------------------------------------------------------------------
 // om encoder: c_o = dropout(relu(om(y, w))), P0, U0 = P0·W1b, V0 = P0·W1c (transposed orientation,
 // 32 nodes per wave).
-__global__ __launch_bounds__(256, 2) void k_enc_node(EncNodeArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_node(EncNodeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int n = nb * 32 + j;
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node(EncNodeArgs a) {
 // rm encoder (transposed orientation, one 32-edge block per wave): d = pos[r]-pos[s] (2 feats)
 // → 150 → 150 → 150 → 150 (+relu, dropout) = c_r; A = c_r·W1a + b1 (step-invariant first-layer
 // term of rmp: W1·[c_r|P_s|P_r] = (c_r·W1a + b1) + P_s·W1b + P_r·W1c).
-__global__ __launch_bounds__(256, 2) void k_enc_edge(EncEdgeArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_edge(EncEdgeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (blk >= a.n_eblocks) return;
@@ -197,7 +197,7 @@ __device__ __forceinline__ void stage_pair(float* st, const f32x16 (&acc)[5], in
 
 // ------------------------------------------------------------------------------------------------
 // One propagation step, edge side (natural orientation, one wave-tile of whole towers per wave).
-__global__ __launch_bounds__(256, 2) void k_edge_fwd(EdgeFwdArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_fwd(EdgeFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = threadIdx.x >> 6;
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256, 2) void k_edge_fwd(EdgeFwdArgs a) {
 //   x' = o1·Wo2' + bo2'   (x' = x with the logit moved to column 100)
 //   P' = tanh(x'[0:100] + P); logit = x'[100]     (Networks.py:181, 184)
 //   U' = P'·W1b, V' = P'·W1c for the next step
-__global__ __launch_bounds__(256, 2) void k_node_fwd(NodeFwdArgs a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node_fwd(NodeFwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (nb * 32 >= a.n_nodes) return;

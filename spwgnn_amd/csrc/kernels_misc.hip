@@ -4,7 +4,7 @@
 
 namespace spw {
 
-constexpr int kWgThreads = 320;   // 5 waves: wave w owns output row tile w (32 x-features × all y tiles)
+constexpr int kWgThreads = 256;   // 4 waves; the TX×TY output tiles are dealt round-robin to waves
 
 __device__ __forceinline__ int64_t wg_phys(int64_t L, int64_t count, int64_t stride) {
     const int64_t s = L / count, n = L - s * count;
@@ -21,109 +21,231 @@ __device__ __forceinline__ float4 f4add3(float4 a, float4 b, float4 c) {
     return make_float4(a.x + b.x + c.x, a.y + b.y + c.y, a.z + b.z + c.z, a.w + b.w + c.w);
 }
 
-// 4 consecutive X features [f0, f0+4) of logical row L (all producers write zero padding up to ld)
+// Raw operand fetch, split in two phases so global-load latency overlaps the MFMAs:
+//   fetch_*  : issue the loads of one float4 group into registers (no use of the data)
+//   finish_* : combine the fetched registers into the staged value (after the MFMAs)
+struct XRaw { float4 a, u, v; int flag; };
+struct YRaw { float4 g; uint32_t bits; int flag; };
+
+// Row mapping of a 32-row block: logical row L = r0 + rr → (step s, row n) with n < count.
+// One 64-bit division per block (scalar), then a carry per row (count >= 1).
+struct RowBase { int64_t s0, n0, count; };
+__device__ __forceinline__ RowBase row_base(int64_t r0, int64_t count) {
+    const int64_t s0 = r0 / count;
+    return {s0, r0 - s0 * count, count};
+}
+__device__ __forceinline__ void row_at(const RowBase& b, int rr, int64_t& s, int64_t& n) {
+    s = b.s0;
+    n = b.n0 + rr;
+    while (n >= b.count) {   // at most once when count >= 32
+        n -= b.count;
+        ++s;
+    }
+}
+
 template <int XM>
-__device__ __forceinline__ float4 wg_x4(const WgradArgs& a, int64_t L, int f0) {
+__device__ __forceinline__ void fetch_x(const WgradArgs& a, const RowBase& rb, int rr, int f0, bool in, XRaw& r) {
+    r.flag = 0;
+    if (!in) return;
+    int64_t s, n;
+    row_at(rb, rr, s, n);
     if (XM == XM_ROW) {
-        const int64_t r = wg_phys(L, a.x_count, a.x_stride);
-        float4 v = f0 < a.x_ld ? *reinterpret_cast<const float4*>(a.x_ptr + r * a.x_ld + f0) : f4zero();
-        if (a.x_ones >= f0 && a.x_ones < f0 + 4) f4set(v, a.x_ones - f0, 1.f);
+        const int64_t row = (a.x_stride ? s * a.x_stride : 0) + n;
+        r.a = *reinterpret_cast<const float4*>(a.x_ptr + row * a.x_ld + f0);
+        r.flag = 1;
+    } else if (XM == XM_EDGE_D) {
+        const int sidx = a.esrc[n];
+        if (sidx >= 0 && f0 == 0) {
+            r.a = reinterpret_cast<const float4*>(a.pos)[sidx];
+            r.u = reinterpret_cast<const float4*>(a.pos)[a.edst[n]];
+            r.flag = 1;
+        }
+    } else if (XM == XM_NODE_O) {
+        if (f0 == 0) {
+            r.a = reinterpret_cast<const float4*>(a.pos)[n];
+            r.flag = 1;
+        }
+    } else {  // XM_EDGE_H1: (s, e = n); 32-row blocks never straddle a step (RE % 32 == 0)
+        const int e = (int)n;
+        const int sidx = a.esrc[e];
+        if (sidx >= 0 && f0 < 152) {
+            const int didx = a.edst[e];
+            const float* Us = a.U + s * a.RN * kLdE;
+            const float* Vs = a.V + s * a.RN * kLdE;
+            r.a = *reinterpret_cast<const float4*>(a.A + (uint32_t)(e * kLdE + f0));
+            r.u = *reinterpret_cast<const float4*>(Us + (uint32_t)(sidx * kLdE + f0));
+            r.v = *reinterpret_cast<const float4*>(Vs + (uint32_t)(didx * kLdE + f0));
+            r.flag = 1;
+        }
+    }
+}
+
+template <int XM>
+__device__ __forceinline__ float4 finish_x(const WgradArgs& a, int f0, const XRaw& r) {
+    if (XM == XM_ROW) {
+        float4 v = r.flag ? r.a : f4zero();
+        if (r.flag && a.x_ones >= f0 && a.x_ones < f0 + 4) f4set(v, a.x_ones - f0, 1.f);
         return v;
     } else if (XM == XM_EDGE_D) {
-        const int sidx = a.esrc[L];
-        float4 v = f4zero();
-        if (sidx >= 0 && f0 == 0) {
-            const float4 ps = reinterpret_cast<const float4*>(a.pos)[sidx];
-            const float4 pd = reinterpret_cast<const float4*>(a.pos)[a.edst[L]];
-            v = make_float4(pd.x - ps.x, pd.y - ps.y, 1.f, 0.f);
-        }
-        return v;
+        return r.flag ? make_float4(r.u.x - r.a.x, r.u.y - r.a.y, 1.f, 0.f) : f4zero();
     } else if (XM == XM_NODE_O) {
-        float4 v = f4zero();
-        if (f0 == 0) {
-            const float4 p = reinterpret_cast<const float4*>(a.pos)[L];
-            v = make_float4(p.y, p.z, 1.f, 0.f);
-        }
-        return v;
-    } else {  // XM_EDGE_H1
-        const int64_t s = L / a.RE, e = L - s * a.RE;
-        const int sidx = a.esrc[e];
-        if (sidx < 0) return f4zero();
-        const int didx = a.edst[e];
-        const float4 x = *reinterpret_cast<const float4*>(a.A + e * kLdE + f0);
-        const float4 u = *reinterpret_cast<const float4*>(a.U + (s * a.RN + sidx) * kLdE + f0);
-        const float4 w = *reinterpret_cast<const float4*>(a.V + (s * a.RN + didx) * kLdE + f0);
-        float4 v = f4relu(f4add3(x, u, w));
+        return r.flag ? make_float4(r.a.y, r.a.z, 1.f, 0.f) : f4zero();
+    } else {
+        if (!r.flag) return f4zero();
+        float4 v = f4relu(f4add3(r.a, r.u, r.v));
         if (f0 == 148) { v.z = 1.f; v.w = 0.f; }        // feature 150 = ones (b2), 151 = 0
-        else if (f0 >= 152) v = f4zero();
         return v;
     }
 }
 
 template <int YM>
-__device__ __forceinline__ float4 wg_y4(const WgradArgs& a, int64_t L, int f0) {
+__device__ __forceinline__ void fetch_y(const WgradArgs& a, const RowBase& rb, int rr, int f0, bool in, YRaw& r) {
+    r.flag = 0;
+    if (!in) return;
+    int64_t s, n;
+    row_at(rb, rr, s, n);
     if (YM == YM_ROW) {
-        const int64_t r = wg_phys(L, a.y_count, a.y_stride);
-        return f0 < a.y_ld ? *reinterpret_cast<const float4*>(a.y_ptr + r * a.y_ld + f0) : f4zero();
-    } else {  // YM_EDGE_DH2
-        const int64_t s = L / a.RE, e = L - s * a.RE;
+        const int64_t row = (a.y_stride ? s * a.y_stride : 0) + n;
+        r.g = *reinterpret_cast<const float4*>(a.y_ptr + row * a.y_ld + f0);
+        r.bits = 15u;
+        r.flag = 1;
+    } else {  // YM_EDGE_DH2: (s, e = n)
+        const int e = (int)n;
         const int didx = a.edst[e];
-        if (didx < 0 || f0 >= 152) return f4zero();
-        const uint32_t word = a.mask2[(s * (a.RE / 32) + (e >> 5)) * 160 + (f0 >> 5) * 32 + (e & 31)];
-        const uint32_t bits = word >> (f0 & 31);
-        const float4 g = *reinterpret_cast<const float4*>(a.G3 + (s * a.RN + didx) * kLdE + f0);
-        return make_float4((bits & 1u) ? g.x : 0.f, (bits & 2u) ? g.y : 0.f, (bits & 4u) ? g.z : 0.f,
-                           (bits & 8u) ? g.w : 0.f);
+        if (didx >= 0 && f0 < 152) {
+            const uint32_t* ms = a.mask2 + s * (a.RE / 32) * 160;
+            const uint32_t word = ms[(uint32_t)((e >> 5) * 160 + (f0 >> 5) * 32 + (e & 31))];
+            r.bits = word >> (f0 & 31);
+            const float* Gs = a.G3 + s * a.RN * kLdE;
+            r.g = *reinterpret_cast<const float4*>(Gs + (uint32_t)(didx * kLdE + f0));
+            r.flag = 1;
+        }
     }
 }
 
-// dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n]
+__device__ __forceinline__ float4 finish_y(const YRaw& r) {
+    if (!r.flag) return f4zero();
+    return make_float4((r.bits & 1u) ? r.g.x : 0.f, (r.bits & 2u) ? r.g.y : 0.f, (r.bits & 4u) ? r.g.z : 0.f,
+                       (r.bits & 8u) ? r.g.w : 0.f);
+}
+
+// dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n].
+// Software pipeline per 32-row block: [barrier] write staged regs → LDS [barrier] issue the
+// next block's loads → MFMAs on the LDS block (the loads land meanwhile).
 template <int XM, int YM, int KXP, int NYP>
-__global__ __launch_bounds__(kWgThreads) void k_wgrad_t(WgradArgs a) {
+__global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     constexpr int TX = KXP / 32, TY = NYP / 32;
-    constexpr int LDX = KXP + 4, LDY = NYP + 4;   // 16-B aligned rows; MFMA reads are conflict-free
+    constexpr int NT = TX * TY;                    // output tiles
+    constexpr int TPW = (NT + 3) / 4;              // tiles per wave (max)
+    constexpr int LDX = KXP + 4, LDY = NYP + 4;    // 16-B aligned rows; MFMA reads are conflict-free
     constexpr int GX = KXP / 4, GY = NYP / 4;
+    constexpr int NGX = (32 * GX + kWgThreads - 1) / kWgThreads;   // float4 groups per thread
+    constexpr int NGY = (32 * GY + kWgThreads - 1) / kWgThreads;
     __shared__ __attribute__((aligned(16))) float Xs[32 * LDX];
     __shared__ __attribute__((aligned(16))) float Ys[32 * LDY];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
     const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
-    f32x16 acc[TY];
+    f32x16 acc[TPW];
 #pragma unroll
-    for (int t = 0; t < TY; ++t) acc[t] = zero16();
+    for (int t = 0; t < TPW; ++t) acc[t] = zero16();
+    // the recomputed-h1 operand (3 gathers per group) is fetched in the write phase instead of a
+    // block ahead: holding its raw registers across the MFMAs would spill
+    constexpr bool PFX = (XM != XM_EDGE_H1);
+    XRaw xr[NGX];
+    YRaw yr[NGY];
+    const int64_t xcount = (XM == XM_ROW) ? a.x_count : (XM == XM_EDGE_H1 ? a.RE : a.rows);
+    const int64_t ycount = (YM == YM_ROW) ? a.y_count : a.RE;
+    auto fetch_xs = [&](int64_t r0) {
+        const RowBase xb = row_base(r0, xcount);
+#pragma unroll
+        for (int k = 0; k < NGX; ++k) {
+            const int g = tid + k * kWgThreads;
+            const int rr = g / GX, c4 = g - rr * GX;
+            fetch_x<XM>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
+        }
+    };
+    auto fetch_ys = [&](int64_t r0) {
+        const RowBase yb = row_base(r0, ycount);
+#pragma unroll
+        for (int k = 0; k < NGY; ++k) {
+            const int g = tid + k * kWgThreads;
+            const int rr = g / GY, c4 = g - rr * GY;
+            fetch_y<YM>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
+        }
+    };
+    auto fetch = [&](int64_t r0) {
+        if (PFX) fetch_xs(r0);
+        fetch_ys(r0);
+    };
+    fetch(r_begin);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
+        if (PFX) {
 #pragma unroll
-        for (int g = tid; g < 32 * GX; g += kWgThreads) {
-            const int rr = g / GX, c4 = g - rr * GX;
-            const int64_t L = r0 + rr;
-            const float4 v = L < r_end ? wg_x4<XM>(a, L, 4 * c4) : f4zero();
-            *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = v;
+            for (int k = 0; k < NGX; ++k) {
+                const int g = tid + k * kWgThreads;
+                if (g < 32 * GX) {
+                    const int rr = g / GX, c4 = g - rr * GX;
+                    *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
+                }
+            }
+        } else {
+            // two groups in flight at a time (bounded registers)
+            const RowBase xb = row_base(r0, xcount);
+#pragma unroll
+            for (int k0 = 0; k0 < NGX; k0 += 2) {
+#pragma unroll
+                for (int k = k0; k < k0 + 2 && k < NGX; ++k) {
+                    const int g = tid + k * kWgThreads;
+                    const int rr = g / GX, c4 = g - rr * GX;
+                    fetch_x<XM>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
+                }
+#pragma unroll
+                for (int k = k0; k < k0 + 2 && k < NGX; ++k) {
+                    const int g = tid + k * kWgThreads;
+                    if (g < 32 * GX) {
+                        const int rr = g / GX, c4 = g - rr * GX;
+                        *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
 #pragma unroll
-        for (int g = tid; g < 32 * GY; g += kWgThreads) {
-            const int rr = g / GY, c4 = g - rr * GY;
-            const int64_t L = r0 + rr;
-            const float4 v = L < r_end ? wg_y4<YM>(a, L, 4 * c4) : f4zero();
-            *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = v;
+        for (int k = 0; k < NGY; ++k) {
+            const int g = tid + k * kWgThreads;
+            if (g < 32 * GY) {
+                const int rr = g / GY, c4 = g - rr * GY;
+                *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = finish_y(yr[k]);
+            }
         }
         __syncthreads();
-        if (wave < TX) {
+        if (r0 + 32 < r_end) fetch(r0 + 32);
+#pragma unroll 2
+        for (int k2 = 0; k2 < 16; ++k2) {
+            const int rr = 2 * k2 + h;
 #pragma unroll
-            for (int k2 = 0; k2 < 16; ++k2) {
-                const int rr = 2 * k2 + h;
-                const float av = Xs[rr * LDX + 32 * wave + i];
-#pragma unroll
-                for (int ty = 0; ty < TY; ++ty) acc[ty] = mfma32(av, Ys[rr * LDY + 32 * ty + i], acc[ty]);
+            for (int u = 0; u < TPW; ++u) {
+                const int tile = wave + 4 * u;      // wave-uniform
+                if (tile < NT) {
+                    const int ti = tile / TY, tj = tile - ti * TY;
+                    acc[u] = mfma32(Xs[rr * LDX + 32 * ti + i], Ys[rr * LDY + 32 * tj + i], acc[u]);
+                }
             }
         }
     }
-    if (wave < TX) {
-        float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
+    float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
 #pragma unroll
-        for (int ty = 0; ty < TY; ++ty)
+    for (int u = 0; u < TPW; ++u) {
+        const int tile = wave + 4 * u;
+        if (tile < NT) {
+            const int ti = tile / TY, tj = tile - ti * TY;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) out[(int64_t)(32 * wave + rho(r, 0) + 4 * h) * NYP + 32 * ty + i] = acc[ty][r];
+            for (int r = 0; r < 16; ++r)
+                out[(int64_t)(32 * ti + rho(r, 0) + 4 * h) * NYP + 32 * tj + i] = acc[u][r];
+        }
     }
 }
 
