@@ -24,9 +24,10 @@ def _ptr(a: np.ndarray) -> int:
 
 
 def default_nw_max(max_nodes: int) -> int:
-    """Nodes per wave-tile: at least one whole tower, at least ~10 nodes so small towers share a
-    wave (bounded by the LDS node accumulators)."""
-    return int(min(_NW_LIMIT, max(max_nodes, 10)))
+    """Nodes per wave-tile: at least one whole tower. Up to 16 nodes the backward segment sums run
+    as one one-hot matrix product (receiver rows 0-15, sender rows 16-31), so small towers are
+    packed up to 16 nodes per wave; larger towers take one wave-tile each (≤ 32 nodes)."""
+    return 16 if max_nodes <= 16 else int(min(_NW_LIMIT, max_nodes))
 
 
 _NW_LIMIT = 32

@@ -289,7 +289,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         EdgeFwdArgs ef{};
         ef.n_wtiles = b->n_wtiles;
         ef.nw_max = b->nw_max;
-        ef.wpg = edge_wpg(edge_fwd_lds_per_wave(b->nw_max));
+        ef.wpg = 4;
         ef.wtile = b->wtile;
         ef.esrc = b->edge_src;
         ef.edst = b->edge_dst;
@@ -449,7 +449,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         EdgeBwdArgs eb{};
         eb.n_wtiles = b->n_wtiles;
         eb.nw_max = b->nw_max;
-        eb.wpg = edge_wpg(edge_bwd_lds_per_wave(b->nw_max));
+        eb.wpg = b->nw_max <= 16 ? 4 : edge_wpg(edge_bwd_lds_per_wave(b->nw_max));
         eb.dA_accumulate = !first;
         eb.wtile = b->wtile;
         eb.esrc = b->edge_src;

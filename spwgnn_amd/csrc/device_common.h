@@ -44,6 +44,15 @@ __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 __device__ __forceinline__ uint32_t writelane(uint32_t val, int ln, uint32_t old) {
     return ((int)(threadIdx.x & 63) == ln) ? val : old;
 }
+// v_writelane_b32 with a compile-time lane (ln must fold to a constant after unrolling; a uniform
+// SGPR value goes straight into one lane: 1 VALU instead of a compare + select). The compiler does
+// not see the SGPR read inside the asm: a v_cmp writing the SGPR right before it is read stale
+// without a wait state (measured on gfx950: tools/wltest), hence the s_nop.
+__device__ __forceinline__ uint32_t writelane_imm(uint32_t val, int ln, uint32_t old) {
+    uint32_t r;
+    asm volatile("s_nop 1\n\tv_writelane_b32 %0, %1, %2" : "=v"(r) : "s"(val), "i"(ln), "0"(old));
+    return r;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Dropout key (our own counter-based RNG; Keras' TF draws cannot be reproduced — DESIGN.md §6).

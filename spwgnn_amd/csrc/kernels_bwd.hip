@@ -183,20 +183,34 @@ __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint
     }
 }
 
+// ONEHOT (wave-tiles of ≤ 16 nodes): both segment sums run on the matrix core as one product
+//   nacc[t] += onehot·dh1pre[t],  A operand of lane (m, h) at k-step r (edge e = rho(r,h)):
+//   m < 16: [dst(e) == n0+m] (receiver sum → dV),  m ≥ 16: [src(e) == n0+m−16] (sender sum → dU);
+// otherwise (up to 32 nodes) the sums walk the block csr through a per-wave LDS stage.
+// dA (Σ over steps of dh1pre) is written by the first backward step and accumulated by the later
+// ones with no-return float atomics (one add per element per launch, launches stream-ordered:
+// the summation order is fixed, so the result stays deterministic).
+template <bool ONEHOT>
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd(EdgeBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wt = blockIdx.x * a.wpg + wave;
     if (wt >= a.n_wtiles) return;
+    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     float* st = smem + wave * (2112 + 2 * a.nw_max * kLdE);
     float* naccR = st + 2112;
     float* naccS = naccR + a.nw_max * kLdE;
-    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
-    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
-    for (int idx = lane; idx < nn * kLdE; idx += 64) {
-        naccR[idx] = 0.f;
-        naccS[idx] = 0.f;
+    f32x16 nacc[5];
+    const int key = n0 + (i & 15);
+    if (ONEHOT) {
+        zero_tiles(nacc);
+    } else {
+        for (int idx = lane; idx < nn * kLdE; idx += 64) {
+            naccR[idx] = 0.f;
+            naccS[idx] = 0.f;
+        }
     }
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
@@ -208,47 +222,44 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
         uint32_t w[5];
 #pragma unroll
-        for (int t = 0; t < 5; ++t) w[t] = m2[32 * t];
+        for (int t = 0; t < 5; ++t) w[t] = valid ? m2[32 * t] : 0u;
+        // this lane's 76 feature bits (features 76h + 0..75) as a 64-bit low part and 12-bit tail
+        const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
+                                    : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
+        const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
         const float4* G4 = reinterpret_cast<const float4*>(a.G3 + (int64_t)dc * kLdE + kKhE * h);
         f32x16 acc[5];
         zero_tiles(acc);
         const float* wbase = a.w2t + (kKhE * h) * kLdE + i;
-        float wc[4][5], wn[4][5];
+        // one W fragment set, each k-step's fragments reloaded right after their MFMAs issue
+        float wf[4][5];
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int t = 0; t < 5; ++t) wc[c][t] = wbase[c * kLdE + 32 * t];
-        float4 nxt = G4[0];
-#pragma unroll 1
-        for (int q = 0; q < kKhE / 4; ++q) {
-            const float4 cur = nxt;
-            if (q + 1 < kKhE / 4) {
-                const float* wrow = wbase + (4 * q + 4) * kLdE;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-#pragma unroll
-                    for (int t = 0; t < 5; ++t) wn[c][t] = wrow[c * kLdE + 32 * t];
-                nxt = G4[q + 1];
-            }
-            // 4 features f0..f0+3 (f0 = 76h + 4q) share one mask word (f0 % 4 == 0)
-            const int f0 = kKhE * h + 4 * q;
-            const int wi = f0 >> 5;
-            const uint32_t wd = wi == 0 ? w[0] : wi == 1 ? w[1] : wi == 2 ? w[2] : wi == 3 ? w[3] : w[4];
-            const uint32_t bits = valid ? (wd >> (f0 & 31)) : 0u;
+            for (int t = 0; t < 5; ++t) wf[c][t] = wbase[c * kLdE + 32 * t];
+        float4 g = G4[0];
+        auto chunk = [&](int q, bool more) {
+            const uint32_t bits = (uint32_t)(q < 16 ? mlo >> (4 * q) : (uint64_t)(mhi >> (4 * q - 64)));
             float xv[4];
-            xv[0] = (bits & 1u) ? cur.x : 0.f;
-            xv[1] = (bits & 2u) ? cur.y : 0.f;
-            xv[2] = (bits & 4u) ? cur.z : 0.f;
-            xv[3] = (bits & 8u) ? cur.w : 0.f;
+            xv[0] = (bits & 1u) ? g.x : 0.f;
+            xv[1] = (bits & 2u) ? g.y : 0.f;
+            xv[2] = (bits & 4u) ? g.z : 0.f;
+            xv[3] = (bits & 8u) ? g.w : 0.f;
+            if (more) g = G4[q + 1];
+            const float* wrow = wbase + (4 * q + 4) * kLdE;
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < 4; ++c) {
 #pragma unroll
-                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wc[c][t], acc[t]);
+                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wf[c][t], acc[t]);
+                if (more) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int t = 0; t < 5; ++t) wc[c][t] = wn[c][t];
-        }
+                    for (int t = 0; t < 5; ++t) wf[c][t] = wrow[c * kLdE + 32 * t];
+                }
+            }
+        };
+#pragma unroll 1
+        for (int q = 0; q < kKhE / 4 - 1; ++q) chunk(q, true);
+        chunk(kKhE / 4 - 1, false);
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
         const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
         float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
@@ -258,36 +269,68 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = rho(r, 0) + 4 * h;
-                float v = ((mw >> row) & 1u) ? acc[t][r] : 0.f;
-                float* p = dArow + row * kLdE + 32 * t;
-                if (a.dA_accumulate) v = *p + v;
-                *p = v;
                 acc[t][r] = ((mw >> row) & 1u) ? acc[t][r] : 0.f;
             }
         }
-        // segment sums: receiver → dV, sender → dU
-        const uint32_t csrw = reinterpret_cast<const uint32_t*>(a.csr)[(int64_t)blk * 32 + i];
+        if (a.dA_accumulate) {
 #pragma unroll
-        for (int rd = 0; rd < 3; ++rd) {
+            for (int t = 0; t < 5; ++t)
 #pragma unroll
-            for (int slot = 0; slot < 2; ++slot) {
-                const int t = 2 * rd + slot;
-                if (t >= 5) continue;
+                for (int r = 0; r < 16; ++r) unsafeAtomicAdd(dArow + (rho(r, 0) + 4 * h) * kLdE + 32 * t, acc[t][r]);
+        } else {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = acc[t][r];
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) dArow[(rho(r, 0) + 4 * h) * kLdE + 32 * t] = acc[t][r];
+        }
+        if (ONEHOT) {  // segment sums on the matrix core (padding edges: src = dst = -1, no match)
+            const int s = a.esrc[e];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d0 = __builtin_amdgcn_readlane(d, rho(r, 0)), d1 = __builtin_amdgcn_readlane(d, rho(r, 1));
+                const int s0 = __builtin_amdgcn_readlane(s, rho(r, 0)), s1 = __builtin_amdgcn_readlane(s, rho(r, 1));
+                const int node = i < 16 ? (h ? d1 : d0) : (h ? s1 : s0);
+                const float oh = node == key ? 1.f : 0.f;
+#pragma unroll
+                for (int t = 0; t < 5; ++t) nacc[t] = mfma32(oh, acc[t][r], nacc[t]);
             }
-            wave_lds_sync();
-            const int t = 2 * rd + h;
-            segsum_walk_b<0>(st, naccR, csrw, t, t < 5, lane);
-            segsum_walk_b<16>(st, naccS, csrw, t, t < 5, lane);
-            wave_lds_sync();
+        } else {  // segment sums: receiver → dV, sender → dU
+            const uint32_t csrw = reinterpret_cast<const uint32_t*>(a.csr)[(int64_t)blk * 32 + i];
+#pragma unroll
+            for (int rd = 0; rd < 3; ++rd) {
+#pragma unroll
+                for (int slot = 0; slot < 2; ++slot) {
+                    const int t = 2 * rd + slot;
+                    if (t >= 5) continue;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = acc[t][r];
+                }
+                wave_lds_sync();
+                const int t = 2 * rd + h;
+                segsum_walk_b<0>(st, naccR, csrw, t, t < 5, lane);
+                segsum_walk_b<16>(st, naccS, csrw, t, t < 5, lane);
+                wave_lds_sync();
+            }
         }
     }
-    float* oU = a.dU + (int64_t)n0 * kLdE;
-    float* oV = a.dV + (int64_t)n0 * kLdE;
-    for (int idx = lane; idx < nn * kLdE; idx += 64) {
-        oU[idx] = naccS[idx];
-        oV[idx] = naccR[idx];
+    if (ONEHOT) {  // nacc[t] reg r = row rho(r,h): rows 0..15 receiver nodes, 16..31 sender nodes
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = rho(r, 0) + 4 * h;
+            const int node = row & 15;
+            if (node < nn) {
+                float* o = (row < 16 ? a.dV : a.dU) + (int64_t)(n0 + node) * kLdE + i;
+#pragma unroll
+                for (int t = 0; t < 5; ++t) o[32 * t] = nacc[t][r];
+            }
+        }
+    } else {
+        float* oU = a.dU + (int64_t)n0 * kLdE;
+        float* oV = a.dV + (int64_t)n0 * kLdE;
+        for (int idx = lane; idx < nn * kLdE; idx += 64) {
+            oU[idx] = naccS[idx];
+            oV[idx] = naccR[idx];
+        }
     }
 }
 
@@ -365,8 +408,13 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st) {
-    const size_t lds = edge_bwd_lds_per_wave(a.nw_max) * a.wpg;
-    hipLaunchKernelGGL(k_edge_bwd, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+    if (a.nw_max <= 16) {
+        if (a.wpg != 4) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_edge_bwd<true>, dim3((a.n_wtiles + 3) / 4), dim3(256), 0, st, a);
+    } else {
+        const size_t lds = edge_bwd_lds_per_wave(a.nw_max) * a.wpg;
+        hipLaunchKernelGGL(k_edge_bwd<false>, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+    }
     return hipGetLastError();
 }
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st) {

@@ -151,63 +151,22 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Segment sum of a C-layout tile pair through a per-wave LDS stage (deterministic: each node's
-// edges are summed in csr order, blocks in order). st: [2][32][33]; csrw = this lane's word of
-// the block's 128-byte csr; word_base 0 = receiver tables, 16 = sender tables.
-template <int WORD_BASE>
-__device__ __forceinline__ void segsum_walk(const float* st, float* nacc, uint32_t csrw, int t, bool tv, int lane) {
-    const int i = lane & 31, h = lane >> 5;
-    // all LDS reads first (independent, pipelined), then the ordered per-node sums
-    float vals[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const uint32_t ow = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + (k >> 2));
-        const int eo = (ow >> (8 * (k & 3))) & 31;
-        vals[k] = st[h * 1056 + eo * 33 + i];
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + (k >> 2));
-        const int nd = (nw >> (8 * (k & 3))) & 255;
-        if (nd == 255) break;
-        sum += vals[k];
-        int ndn = 255;
-        if (k < 31) {
-            const uint32_t nw2 = (uint32_t)__builtin_amdgcn_readlane((int)csrw, WORD_BASE + 8 + ((k + 1) >> 2));
-            ndn = (nw2 >> (8 * ((k + 1) & 3))) & 255;
-        }
-        if (ndn != nd) {
-            if (tv) nacc[nd * kLdE + 32 * t + i] += sum;
-            sum = 0.f;
-        }
-    }
-}
-
-__device__ __forceinline__ void stage_pair(float* st, const f32x16 (&acc)[5], int t0, int lane) {
-    const int i = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int slot = 0; slot < 2; ++slot) {
-        const int t = t0 + slot;
-        if (t >= 5) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = acc[t][r];
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
 // One propagation step, edge side (natural orientation, one wave-tile of whole towers per wave).
+// The receiver segment sum (Networks.py:178 dot(receiver_relations, x)) runs on the matrix core:
+// C reg r of tile t holds h2[edge rho(r,h)][feature 32t+i], which is exactly the B operand of
+// k-step r of  nacc[t] += onehot·h2  when the A operand of lane (m, h) is
+// [dst(edge rho(r,h)) == node n0+m].  16 k-steps × 5 tiles per block; the wave-tile's node rows
+// stay in registers (≤ 32 nodes): no LDS, fixed summation order (deterministic).
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_fwd(EdgeFwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
-    const int wave = threadIdx.x >> 6;
-    const int wt = blockIdx.x * a.wpg + wave;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wt = blockIdx.x * 4 + wave;
     if (wt >= a.n_wtiles) return;
-    float* st = smem + wave * (2112 + a.nw_max * kLdE);
-    float* nacc = st + 2112;
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
-    for (int idx = lane; idx < nn * kLdE; idx += 64) nacc[idx] = 0.f;
+    const int key = n0 + i;  // node of this lane's one-hot row
+    f32x16 nacc[5];
+    zero_tiles(nacc);
 
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
@@ -223,62 +182,58 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const float4* A4 = reinterpret_cast<const float4*>(a.A + e * kLdE + kKhE * h);
         const float4* U4 = reinterpret_cast<const float4*>(a.U + (int64_t)sc * kLdE + kKhE * h);
         const float4* V4 = reinterpret_cast<const float4*>(a.V + (int64_t)dc * kLdE + kKhE * h);
-        const bool want_m1 = a.mask1 != nullptr;
-        uint32_t mw0 = 0, mw1 = 0, mw2 = 0;
+        // h1 > 0 bits (mask1: word per (block, feature), bit = edge): each chunk's 8 ballots go
+        // into lanes 0..7 of one staging register (lanes 0-3: features 4q+c, lanes 4-7: 76+4q+c)
+        // and are stored straight away.
+        uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
+        const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         f32x16 acc[5];
         zero_tiles(acc);
         const float* wbase = a.w2 + (kKhE * h) * kLdE + i;
-        float wc[4][5], wn[4][5];
+        // one W fragment set (4 k-steps × 5 tiles); each k-step's fragments are reloaded for the next
+        // chunk right after their MFMAs issue (one chunk of latency cover, 20 registers)
+        float w[4][5];
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int t = 0; t < 5; ++t) wc[c][t] = wbase[c * kLdE + 32 * t];
+            for (int t = 0; t < 5; ++t) w[c][t] = wbase[c * kLdE + 32 * t];
         float4 pa = A4[0], pu = U4[0], pv = V4[0];
-#pragma unroll 1
-        for (int q = 0; q < kKhE / 4; ++q) {
-            const float4 ca = pa, cu = pu, cv = pv;
-            if (q + 1 < kKhE / 4) {
-                const float* wrow = wbase + (4 * q + 4) * kLdE;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-#pragma unroll
-                    for (int t = 0; t < 5; ++t) wn[c][t] = wrow[c * kLdE + 32 * t];
+        auto chunk = [&](int q, bool more) {
+            float xv[4];
+            xv[0] = relu(pa.x + pu.x + pv.x) * vf;
+            xv[1] = relu(pa.y + pu.y + pv.y) * vf;
+            xv[2] = relu(pa.z + pu.z + pv.z) * vf;
+            xv[3] = relu(pa.w + pu.w + pv.w) * vf;
+            if (more) {
                 pa = A4[q + 1];
                 pu = U4[q + 1];
                 pv = V4[q + 1];
             }
-            float xv[4];
-            xv[0] = relu(ca.x + cu.x + cv.x) * vf;
-            xv[1] = relu(ca.y + cu.y + cv.y) * vf;
-            xv[2] = relu(ca.z + cu.z + cv.z) * vf;
-            xv[3] = relu(ca.w + cu.w + cv.w) * vf;
+            const float* wrow = wbase + (4 * q + 4) * kLdE;
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < 4; ++c) {
 #pragma unroll
-                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wc[c][t], acc[t]);
-            if (want_m1) {  // h1 > 0 bits: word per (block, feature), bit = edge; feature f → lane f&63
+                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], w[c][t], acc[t]);
+                if (more) {
+#pragma unroll
+                    for (int t = 0; t < 5; ++t) w[c][t] = wrow[c * kLdE + 32 * t];
+                }
+            }
+            if (mrow) {
+                uint32_t stg = 0u;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const uint64_t bal = __ballot(xv[c] > 0.f);
-                    const int f0 = 4 * q + c, f1 = kKhE + 4 * q + c;
-                    const uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
-                    if (f0 < 64) mw0 = writelane(lo, f0, mw0);
-                    else mw1 = writelane(lo, f0 - 64, mw1);
-                    if (f1 < 128) mw1 = writelane(hi, f1 - 64, mw1);
-                    else mw2 = writelane(hi, f1 - 128, mw2);
+                    stg = writelane_imm((uint32_t)bal, c, stg);
+                    stg = writelane_imm((uint32_t)(bal >> 32), 4 + c, stg);
                 }
+                if (lane < 8) mrow[m1off + 4 * q] = stg;
             }
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int t = 0; t < 5; ++t) wc[c][t] = wn[c][t];
-        }
-        if (want_m1) {
-            uint32_t* mrow = a.mask1 + (int64_t)blk * kLdE;
-            mrow[lane] = mw0;
-            mrow[64 + lane] = mw1;
-            if (lane < 32) mrow[128 + lane] = lane < 24 ? mw2 : 0u;
-        }
+        };
+#pragma unroll 1
+        for (int q = 0; q < kKhE / 4 - 1; ++q) chunk(q, true);
+        chunk(kKhE / 4 - 1, false);
+        if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const float b = a.b2[32 * t + i];
@@ -299,27 +254,33 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 for (int r = 0; r < 16; ++r) {
                     const uint64_t bal = __ballot(acc[t][r] > 0.f);
                     const int w0 = t * 32 + rho(r, 0), w1 = t * 32 + rho(r, 1);
-                    mw[w0 >> 6] = writelane((uint32_t)bal, w0 & 63, mw[w0 >> 6]);
-                    mw[w1 >> 6] = writelane((uint32_t)(bal >> 32), w1 & 63, mw[w1 >> 6]);
+                    mw[w0 >> 6] = writelane_imm((uint32_t)bal, w0 & 63, mw[w0 >> 6]);
+                    mw[w1 >> 6] = writelane_imm((uint32_t)(bal >> 32), w1 & 63, mw[w1 >> 6]);
                 }
             m2row[lane] = mw[0];
             m2row[64 + lane] = mw[1];
             if (lane < 32) m2row[128 + lane] = mw[2];
         }
-        // receiver segment sum (Networks.py:178 dot(receiver_relations, x)) into LDS node rows
-        const uint32_t csrw = a.csr[(int64_t)blk * 32 + i];
+        // receiver segment sum on the matrix core (padding edges have dst -1: no match)
 #pragma unroll
-        for (int rd = 0; rd < 3; ++rd) {
-            stage_pair(st, acc, 2 * rd, lane);
-            wave_lds_sync();
-            const int t = 2 * rd + h;
-            segsum_walk<0>(st, nacc, csrw, t, t < 5, lane);
-            wave_lds_sync();
+        for (int r = 0; r < 16; ++r) {
+            const int d0 = __builtin_amdgcn_readlane(d, rho(r, 0)), d1 = __builtin_amdgcn_readlane(d, rho(r, 1));
+            const float oh = ((h ? d1 : d0) == key) ? 1.f : 0.f;
+#pragma unroll
+            for (int t = 0; t < 5; ++t) nacc[t] = mfma32(oh, acc[t][r], nacc[t]);
         }
     }
-    // write the wave-tile's node rows (each node is owned by exactly one wave-tile)
-    float* out = a.H2s + (int64_t)n0 * kLdE;
-    for (int idx = lane; idx < nn * kLdE; idx += 64) out[idx] = nacc[idx];
+    // the wave-tile's node rows (each node is owned by exactly one wave-tile):
+    // nacc[t] reg r = node rho(r,h), feature 32t+i
+    float* out = a.H2s + (int64_t)n0 * kLdE + i;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int node = rho(r, 0) + 4 * h;
+        if (node < nn) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t) out[node * kLdE + 32 * t] = nacc[t][r];
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -412,8 +373,8 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st) {
-    const size_t lds = edge_fwd_lds_per_wave(a.nw_max) * a.wpg;
-    hipLaunchKernelGGL(k_edge_fwd, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+    if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
+    hipLaunchKernelGGL(k_edge_fwd, dim3((a.n_wtiles + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st) {

@@ -58,12 +58,15 @@ def test_forward_parity_sizes(N):
     assert np.all(np.abs(got - ref) <= LOGIT_ATOL + LOGIT_RTOL * np.abs(ref)), np.abs(got - ref).max()
 
 
-def test_backward_parity_small():
+# (towers, nodes, nw_max): nw_max <= 16 runs the backward segment sums as a one-hot matrix product,
+# larger wave-tiles walk the block csr through LDS — both paths, single- and multi-tower tiles.
+@pytest.mark.parametrize("T,N,nw", [(6, 6, None), (6, 6, 6), (5, 16, None), (7, 5, 32), (3, 20, None), (2, 32, None)])
+def test_backward_parity_small(T, N, nw):
     params = O.random_params(seed=7)
-    obj, Rs, Rr, prop, tgt = D.synthetic_batch(6, 6, seed=2, fully_connected=False)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(T, N, seed=2, fully_connected=False)
     S = 5
     loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, S)
-    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda", nw_max=nw)
     flat, ws, z = _gpu_forward(params, batch, S, training=True)
     scratch = E.BceScratch("cuda")
     out3, dz = E.bce(z, torch.tensor(tgt, device="cuda").reshape(-1), scratch)

@@ -1,0 +1,47 @@
+"""Summarise rocprofv3 --pmc passes: per kernel, the average counter value per dispatch.
+
+usage: python tools_pmcsum.py OUT.json DIR [DIR ...]   (each DIR holds run_counter_collection.csv)
+FETCH_SIZE / WRITE_SIZE are reported in KiB by rocprofv3; the summary also carries bytes with the
+gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reads half of wide streaming reads: ×2).
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def short(name: str) -> str:
+    n = name.split("(")[0]
+    for pre in ("void ", "spw::"):
+        n = n.replace(pre, "")
+    return n.strip()
+
+
+def main():
+    out = sys.argv[1]
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in sys.argv[2:]:
+        per = collections.defaultdict(float)
+        meta = {}
+        with open(f"{d}/run_counter_collection.csv") as f:
+            for r in csv.DictReader(f):
+                key = (r["Dispatch_Id"], r["Counter_Name"])
+                per[key] += float(r["Counter_Value"])
+                meta[r["Dispatch_Id"]] = short(r["Kernel_Name"])
+        for (disp, ctr), v in per.items():
+            acc[meta[disp]][ctr].append(v)
+    res = {}
+    for k, ctrs in acc.items():
+        res[k] = {c: sum(v) / len(v) for c, v in ctrs.items()}
+        res[k]["dispatches"] = max(len(v) for v in ctrs.values())
+        if "FETCH_SIZE" in res[k]:
+            res[k]["hbm_read_bytes"] = res[k]["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in res[k]:
+            res[k]["hbm_write_bytes"] = res[k]["WRITE_SIZE"] * 1024
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    for k in sorted(res):
+        print(k, {c: (round(v, 3) if isinstance(v, float) else v) for c, v in sorted(res[k].items())})
+
+
+if __name__ == "__main__":
+    main()
