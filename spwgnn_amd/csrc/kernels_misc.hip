@@ -129,30 +129,39 @@ __device__ __forceinline__ float4 finish_y(const YRaw& r) {
                        (r.bits & 8u) ? r.g.w : 0.f);
 }
 
-// dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n].
-// Software pipeline per 32-row block: [barrier] write staged regs → LDS [barrier] issue the
-// next block's loads → MFMAs on the LDS block (the loads land meanwhile).
+// dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n] on v_mfma_f32_16x16x4_f32.
+// The (KXP/16)×(NYP/16) output tiles split 2×2 over the 4 waves (5×5 tiles of 16×16 per wave at
+// 160×160, so every SIMD gets the same work); per k-step (4 rows) a wave reads MX + MY fragments
+// from LDS for MX·MY MFMAs. Software pipeline per 32-row block: [barrier] write the staged
+// registers → LDS [barrier] issue the next block's loads → 8 k-steps of MFMAs on the LDS block.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 template <int XM, int YM, int KXP, int NYP>
 __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
-    constexpr int TX = KXP / 32, TY = NYP / 32;
-    constexpr int NT = TX * TY;                    // output tiles
-    constexpr int TPW = (NT + 3) / 4;              // tiles per wave (max)
-    constexpr int LDX = KXP + 4, LDY = NYP + 4;    // 16-B aligned rows; MFMA reads are conflict-free
+    constexpr int MX = KXP / 32, MY = NYP / 32;    // 16×16 tiles per wave along X / Y features
+    constexpr int LDX = KXP + 16, LDY = NYP + 16;  // ≡ 16 (mod 32): the 4 rows of a fragment read
+                                                   // fall in alternate bank halves (no conflicts)
     constexpr int GX = KXP / 4, GY = NYP / 4;
     constexpr int NGX = (32 * GX + kWgThreads - 1) / kWgThreads;   // float4 groups per thread
     constexpr int NGY = (32 * GY + kWgThreads - 1) / kWgThreads;
     __shared__ __attribute__((aligned(16))) float Xs[32 * LDX];
     __shared__ __attribute__((aligned(16))) float Ys[32 * LDY];
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, i = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, c16 = lane & 15, kq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wx = wave >> 1, wy = wave & 1;
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
     const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
-    f32x16 acc[TPW];
+    f32x4 acc[MX][MY];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = zero16();
-    // the recomputed-h1 operand (3 gathers per group) is fetched in the write phase instead of a
-    // block ahead: holding its raw registers across the MFMAs would spill
-    constexpr bool PFX = (XM != XM_EDGE_H1);
+    for (int x = 0; x < MX; ++x)
+#pragma unroll
+        for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every operand is fetched a block ahead (PFX); the write-phase fetch of X is kept for shapes
+    // whose raw registers would not fit beside the accumulators
+    constexpr bool PFX = true;
     XRaw xr[NGX];
     YRaw yr[NGY];
     const int64_t xcount = (XM == XM_ROW) ? a.x_count : (XM == XM_EDGE_H1 ? a.RE : a.rows);
@@ -223,30 +232,30 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
         }
         __syncthreads();
         if (r0 + 32 < r_end) fetch(r0 + 32);
+        const float* xs = Xs + kq * LDX + 16 * MX * wx + c16;
+        const float* ys = Ys + kq * LDY + 16 * MY * wy + c16;
 #pragma unroll 2
-        for (int k2 = 0; k2 < 16; ++k2) {
-            const int rr = 2 * k2 + h;
+        for (int k = 0; k < 8; ++k) {
+            float xa[MX], yb[MY];
 #pragma unroll
-            for (int u = 0; u < TPW; ++u) {
-                const int tile = wave + 4 * u;      // wave-uniform
-                if (tile < NT) {
-                    const int ti = tile / TY, tj = tile - ti * TY;
-                    acc[u] = mfma32(Xs[rr * LDX + 32 * ti + i], Ys[rr * LDY + 32 * tj + i], acc[u]);
-                }
-            }
+            for (int x = 0; x < MX; ++x) xa[x] = xs[4 * k * LDX + 16 * x];
+#pragma unroll
+            for (int y = 0; y < MY; ++y) yb[y] = ys[4 * k * LDY + 16 * y];
+#pragma unroll
+            for (int x = 0; x < MX; ++x)
+#pragma unroll
+                for (int y = 0; y < MY; ++y) acc[x][y] = mfma16(xa[x], yb[y], acc[x][y]);
         }
     }
+    // C layout of a 16×16 tile: reg r of lane l = row 4(l>>4) + r, col l&15
     float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
 #pragma unroll
-    for (int u = 0; u < TPW; ++u) {
-        const int tile = wave + 4 * u;
-        if (tile < NT) {
-            const int ti = tile / TY, tj = tile - ti * TY;
+    for (int x = 0; x < MX; ++x)
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-                out[(int64_t)(32 * ti + rho(r, 0) + 4 * h) * NYP + 32 * tj + i] = acc[u][r];
-        }
-    }
+        for (int y = 0; y < MY; ++y)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(int64_t)(16 * (MX * wx + x) + 4 * kq + r) * NYP + 16 * (MY * wy + y) + c16] = acc[x][y][r];
 }
 
 // stage 1: partial[g][idx] = Σ_{c in group g} slab[c][idx] (contiguous chunk ranges, fixed order)
