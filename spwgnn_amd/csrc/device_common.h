@@ -21,6 +21,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// v_mfma_f32_16x16x4_f32: A lane l = A[l&15][k=l>>4], B lane l = B[k=l>>4][l&15];
+// C reg r of lane l = C[row 4(l>>4) + r][col l&15].
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 __device__ __forceinline__ constexpr int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ f32x16 zero16() {

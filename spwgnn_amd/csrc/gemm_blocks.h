@@ -127,6 +127,21 @@ __device__ __forceinline__ void ngemm_acc(const float (&a)[KH], f32x16 (&acc)[NT
     }
 }
 
+// ---- LDS image of a [160][160] (k-major, ld kLdE) packed weight for the natural-orientation edge
+// kernels: wl[col * kWlK + k] = W[k][col], k < 152 (the two 76-feature halves). A lane's 4
+// consecutive k of one column are one ds_read_b128; kWlK ≡ 28 (mod 32) keeps 8 consecutive
+// lanes on distinct 4-bank groups.
+constexpr int kWlK = 156;
+constexpr int kWlFloats = 160 * kWlK;
+constexpr int kEdgeWaves = 8;   // waves per edge workgroup (one workgroup per CU: 97.5 KiB of LDS)
+__device__ __forceinline__ void wl_fill(float* wl, const float* __restrict__ W) {
+    for (int idx = threadIdx.x; idx < 160 * 2 * kKhE; idx += blockDim.x) {
+        const int k = idx / 160, col = idx - k * 160;
+        wl[col * kWlK + k] = W[k * kLdE + col];
+    }
+    __syncthreads();
+}
+
 template <int NT>
 __device__ __forceinline__ void zero_tiles(f32x16 (&X)[NT]) {
 #pragma unroll

@@ -172,6 +172,8 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
+// persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)
+int edge_grid(int n_wtiles);
 inline size_t edge_fwd_lds_per_wave(int nw_max) { return (size_t)(2112 + nw_max * kLdE) * 4; }
 inline size_t edge_bwd_lds_per_wave(int nw_max) { return (size_t)(2112 + 2 * nw_max * kLdE) * 4; }
 inline int edge_wpg(size_t lds_per_wave) {

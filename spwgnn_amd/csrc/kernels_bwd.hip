@@ -191,12 +191,18 @@ __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint
 // ones with no-return float atomics (one add per element per launch, launches stream-ordered:
 // the summation order is fixed, so the result stays deterministic).
 template <bool ONEHOT>
-__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd(EdgeBwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
+__global__ __launch_bounds__(ONEHOT ? 512 : 256, ONEHOT ? 1 : 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_edge_bwd(EdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wt = blockIdx.x * a.wpg + wave;
-    if (wt >= a.n_wtiles) return;
+    // ONEHOT: persistent 8-wave workgroup with the W2ᵀ image in LDS (see k_edge_fwd);
+    // otherwise one wave-tile per wave, LDS = segment-sum stage + node accumulators
+    __shared__ __attribute__((aligned(16))) float wl[ONEHOT ? kWlFloats : 1];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    if (ONEHOT) wl_fill(wl, a.w2t);
+    const float* wrow = ONEHOT ? wl + i * kWlK + kKhE * h : a.w2t + (kKhE * h) * kLdE + i;
+    const int wstep = ONEHOT ? gridDim.x * kEdgeWaves : a.n_wtiles;
+    for (int wt = ONEHOT ? blockIdx.x * kEdgeWaves + wave : blockIdx.x * a.wpg + wave; wt < a.n_wtiles; wt += wstep) {
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     float* st = smem + wave * (2112 + 2 * a.nw_max * kLdE);
@@ -230,36 +236,37 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const float4* G4 = reinterpret_cast<const float4*>(a.G3 + (int64_t)dc * kLdE + kKhE * h);
         f32x16 acc[5];
         zero_tiles(acc);
-        const float* wbase = a.w2t + (kKhE * h) * kLdE + i;
-        // one W fragment set, each k-step's fragments reloaded right after their MFMAs issue
-        float wf[4][5];
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int t = 0; t < 5; ++t) wf[c][t] = wbase[c * kLdE + 32 * t];
-        float4 g = G4[0];
-        auto chunk = [&](int q, bool more) {
+        // G3 rows run two chunks ahead; W2ᵀ fragments come from the LDS image (ONEHOT) or global
+        float4 g = G4[0], g1 = G4[1];
+        auto chunk = [&](int q) {
             const uint32_t bits = (uint32_t)(q < 16 ? mlo >> (4 * q) : (uint64_t)(mhi >> (4 * q - 64)));
             float xv[4];
             xv[0] = (bits & 1u) ? g.x : 0.f;
             xv[1] = (bits & 2u) ? g.y : 0.f;
             xv[2] = (bits & 4u) ? g.z : 0.f;
             xv[3] = (bits & 8u) ? g.w : 0.f;
-            if (more) g = G4[q + 1];
-            const float* wrow = wbase + (4 * q + 4) * kLdE;
+            g = g1;
+            if (q + 2 < kKhE / 4) g1 = G4[q + 2];
+            const float* wq = wrow + (ONEHOT ? 4 * q : 4 * q * kLdE);
+            float4 wv = ONEHOT ? *reinterpret_cast<const float4*>(wq)
+                               : make_float4(wq[0], wq[kLdE], wq[2 * kLdE], wq[3 * kLdE]);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-#pragma unroll
-                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], wf[c][t], acc[t]);
-                if (more) {
-#pragma unroll
-                    for (int t = 0; t < 5; ++t) wf[c][t] = wrow[c * kLdE + 32 * t];
+            for (int t = 0; t < 5; ++t) {
+                float4 wn;
+                if (t < 4) {
+                    const float* wt1 = wq + (t + 1) * (ONEHOT ? 32 * kWlK : 32);
+                    wn = ONEHOT ? *reinterpret_cast<const float4*>(wt1)
+                                : make_float4(wt1[0], wt1[kLdE], wt1[2 * kLdE], wt1[3 * kLdE]);
                 }
+                acc[t] = mfma32(xv[0], wv.x, acc[t]);
+                acc[t] = mfma32(xv[1], wv.y, acc[t]);
+                acc[t] = mfma32(xv[2], wv.z, acc[t]);
+                acc[t] = mfma32(xv[3], wv.w, acc[t]);
+                if (t < 4) wv = wn;
             }
         };
 #pragma unroll 1
-        for (int q = 0; q < kKhE / 4 - 1; ++q) chunk(q, true);
-        chunk(kKhE / 4 - 1, false);
+        for (int q = 0; q < kKhE / 4; ++q) chunk(q);
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
         const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
         float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
@@ -331,6 +338,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             oU[idx] = naccS[idx];
             oV[idx] = naccR[idx];
         }
+    }
     }
 }
 
@@ -409,8 +417,7 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
 }
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st) {
     if (a.nw_max <= 16) {
-        if (a.wpg != 4) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_edge_bwd<true>, dim3((a.n_wtiles + 3) / 4), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_edge_bwd<true>, dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
     } else {
         const size_t lds = edge_bwd_lds_per_wave(a.nw_max) * a.wpg;
         hipLaunchKernelGGL(k_edge_bwd<false>, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);

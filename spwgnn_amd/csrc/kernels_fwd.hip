@@ -151,22 +151,102 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 // ------------------------------------------------------------------------------------------------
-// One propagation step, edge side (natural orientation, one wave-tile of whole towers per wave).
-// The receiver segment sum (Networks.py:178 dot(receiver_relations, x)) runs on the matrix core:
-// C reg r of tile t holds h2[edge rho(r,h)][feature 32t+i], which is exactly the B operand of
-// k-step r of  nacc[t] += onehot·h2  when the A operand of lane (m, h) is
-// [dst(edge rho(r,h)) == node n0+m].  16 k-steps × 5 tiles per block; the wave-tile's node rows
-// stay in registers (≤ 32 nodes): no LDS, fixed summation order (deterministic).
-__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_fwd(EdgeFwdArgs a) {
+// Receiver segment sum of one wave-tile on the matrix core (Networks.py:178 dot(receiver_relations,
+// x)). C reg r of tile t of the h2 accumulators holds h2[edge rho(r,h)][feature 32t+i] — exactly a
+// B operand whose k index runs over the edges, so  nodes += onehot(dst)·h2  needs no lane movement.
+//  NW16 (≤ 16 nodes): 16x16x4 MFMAs, 10 tiles of 16 nodes × 16 features (40 registers). Lane l of
+//    the B operand is edge rho(r, l>>5) (k = l>>4) carrying feature 32t + (l&31): lanes with
+//    (l>>4) even carry feature tile 2t, odd ones tile 2t+1, so each (t, r) is two MFMAs whose
+//    one-hot A operands are zero on the other parity.
+//  else (≤ 32 nodes): one 32x32x2 MFMA per (t, r), 5 tiles of 32 nodes × 32 features.
+// Padding edges have dst -1 and match no node; summation order is fixed (deterministic).
+template <bool NW16> struct NodeSum;
+template <> struct NodeSum<true> {
+    f32x4 acc[10];
+    int key, kq;
+    __device__ __forceinline__ void init(int n0, int lane) {
+        key = n0 + (lane & 15);
+        kq = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < 10; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __device__ __forceinline__ void add(const f32x16 (&h2)[5], int d) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d0 = __builtin_amdgcn_readlane(d, rho(r, 0)), d1 = __builtin_amdgcn_readlane(d, rho(r, 1));
+            const bool match = (kq < 2 ? d0 : d1) == key;
+            const float ae = (match && !(kq & 1)) ? 1.f : 0.f, ao = (match && (kq & 1)) ? 1.f : 0.f;
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+                acc[2 * t] = mfma16(ae, h2[t][r], acc[2 * t]);
+                acc[2 * t + 1] = mfma16(ao, h2[t][r], acc[2 * t + 1]);
+            }
+        }
+    }
+    // reg r of tile T: node 4·kq + r, feature 16T + (lane&15)
+    __device__ __forceinline__ void store(float* rows, int nn, int lane) const {
+        float* o = rows + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int node = 4 * kq + r;
+            if (node < nn) {
+#pragma unroll
+                for (int t = 0; t < 10; ++t) o[node * kLdE + 16 * t] = acc[t][r];
+            }
+        }
+    }
+};
+template <> struct NodeSum<false> {
+    f32x16 acc[5];
+    int key;
+    __device__ __forceinline__ void init(int n0, int lane) {
+        key = n0 + (lane & 31);
+        zero_tiles(acc);
+    }
+    __device__ __forceinline__ void add(const f32x16 (&h2)[5], int d) {
+        const int h = (threadIdx.x >> 5) & 1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d0 = __builtin_amdgcn_readlane(d, rho(r, 0)), d1 = __builtin_amdgcn_readlane(d, rho(r, 1));
+            const float oh = ((h ? d1 : d0) == key) ? 1.f : 0.f;
+#pragma unroll
+            for (int t = 0; t < 5; ++t) acc[t] = mfma32(oh, h2[t][r], acc[t]);
+        }
+    }
+    // reg r of tile t: node rho(r,h), feature 32t + (lane&31)
+    __device__ __forceinline__ void store(float* rows, int nn, int lane) const {
+        const int h = lane >> 5;
+        float* o = rows + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int node = rho(r, 0) + 4 * h;
+            if (node < nn) {
+#pragma unroll
+                for (int t = 0; t < 5; ++t) o[node * kLdE + 32 * t] = acc[t][r];
+            }
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// One propagation step, edge side (natural orientation, one wave-tile of whole towers per wave;
+// one 8-wave workgroup per CU walks the wave-tiles persistently).
+// W2 lives in LDS as a [col][k] image (wl_fill): a lane's 4 consecutive k of one 32-column tile
+// are one ds_read_b128, so a chunk (4 k-steps × 5 tiles) costs 5 LDS reads instead of 20 global
+// loads, and only two tiles' fragments are live at a time.
+// The receiver segment sum runs on the matrix core into registers (NodeSum).
+template <bool NW16>
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_fwd(EdgeFwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[kWlFloats];
+    wl_fill(wl, a.w2);
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wt = blockIdx.x * 4 + wave;
-    if (wt >= a.n_wtiles) return;
+    const float* wrow = wl + i * kWlK + kKhE * h;
+    for (int wt = blockIdx.x * kEdgeWaves + wave; wt < a.n_wtiles; wt += gridDim.x * kEdgeWaves) {
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
-    const int key = n0 + i;  // node of this lane's one-hot row
-    f32x16 nacc[5];
-    zero_tiles(nacc);
+    NodeSum<NW16> nsum;
+    nsum.init(n0, lane);
 
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
@@ -176,7 +256,6 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const int sc = valid ? s : n0, dc = valid ? d : n0;
         // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:174-177), lane = edge, split
         // halves, streamed 4 features at a time straight into h2 = h1·W2 (rmp layer 2).
-        // W2 fragments are double-buffered in registers one chunk ahead (no load→MFMA stall).
         const uint64_t vmask = __ballot(valid);
         const float vf = valid ? 1.f : 0.f;
         const float4* A4 = reinterpret_cast<const float4*>(a.A + e * kLdE + kKhE * h);
@@ -189,35 +268,33 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         f32x16 acc[5];
         zero_tiles(acc);
-        const float* wbase = a.w2 + (kKhE * h) * kLdE + i;
-        // one W fragment set (4 k-steps × 5 tiles); each k-step's fragments are reloaded for the next
-        // chunk right after their MFMAs issue (one chunk of latency cover, 20 registers)
-        float w[4][5];
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int t = 0; t < 5; ++t) w[c][t] = wbase[c * kLdE + 32 * t];
+        // A/U/V run two chunks ahead (A streams from HBM)
         float4 pa = A4[0], pu = U4[0], pv = V4[0];
-        auto chunk = [&](int q, bool more) {
+        float4 qa = A4[1], qu = U4[1], qv = V4[1];
+        auto chunk = [&](int q) {
             float xv[4];
             xv[0] = relu(pa.x + pu.x + pv.x) * vf;
             xv[1] = relu(pa.y + pu.y + pv.y) * vf;
             xv[2] = relu(pa.z + pu.z + pv.z) * vf;
             xv[3] = relu(pa.w + pu.w + pv.w) * vf;
-            if (more) {
-                pa = A4[q + 1];
-                pu = U4[q + 1];
-                pv = V4[q + 1];
+            pa = qa;
+            pu = qu;
+            pv = qv;
+            if (q + 2 < kKhE / 4) {
+                qa = A4[q + 2];
+                qu = U4[q + 2];
+                qv = V4[q + 2];
             }
-            const float* wrow = wbase + (4 * q + 4) * kLdE;
+            float4 wv = *reinterpret_cast<const float4*>(wrow + 4 * q);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-#pragma unroll
-                for (int t = 0; t < 5; ++t) acc[t] = mfma32(xv[c], w[c][t], acc[t]);
-                if (more) {
-#pragma unroll
-                    for (int t = 0; t < 5; ++t) w[c][t] = wrow[c * kLdE + 32 * t];
-                }
+            for (int t = 0; t < 5; ++t) {
+                float4 wn;
+                if (t < 4) wn = *reinterpret_cast<const float4*>(wrow + (t + 1) * 32 * kWlK + 4 * q);
+                acc[t] = mfma32(xv[0], wv.x, acc[t]);
+                acc[t] = mfma32(xv[1], wv.y, acc[t]);
+                acc[t] = mfma32(xv[2], wv.z, acc[t]);
+                acc[t] = mfma32(xv[3], wv.w, acc[t]);
+                if (t < 4) wv = wn;
             }
             if (mrow) {
                 uint32_t stg = 0u;
@@ -231,8 +308,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
         };
 #pragma unroll 1
-        for (int q = 0; q < kKhE / 4 - 1; ++q) chunk(q, true);
-        chunk(kKhE / 4 - 1, false);
+        for (int q = 0; q < kKhE / 4; ++q) chunk(q);
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
@@ -261,25 +337,10 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             m2row[64 + lane] = mw[1];
             if (lane < 32) m2row[128 + lane] = mw[2];
         }
-        // receiver segment sum on the matrix core (padding edges have dst -1: no match)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int d0 = __builtin_amdgcn_readlane(d, rho(r, 0)), d1 = __builtin_amdgcn_readlane(d, rho(r, 1));
-            const float oh = ((h ? d1 : d0) == key) ? 1.f : 0.f;
-#pragma unroll
-            for (int t = 0; t < 5; ++t) nacc[t] = mfma32(oh, acc[t][r], nacc[t]);
-        }
+        nsum.add(acc, d);
     }
-    // the wave-tile's node rows (each node is owned by exactly one wave-tile):
-    // nacc[t] reg r = node rho(r,h), feature 32t+i
-    float* out = a.H2s + (int64_t)n0 * kLdE + i;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int node = rho(r, 0) + 4 * h;
-        if (node < nn) {
-#pragma unroll
-            for (int t = 0; t < 5; ++t) out[node * kLdE + 32 * t] = nacc[t][r];
-        }
+    // the wave-tile's node rows (each node is owned by exactly one wave-tile)
+    nsum.store(a.H2s + (int64_t)n0 * kLdE, nn, lane);
     }
 }
 
@@ -359,6 +420,18 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 // ------------------------------------------------------------------------------------------------
+int edge_grid(int n_wtiles) {
+    static int cus = 0;  // compute units of the device (all devices of a node are alike)
+    if (cus <= 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        cus = v;
+    }
+    const int need = (n_wtiles + kEdgeWaves - 1) / kEdgeWaves;
+    return need < 1 ? 1 : (need < cus ? need : cus);
+}
+
 hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_prep_weights, dim3(32, PK_COUNT), dim3(256), 0, st, a);
     return hipGetLastError();
@@ -374,7 +447,10 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st) {
 }
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
-    hipLaunchKernelGGL(k_edge_fwd, dim3((a.n_wtiles + 3) / 4), dim3(256), 0, st, a);
+    if (a.nw_max <= 16)
+        hipLaunchKernelGGL(k_edge_fwd<true>, dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_edge_fwd<false>, dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st) {

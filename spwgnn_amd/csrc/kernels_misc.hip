@@ -134,11 +134,6 @@ __device__ __forceinline__ float4 finish_y(const YRaw& r) {
 // 160×160, so every SIMD gets the same work); per k-step (4 rows) a wave reads MX + MY fragments
 // from LDS for MX·MY MFMAs. Software pipeline per 32-row block: [barrier] write the staged
 // registers → LDS [barrier] issue the next block's loads → 8 k-steps of MFMAs on the LDS block.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
 template <int XM, int YM, int KXP, int NYP>
 __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     constexpr int MX = KXP / 32, MY = NYP / 32;    // 16×16 tiles per wave along X / Y features
