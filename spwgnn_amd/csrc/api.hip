@@ -126,6 +126,9 @@ static void build_packs(const Ws& w, PrepArgs& pa) {
         d.src_row0 = row0;
         d.transpose = transpose;
         d.perm = perm;
+        // A operands of the transposed-orientation MLP chains are k4-blocked (gemm_blocks.h);
+        // W2/W2ᵀ (LDS images built by the edge kernels), rm.0/om.0 and the biases stay row-major
+        d.k4 = !(pid == PK_W2 || pid == PK_W2T || pid == PK_RM0 || pid == PK_OM0 || pack_rows(pid) == 1);
         pa.desc[pid] = d;
     };
     // forward [in][out]
@@ -221,8 +224,10 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     build_packs(w, pa);
     SPW_CHECK(launch_prep_weights(pa, st));
     // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
-    SPW_CHECK(hipMemcpyAsync(c.f(w.pk + w.ps.off[PK_W3A] + 150 * 128), params + param_table().t[T_RMP2B].offset,
-                             100 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    // (k4-blocked: element (150, c) sits at ((150/4)·128 + c)·4 + 150%4, a 16-byte stride)
+    SPW_CHECK(hipMemcpy2DAsync(c.f(w.pk + w.ps.off[PK_W3A] + ((150 / 4) * kLdN) * 4 + 150 % 4), 4 * sizeof(float),
+                               params + param_table().t[T_RMP2B].offset, sizeof(float), sizeof(float), 100,
+                               hipMemcpyDeviceToDevice, st));
     const bool drop = r->training && r->dropout > 0.f;
     const uint32_t thresh = (uint32_t)std::min(4294967295.0, std::floor((double)r->dropout * 4294967296.0));
     const float scale = drop ? 1.0f / (1.0f - r->dropout) : 1.0f;

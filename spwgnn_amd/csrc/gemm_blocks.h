@@ -56,60 +56,111 @@ __device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh
     }
 }
 
-// ---- transposed orientation: out[t] += Wᵀ·in over register k-steps.
-// in: C layout of the previous layer (feature rho(r,h)+32tp on the lane's row); the k-steps are
-// (tp, r) for tp < NT_IN, with r < LAST_R in the last input tile (rows beyond are zero padding).
-// W: [in][out] row-major with row stride LDW; the A operand of lane (i,h) is W[k(h)][32t + i].
-// The weight fragments run PF k-steps ahead in a register ring (hipcc otherwise serialises each
-// load with its MFMA under register pressure — see DESIGN.md §3).
-template <int NT_OUT, int NT_IN, int LAST_R, int LDW, int PF = 3>
+// ---- transposed orientation: out[t] += Wᵀ·in with the [K][N] weight as a k4-blocked image
+// W4[((k>>2)·N + col)·4 + (k&3)] (built by k_prep_weights). The A operand of lane (i, h) at
+// k-step kk of input tile tp is W[rho(kk,h) + 32tp][32t + i]; k-steps 4g..4g+3 are the 4
+// consecutive features 8g + 4h + 0..3 — one 16-byte load per tile per 4 MFMAs, and the 32 lanes
+// of a half read 512 contiguous bytes. (One dword load per MFMA caps the matrix pipe near 50 %;
+// tools/mb/chain.hip.) The next group's fragments load while this group's MFMAs issue.
+// in: C layout of the previous layer; k-steps (tp, r) for tp < NT_IN, r < LAST_R in the last
+// input tile (LAST_R % 4 == 0; rows beyond are zero padding).
+template <int NT_OUT, int NT_IN, int LAST_R, int N>
 __device__ __forceinline__ void tchain_acc(const f32x16 (&in)[NT_IN], f32x16 (&out)[NT_OUT],
-                                           const float* __restrict__ W, int lane) {
-    const int i = lane & 31, h = lane >> 5;
-    const float* wbase = W + (4 * h) * LDW + i;
-    constexpr int NK = (NT_IN - 1) * 16 + LAST_R;
-    float w[PF + 1][NT_OUT];
+                                           const float* __restrict__ W4, int lane) {
+    static_assert(LAST_R % 4 == 0, "16-byte fragments");
+    const float* wb = W4 + ((lane >> 5) * N + (lane & 31)) * 4;   // k-block h, column i
+    constexpr int NG = (NT_IN - 1) * 4 + LAST_R / 4;   // groups of 4 k-steps: k-block 2gi + h
+    float4 cur[NT_OUT], nxt[NT_OUT];
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-        if (k >= NK) break;
-        const float* wrow = wbase + (rho(k & 15, 0) + 32 * (k >> 4)) * LDW;
+    for (int t = 0; t < NT_OUT; ++t) cur[t] = *reinterpret_cast<const float4*>(wb + 128 * t);
 #pragma unroll
-        for (int t = 0; t < NT_OUT; ++t) w[k][t] = wrow[32 * t];
-    }
+    for (int gi = 0; gi < NG; ++gi) {
+        if (gi + 1 < NG) {
 #pragma unroll
-    for (int k = 0; k < NK; ++k) {
-        if (k + PF < NK) {
-            const int kk = k + PF;
-            const float* wrow = wbase + (rho(kk & 15, 0) + 32 * (kk >> 4)) * LDW;
-#pragma unroll
-            for (int t = 0; t < NT_OUT; ++t) w[kk % (PF + 1)][t] = wrow[32 * t];
+            for (int t = 0; t < NT_OUT; ++t) nxt[t] = *reinterpret_cast<const float4*>(wb + 8 * N * (gi + 1) + 128 * t);
         }
-        const float b = in[k >> 4][k & 15];
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
+        const int tp = gi >> 2, r0 = 4 * (gi & 3);
 #pragma unroll
-        for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(w[k % (PF + 1)][t], b, out[t]);
+        for (int t = 0; t < NT_OUT; ++t) {
+            out[t] = mfma32(cur[t].x, in[tp][r0], out[t]);
+            out[t] = mfma32(cur[t].y, in[tp][r0 + 1], out[t]);
+            out[t] = mfma32(cur[t].z, in[tp][r0 + 2], out[t]);
+            out[t] = mfma32(cur[t].w, in[tp][r0 + 3], out[t]);
+        }
+        if (gi + 1 < NG) {
+#pragma unroll
+            for (int t = 0; t < NT_OUT; ++t) cur[t] = nxt[t];
+        }
     }
 }
 
-// ---- transposed orientation, B operand from a split-halves row chunk x (features KH*h + s).
-template <int NT_OUT, int KH, int LDW, int PF = 3>
+// ---- transposed orientation, B operand from a split-halves row chunk x (features KH*h + s),
+// k4-blocked weight: k-steps 4q..4q+3 of half h are k-block KH/4·h + q.
+template <int NT_OUT, int KH, int N>
 __device__ __forceinline__ void tgemm_half_acc(const float (&x)[KH], f32x16 (&out)[NT_OUT],
-                                               const float* __restrict__ W, int lane) {
-    const int i = lane & 31, h = lane >> 5;
-    const float* wbase = W + (KH * h) * LDW + i;
-    float w[PF + 1][NT_OUT];
+                                               const float* __restrict__ W4, int lane) {
+    static_assert(KH % 4 == 0, "16-byte fragments");
+    const float* wb = W4 + ((KH / 4) * (lane >> 5) * N + (lane & 31)) * 4;
+    float4 cur[NT_OUT], nxt[NT_OUT];
 #pragma unroll
-    for (int k = 0; k < PF; ++k)
+    for (int t = 0; t < NT_OUT; ++t) cur[t] = *reinterpret_cast<const float4*>(wb + 128 * t);
 #pragma unroll
-        for (int t = 0; t < NT_OUT; ++t) w[k][t] = wbase[k * LDW + 32 * t];
+    for (int q = 0; q < KH / 4; ++q) {
+        if (q + 1 < KH / 4) {
 #pragma unroll
-    for (int s = 0; s < KH; ++s) {
-        if (s + PF < KH) {
-#pragma unroll
-            for (int t = 0; t < NT_OUT; ++t) w[(s + PF) % (PF + 1)][t] = wbase[(s + PF) * LDW + 32 * t];
+            for (int t = 0; t < NT_OUT; ++t) nxt[t] = *reinterpret_cast<const float4*>(wb + 4 * N * (q + 1) + 128 * t);
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(w[s % (PF + 1)][t], x[s], out[t]);
+        for (int t = 0; t < NT_OUT; ++t) {
+            out[t] = mfma32(cur[t].x, x[4 * q], out[t]);
+            out[t] = mfma32(cur[t].y, x[4 * q + 1], out[t]);
+            out[t] = mfma32(cur[t].z, x[4 * q + 2], out[t]);
+            out[t] = mfma32(cur[t].w, x[4 * q + 3], out[t]);
+        }
+        if (q + 1 < KH / 4) {
+#pragma unroll
+            for (int t = 0; t < NT_OUT; ++t) cur[t] = nxt[t];
+        }
     }
+}
+
+// ---- transposed orientation, B operand streamed from a split-halves global row (features
+// KH*h + s, 16 bytes at a time), k4-blocked weight. Rolled loop (bounded registers).
+template <int NT_OUT, int KH, int N>
+__device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_khh, f32x16 (&out)[NT_OUT],
+                                                 const float* __restrict__ W4, int lane) {
+    static_assert(KH % 4 == 0, "16-byte fragments");
+    const float4* x4 = reinterpret_cast<const float4*>(row_khh);
+    const float* wb = W4 + ((KH / 4) * (lane >> 5) * N + (lane & 31)) * 4;
+    static_assert((KH / 4) % 2 == 1, "ring schedule below: odd chunk count");
+    float4 w0[NT_OUT], w1[NT_OUT];
+    float4 x0 = x4[0], x1;
+#pragma unroll
+    for (int t = 0; t < NT_OUT; ++t) w0[t] = *reinterpret_cast<const float4*>(wb + 128 * t);
+    // two register slots with static names (loop unrolled by 2): the prefetch of chunk q+1 is
+    // never copied, so the wait before chunk q covers chunk q's loads only
+    auto chunk = [&](int q, const float4 (&cw)[NT_OUT], const float4& cx, float4 (&nw)[NT_OUT], float4& nx) {
+        const int qn = min(q + 1, KH / 4 - 1);   // unconditional (clamped) prefetch
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) nw[t] = *reinterpret_cast<const float4*>(wb + 4 * N * qn + 128 * t);
+        nx = x4[qn];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < NT_OUT; ++t) {
+            out[t] = mfma32(cw[t].x, cx.x, out[t]);
+            out[t] = mfma32(cw[t].y, cx.y, out[t]);
+            out[t] = mfma32(cw[t].z, cx.z, out[t]);
+            out[t] = mfma32(cw[t].w, cx.w, out[t]);
+        }
+    };
+#pragma unroll 1
+    for (int q = 0; q + 1 < KH / 4; q += 2) {
+        chunk(q, w0, x0, w1, x1);
+        chunk(q + 1, w1, x1, w0, x0);
+    }
+    chunk(KH / 4 - 1, w0, x0, w1, x1);
 }
 
 // ---- natural orientation: acc[t] += A·W, A operand = this lane's row chunk a (features KH*h+s),

@@ -11,6 +11,8 @@ struct PackDesc {
     int32_t src_rows, src_cols;  // valid source extent (in destination orientation before transpose)
     int32_t src_ld, src_row0;
     int32_t transpose, perm;
+    int32_t k4;        // 1: k4-blocked image W4[((r>>2)·cols + c)·4 + (r&3)] (16-byte A-operand fragments)
+    int32_t pad0;
 };
 struct PrepArgs {
     const float* params;

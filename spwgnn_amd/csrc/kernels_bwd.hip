@@ -13,42 +13,6 @@
 
 namespace spw {
 
-// B operand streamed from a split-halves global row (transposed orientation), KH/4 float4 chunks.
-template <int NT_OUT, int KH, int LDW>
-__device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_khh, f32x16 (&out)[NT_OUT],
-                                                 const float* __restrict__ W, int lane) {
-    const int i = lane & 31, h = lane >> 5;
-    const float4* x4 = reinterpret_cast<const float4*>(row_khh);
-    const float* wbase = W + (KH * h) * LDW + i;
-    float wc[4][NT_OUT], wn[4][NT_OUT];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int t = 0; t < NT_OUT; ++t) wc[c][t] = wbase[c * LDW + 32 * t];
-    float4 nxt = x4[0];
-#pragma unroll 1
-    for (int q = 0; q < KH / 4; ++q) {
-        const float4 cur = nxt;
-        if (q + 1 < KH / 4) {
-            const float* wrow = wbase + (4 * q + 4) * LDW;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int t = 0; t < NT_OUT; ++t) wn[c][t] = wrow[c * LDW + 32 * t];
-            nxt = x4[q + 1];
-        }
-        const float xv[4] = {cur.x, cur.y, cur.z, cur.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int t = 0; t < NT_OUT; ++t) out[t] = mfma32(wc[c][t], xv[c], out[t]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int t = 0; t < NT_OUT; ++t) wc[c][t] = wn[c][t];
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node_bwd(NodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
@@ -236,17 +200,17 @@ void k_edge_bwd(EdgeBwdArgs a) {
         const float4* G4 = reinterpret_cast<const float4*>(a.G3 + (int64_t)dc * kLdE + kKhE * h);
         f32x16 acc[5];
         zero_tiles(acc);
-        // G3 rows run two chunks ahead; W2ᵀ fragments come from the LDS image (ONEHOT) or global
-        float4 g = G4[0], g1 = G4[1];
-        auto chunk = [&](int q) {
+        // G3 rows (L2-resident node rows) run one chunk ahead in a 2-slot ring (loop unrolled by
+        // 2, no register copies); W2ᵀ fragments come from the LDS image (ONEHOT) or global
+        float4 g0 = G4[0], g1;
+        auto chunk = [&](int q, const float4& g, float4& ahead) {
             const uint32_t bits = (uint32_t)(q < 16 ? mlo >> (4 * q) : (uint64_t)(mhi >> (4 * q - 64)));
             float xv[4];
             xv[0] = (bits & 1u) ? g.x : 0.f;
             xv[1] = (bits & 2u) ? g.y : 0.f;
             xv[2] = (bits & 4u) ? g.z : 0.f;
             xv[3] = (bits & 8u) ? g.w : 0.f;
-            g = g1;
-            if (q + 2 < kKhE / 4) g1 = G4[q + 2];
+            ahead = G4[min(q + 1, kKhE / 4 - 1)];  // unconditional (clamped) prefetch
             const float* wq = wrow + (ONEHOT ? 4 * q : 4 * q * kLdE);
             float4 wv = ONEHOT ? *reinterpret_cast<const float4*>(wq)
                                : make_float4(wq[0], wq[kLdE], wq[2 * kLdE], wq[3 * kLdE]);
@@ -264,9 +228,14 @@ void k_edge_bwd(EdgeBwdArgs a) {
                 acc[t] = mfma32(xv[3], wv.w, acc[t]);
                 if (t < 4) wv = wn;
             }
+            __builtin_amdgcn_sched_barrier(0);  // no hoisting across chunks (register pressure)
         };
 #pragma unroll 1
-        for (int q = 0; q < kKhE / 4; ++q) chunk(q);
+        for (int q = 0; q < 18; q += 2) {
+            chunk(q, g0, g1);
+            chunk(q + 1, g1, g0);
+        }
+        chunk(18, g0, g1);
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
         const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
         float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;

@@ -17,7 +17,15 @@ __global__ void k_prep_weights(PrepArgs a) {
     const PackDesc& d = a.desc[id];
     const int total = d.rows * d.cols;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-        const int r = idx / d.cols, c = idx - r * d.cols;
+        int r, c;
+        if (d.k4) {  // idx = ((r>>2)·cols + c)·4 + (r&3)
+            const int q = idx >> 2, kb = q / d.cols;
+            c = q - kb * d.cols;
+            r = 4 * kb + (idx & 3);
+        } else {
+            r = idx / d.cols;
+            c = idx - r * d.cols;
+        }
         int sa = d.transpose ? c : r;  // source row (before row0)
         int sb = d.transpose ? r : c;  // source col (before perm)
         float v = 0.f;
@@ -268,23 +276,21 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         f32x16 acc[5];
         zero_tiles(acc);
-        // A/U/V run two chunks ahead (A streams from HBM)
-        float4 pa = A4[0], pu = U4[0], pv = V4[0];
-        float4 qa = A4[1], qu = U4[1], qv = V4[1];
-        auto chunk = [&](int q) {
+        // A/U/V run two chunks ahead (A streams from HBM) in a 3-slot ring with static slot names
+        // (loop unrolled by 3): no loop-carried register copies, so the waitcnt before a chunk
+        // only covers that chunk's own loads
+        struct AUV { float4 a, u, v; };
+        AUV b0{A4[0], U4[0], V4[0]}, b1{A4[1], U4[1], V4[1]}, b2;
+        auto chunk = [&](int q, const AUV& cur, AUV& ahead) {
             float xv[4];
-            xv[0] = relu(pa.x + pu.x + pv.x) * vf;
-            xv[1] = relu(pa.y + pu.y + pv.y) * vf;
-            xv[2] = relu(pa.z + pu.z + pv.z) * vf;
-            xv[3] = relu(pa.w + pu.w + pv.w) * vf;
-            pa = qa;
-            pu = qu;
-            pv = qv;
-            if (q + 2 < kKhE / 4) {
-                qa = A4[q + 2];
-                qu = U4[q + 2];
-                qv = V4[q + 2];
-            }
+            xv[0] = relu(cur.a.x + cur.u.x + cur.v.x) * vf;
+            xv[1] = relu(cur.a.y + cur.u.y + cur.v.y) * vf;
+            xv[2] = relu(cur.a.z + cur.u.z + cur.v.z) * vf;
+            xv[3] = relu(cur.a.w + cur.u.w + cur.v.w) * vf;
+            const int qn = min(q + 2, kKhE / 4 - 1);   // unconditional (clamped) prefetch
+            ahead.a = A4[qn];
+            ahead.u = U4[qn];
+            ahead.v = V4[qn];
             float4 wv = *reinterpret_cast<const float4*>(wrow + 4 * q);
 #pragma unroll
             for (int t = 0; t < 5; ++t) {
@@ -307,8 +313,14 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 if (lane < 8) mrow[m1off + 4 * q] = stg;
             }
         };
+        static_assert(kKhE / 4 == 19, "ring schedule below assumes 19 chunks");
 #pragma unroll 1
-        for (int q = 0; q < kKhE / 4; ++q) chunk(q);
+        for (int q = 0; q < 18; q += 3) {
+            chunk(q, b0, b2);
+            chunk(q + 1, b1, b0);
+            chunk(q + 2, b2, b1);
+        }
+        chunk(18, b0, b2);
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
