@@ -20,6 +20,7 @@ struct Ws {
     int64_t mask1, mask2;                            // u32
     int64_t dx, do1, g, G3, dU, dV, dP, dco, dzo2, dzo1;   // node (bwd)
     int64_t dA, dz4, dz3, dz2, dz1;                  // edge (bwd)
+    int64_t H1, DH2;                                 // per step: h1 (fwd) and dh2pre (bwd) rows for the W2 gradient
     int64_t slab, bce;
     int64_t slab_floats;
     PackSlots ps;
@@ -40,6 +41,8 @@ struct Ws {
     int64_t dU_at(int s) const { return dU + (int64_t)s * RN * kLdE; }
     int64_t dV_at(int s) const { return dV + (int64_t)s * RN * kLdE; }
     int64_t dP_at(int k) const { return dP + (int64_t)(k & 1) * RN * kLdN; }
+    int64_t H1_at(int s) const { return H1 + (int64_t)s * NB * kCmBlk; }
+    int64_t DH2_at(int s) const { return DH2 + (int64_t)s * NB * kCmBlk; }
 };
 
 static constexpr int kMaxChunks = 1024;
@@ -72,7 +75,8 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     w.U = take(nE * w.sStep());
     w.V = take(nE * w.sStep());
     w.H2s = take(nE * w.sStep());
-    w.A = take(eE);
+    const int64_t eCM = w.NB * kCmBlk;   // chunk-major edge rows
+    w.A = take(eCM);
     if (training) {
         w.zo1 = take(nN);
         w.a = take(nN * S);
@@ -98,12 +102,14 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.dz3 = take(eE);
         w.dz2 = take(eE);
         w.dz1 = take(eE);
+        w.H1 = take(eCM * S);
+        w.DH2 = take(eCM * S);
         w.slab_floats = (int64_t)(kMaxChunks + kReduceGroups) * 160 * 160;
         w.slab = take(w.slab_floats);
     } else {
         w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = -1;
         w.dx = w.do1 = w.g = w.G3 = w.dU = w.dV = w.dP = w.dco = w.dzo2 = w.dzo1 = -1;
-        w.dA = w.dz4 = w.dz3 = w.dz2 = w.dz1 = w.slab = -1;
+        w.dA = w.dz4 = w.dz3 = w.dz2 = w.dz1 = w.slab = w.H1 = w.DH2 = -1;
         w.slab_floats = 0;
     }
     w.total = cur * 4;
@@ -306,6 +312,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.b2 = c.pk(PB_W2);
         ef.H2s = c.f(w.H2s_at(s));
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
+        ef.h1_out = r->training ? c.f(w.H1_at(s)) : nullptr;
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
         SPW_CHECK(launch_edge_fwd(ef, st));
@@ -353,7 +360,7 @@ struct WgSpec {
 };
 
 static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, hipStream_t st,
-                         int64_t U_off, int64_t V_off, int64_t G3_off, int64_t m2_off, const Prof* prof = nullptr) {
+                         const Prof* prof = nullptr) {
     const Ws& w = c.w;
     if (g.rows <= 0) return SPWGNN_OK;
     int64_t chunks = (g.rows + 32 * 16 - 1) / (32 * 16);
@@ -381,13 +388,6 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     a.pos = b->pos;
     a.esrc = b->edge_src;
     a.edst = b->edge_dst;
-    a.A = c.f(w.A);
-    a.U = c.f(U_off);
-    a.V = c.f(V_off);
-    a.G3 = c.f(G3_off);
-    a.mask2 = c.u(m2_off);
-    a.RE = w.RE;
-    a.RN = w.RN;
     a.slab = c.f(w.slab);
     if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
     SPW_CHECK(launch_wgrad(a, (int)chunks, st));
@@ -462,6 +462,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.csr = reinterpret_cast<const uint32_t*>(b->blk_csr);
         eb.mask1 = c.u(w.m1_at(s));
         eb.mask2 = c.u(w.m2_at(s));
+        eb.dh2_out = c.f(w.DH2_at(s));
         eb.G3 = c.f(w.G3_at(s));
         eb.w2t = c.pk(PK_W2T);
         eb.dA = c.f(w.dA);
@@ -528,16 +529,17 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         WgSpec g; g.xmode = XM_EDGE_D; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
-    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e; }
-    {   // rmp.1 (W2, b2): X = [h1 | 1] recomputed, Y = dh2pre, over all steps
-        WgSpec g; g.xmode = XM_EDGE_H1; g.ymode = YM_EDGE_DH2; g.kx_pad = 160; g.ny_pad = 160; g.rows = RE * S;
-        g.tk = T_RMP1K; g.tb = T_RMP1B; g.k_rows = kFE; g.bias_row = kFE;
-        if ((e = run_wgrad(c, b, g, grads, st, w.U, w.V, w.G3, w.mask2, &prof))) return e;
+    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre — chunk-major rows kept by the edge kernels
+        WgSpec g; edge_row(g, w.H1, w.DH2, T_RMP1K, T_RMP1B);
+        g.xmode = XM_CM; g.ymode = YM_CM;
+        g.x_count = g.y_count = g.rows = RE * S;
+        if ((e = run_wgrad(c, b, g, grads, st, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {
@@ -548,49 +550,49 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)
         WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
         g.rows = nN; g.y_stride = 0;
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, st, -1, -1, -1, -1))) return e;
+        if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     return SPWGNN_OK;
 }

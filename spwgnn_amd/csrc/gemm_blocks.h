@@ -41,6 +41,40 @@ __device__ __forceinline__ void load_rho(const float* __restrict__ row, f32x16 (
         }
 }
 
+// ---- chunk-major block rows (transposed orientation, lane (j, h) = edge j of the block):
+// regs 4q..4q+3 of tile t are features f0 = 32t + 8q + 4h .. +3, one 16-byte piece (f0 < 152).
+template <int NT>
+__device__ __forceinline__ void store_cm(float* __restrict__ blk, const f32x16 (&X)[NT], int lane, bool valid) {
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            if (32 * t + 8 * q < 2 * kKhE) {   // f0 < 152 (both halves: 8q + 32t ≤ 144)
+                float4 v = valid ? make_float4(X[t][4 * q], X[t][4 * q + 1], X[t][4 * q + 2], X[t][4 * q + 3])
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+                *reinterpret_cast<float4*>(blk + cm_off(j, f0)) = v;
+            }
+        }
+}
+template <int NT>
+__device__ __forceinline__ void load_cm(const float* __restrict__ blk, f32x16 (&X)[NT], int lane) {
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (32 * t + 8 * q < 2 * kKhE) v = *reinterpret_cast<const float4*>(blk + cm_off(j, f0));
+            X[t][4 * q] = v.x;
+            X[t][4 * q + 1] = v.y;
+            X[t][4 * q + 2] = v.z;
+            X[t][4 * q + 3] = v.w;
+        }
+}
+
 // ---- split-halves row chunk: lane half h holds features [KH*h, KH*h+KH) of its row.
 template <int KH>
 __device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh, float (&x)[KH]) {

@@ -53,6 +53,7 @@ struct EdgeFwdArgs {
     const float *A, *U, *V, *w2, *b2;
     float* H2s;
     uint32_t *mask1, *mask2;
+    float* h1_out;     // training: h1 rows, chunk-major blocks (kCmBlk), for the W2 gradient
 };
 
 struct NodeFwdArgs {
@@ -82,6 +83,7 @@ struct EdgeBwdArgs {
     const uint32_t *mask1, *mask2;
     const float *G3, *w2t;
     float *dA, *dU, *dV;
+    float* dh2_out;    // dh2pre rows, chunk-major blocks (kCmBlk), for the W2 gradient
 };
 
 struct EncEdgeBwdArgs {
@@ -101,34 +103,31 @@ struct EncNodeBwdArgs {
 
 // ---- weight gradients: dW = Σ_rows X[row]ᵀ·Y[row] (deterministic split-row slabs) ----
 enum XMode : int {
-    XM_ROW = 0,     // ptr[(row % bcast_rows) * ld + f], f < width; f == ones_col → 1
+    XM_ROW = 0,     // ptr[phys_row * ld + f]; f == ones_col → 1 (row-major rows, width ld)
     XM_EDGE_D,      // (pos[dst] - pos[src])[f] for f < 2, f == 2 → 1; padding edge → 0
     XM_NODE_O,      // pos[n][1 + f] for f < 2, f == 2 → 1
-    XM_EDGE_H1,     // relu(A[e] + U_s[src] + V_s[dst])[f] for f < 150, f == 150 → 1 (row = s*RE + e)
+    XM_CM,          // chunk-major edge blocks (kCmBlk per 32 rows, f < 152); f == ones_col → 1
 };
 enum YMode : int {
     YM_ROW = 0,
-    YM_EDGE_DH2,    // G3_s[dst][f] * bit(mask2_s) for f < 150 (row = s*RE + e)
+    YM_CM,          // chunk-major edge blocks
 };
 struct WgradArgs {
     int64_t rows;          // logical rows L = s*count + n
     int64_t rows_per_chunk;
     int xmode, ymode;
     int kx_pad, ny_pad;    // multiples of 32, <= 160
-    // X (ROW mode): physical row = (stride ? (L / count) * stride : 0) + L % count
+    // X: physical row = (stride ? (L / count) * stride : 0) + L % count
     const float* x_ptr;
     int x_ld, x_width, x_ones;
     int64_t x_count, x_stride;
-    // Y (ROW mode)
+    // Y
     const float* y_ptr;
     int y_ld, y_width;
     int64_t y_count, y_stride;
     // edge/node context
     const float* pos;
     const int32_t *esrc, *edst;
-    const float *A, *U, *V, *G3;
-    const uint32_t* mask2;
-    int64_t RE, RN;        // edge rows, node rows (per step strides)
     float* slab;           // [chunks][kx_pad][ny_pad]
 };
 struct ReduceArgs {

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     zero_tiles(X);
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_w1a, lane);
     bias_act_rho<5, false>(X, a.b_w1a, h);
-    store_rho_masked<5>(a.A + e * kLdE, X, h, valid);
+    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, valid);   // chunk-major (k_edge_fwd streams it)
     (void)zrow;
 }
 
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         // halves, streamed 4 features at a time straight into h2 = h1·W2 (rmp layer 2).
         const uint64_t vmask = __ballot(valid);
         const float vf = valid ? 1.f : 0.f;
-        const float4* A4 = reinterpret_cast<const float4*>(a.A + e * kLdE + kKhE * h);
+        const float* Acm = a.A + (int64_t)blk * kCmBlk + h * 128 + i * 4;   // chunk q at + 256q
         const float4* U4 = reinterpret_cast<const float4*>(a.U + (int64_t)sc * kLdE + kKhE * h);
         const float4* V4 = reinterpret_cast<const float4*>(a.V + (int64_t)dc * kLdE + kKhE * h);
         // h1 > 0 bits (mask1: word per (block, feature), bit = edge): each chunk's 8 ballots go
@@ -279,16 +279,19 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         // A/U/V run two chunks ahead (A streams from HBM) in a 3-slot ring with static slot names
         // (loop unrolled by 3): no loop-carried register copies, so the waitcnt before a chunk
         // only covers that chunk's own loads
+        float* h1cm = a.h1_out ? a.h1_out + (int64_t)blk * kCmBlk + h * 128 + i * 4 : nullptr;
+        auto ldA = [&](int q) { return *reinterpret_cast<const float4*>(Acm + 256 * q); };
         struct AUV { float4 a, u, v; };
-        AUV b0{A4[0], U4[0], V4[0]}, b1{A4[1], U4[1], V4[1]}, b2;
+        AUV b0{ldA(0), U4[0], V4[0]}, b1{ldA(1), U4[1], V4[1]}, b2;
         auto chunk = [&](int q, const AUV& cur, AUV& ahead) {
             float xv[4];
             xv[0] = relu(cur.a.x + cur.u.x + cur.v.x) * vf;
             xv[1] = relu(cur.a.y + cur.u.y + cur.v.y) * vf;
             xv[2] = relu(cur.a.z + cur.u.z + cur.v.z) * vf;
             xv[3] = relu(cur.a.w + cur.u.w + cur.v.w) * vf;
+            if (h1cm) *reinterpret_cast<float4*>(h1cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
             const int qn = min(q + 2, kKhE / 4 - 1);   // unconditional (clamped) prefetch
-            ahead.a = A4[qn];
+            ahead.a = ldA(qn);
             ahead.u = U4[qn];
             ahead.v = V4[qn];
             float4 wv = *reinterpret_cast<const float4*>(wrow + 4 * q);

@@ -25,7 +25,7 @@ __device__ __forceinline__ float4 f4add3(float4 a, float4 b, float4 c) {
 //   fetch_*  : issue the loads of one float4 group into registers (no use of the data)
 //   finish_* : combine the fetched registers into the staged value (after the MFMAs)
 struct XRaw { float4 a, u, v; int flag; };
-struct YRaw { float4 g; uint32_t bits; int flag; };
+struct YRaw { float4 g; int flag; };
 
 // Row mapping of a 32-row block: logical row L = r0 + rr → (step s, row n) with n < count.
 // One 64-bit division per block (scalar), then a carry per row (count >= 1).
@@ -43,38 +43,39 @@ __device__ __forceinline__ void row_at(const RowBase& b, int rr, int64_t& s, int
     }
 }
 
+__device__ __forceinline__ int64_t phys_row(const RowBase& b, int rr, int64_t stride) {
+    int64_t s, n;
+    row_at(b, rr, s, n);
+    return (stride ? s * stride : 0) + n;
+}
+// chunk-major rows: block = row / 32 (32-row blocks never straddle a step: RE % 32 == 0)
+__device__ __forceinline__ const float* cm_piece(const float* base, int64_t row, int f0) {
+    return base + (row >> 5) * kCmBlk + cm_off((int)(row & 31), f0);
+}
+
 template <int XM>
 __device__ __forceinline__ void fetch_x(const WgradArgs& a, const RowBase& rb, int rr, int f0, bool in, XRaw& r) {
     r.flag = 0;
     if (!in) return;
-    int64_t s, n;
-    row_at(rb, rr, s, n);
     if (XM == XM_ROW) {
-        const int64_t row = (a.x_stride ? s * a.x_stride : 0) + n;
-        r.a = *reinterpret_cast<const float4*>(a.x_ptr + row * a.x_ld + f0);
+        r.a = *reinterpret_cast<const float4*>(a.x_ptr + phys_row(rb, rr, a.x_stride) * a.x_ld + f0);
         r.flag = 1;
+    } else if (XM == XM_CM) {
+        if (f0 < 2 * kKhE) {
+            r.a = *reinterpret_cast<const float4*>(cm_piece(a.x_ptr, phys_row(rb, rr, a.x_stride), f0));
+            r.flag = 1;
+        }
     } else if (XM == XM_EDGE_D) {
+        const int64_t n = phys_row(rb, rr, 0);
         const int sidx = a.esrc[n];
         if (sidx >= 0 && f0 == 0) {
             r.a = reinterpret_cast<const float4*>(a.pos)[sidx];
             r.u = reinterpret_cast<const float4*>(a.pos)[a.edst[n]];
             r.flag = 1;
         }
-    } else if (XM == XM_NODE_O) {
+    } else {  // XM_NODE_O
         if (f0 == 0) {
-            r.a = reinterpret_cast<const float4*>(a.pos)[n];
-            r.flag = 1;
-        }
-    } else {  // XM_EDGE_H1: (s, e = n); 32-row blocks never straddle a step (RE % 32 == 0)
-        const int e = (int)n;
-        const int sidx = a.esrc[e];
-        if (sidx >= 0 && f0 < 152) {
-            const int didx = a.edst[e];
-            const float* Us = a.U + s * a.RN * kLdE;
-            const float* Vs = a.V + s * a.RN * kLdE;
-            r.a = *reinterpret_cast<const float4*>(a.A + (uint32_t)(e * kLdE + f0));
-            r.u = *reinterpret_cast<const float4*>(Us + (uint32_t)(sidx * kLdE + f0));
-            r.v = *reinterpret_cast<const float4*>(Vs + (uint32_t)(didx * kLdE + f0));
+            r.a = reinterpret_cast<const float4*>(a.pos)[phys_row(rb, rr, 0)];
             r.flag = 1;
         }
     }
@@ -82,19 +83,14 @@ __device__ __forceinline__ void fetch_x(const WgradArgs& a, const RowBase& rb, i
 
 template <int XM>
 __device__ __forceinline__ float4 finish_x(const WgradArgs& a, int f0, const XRaw& r) {
-    if (XM == XM_ROW) {
+    if (XM == XM_ROW || XM == XM_CM) {
         float4 v = r.flag ? r.a : f4zero();
         if (r.flag && a.x_ones >= f0 && a.x_ones < f0 + 4) f4set(v, a.x_ones - f0, 1.f);
         return v;
     } else if (XM == XM_EDGE_D) {
         return r.flag ? make_float4(r.u.x - r.a.x, r.u.y - r.a.y, 1.f, 0.f) : f4zero();
-    } else if (XM == XM_NODE_O) {
-        return r.flag ? make_float4(r.a.y, r.a.z, 1.f, 0.f) : f4zero();
     } else {
-        if (!r.flag) return f4zero();
-        float4 v = f4relu(f4add3(r.a, r.u, r.v));
-        if (f0 == 148) { v.z = 1.f; v.w = 0.f; }        // feature 150 = ones (b2), 151 = 0
-        return v;
+        return r.flag ? make_float4(r.a.y, r.a.z, 1.f, 0.f) : f4zero();
     }
 }
 
@@ -102,31 +98,29 @@ template <int YM>
 __device__ __forceinline__ void fetch_y(const WgradArgs& a, const RowBase& rb, int rr, int f0, bool in, YRaw& r) {
     r.flag = 0;
     if (!in) return;
-    int64_t s, n;
-    row_at(rb, rr, s, n);
     if (YM == YM_ROW) {
-        const int64_t row = (a.y_stride ? s * a.y_stride : 0) + n;
-        r.g = *reinterpret_cast<const float4*>(a.y_ptr + row * a.y_ld + f0);
-        r.bits = 15u;
+        r.g = *reinterpret_cast<const float4*>(a.y_ptr + phys_row(rb, rr, a.y_stride) * a.y_ld + f0);
         r.flag = 1;
-    } else {  // YM_EDGE_DH2: (s, e = n)
-        const int e = (int)n;
-        const int didx = a.edst[e];
-        if (didx >= 0 && f0 < 152) {
-            const uint32_t* ms = a.mask2 + s * (a.RE / 32) * 160;
-            const uint32_t word = ms[(uint32_t)((e >> 5) * 160 + (f0 >> 5) * 32 + (e & 31))];
-            r.bits = word >> (f0 & 31);
-            const float* Gs = a.G3 + s * a.RN * kLdE;
-            r.g = *reinterpret_cast<const float4*>(Gs + (uint32_t)(didx * kLdE + f0));
-            r.flag = 1;
-        }
+    } else if (f0 < 2 * kKhE) {  // YM_CM
+        r.g = *reinterpret_cast<const float4*>(cm_piece(a.y_ptr, phys_row(rb, rr, a.y_stride), f0));
+        r.flag = 1;
     }
 }
 
-__device__ __forceinline__ float4 finish_y(const YRaw& r) {
-    if (!r.flag) return f4zero();
-    return make_float4((r.bits & 1u) ? r.g.x : 0.f, (r.bits & 2u) ? r.g.y : 0.f, (r.bits & 4u) ? r.g.z : 0.f,
-                       (r.bits & 8u) ? r.g.w : 0.f);
+__device__ __forceinline__ float4 finish_y(const YRaw& r) { return r.flag ? r.g : f4zero(); }
+
+// float4 group g of a 32-row block → (row rr, column group c4): row-major operands walk a row
+// per thread run (coalesced along the row); chunk-major ones walk the 32 rows of a column group
+// (16 bytes per row, 512 contiguous bytes per run).
+template <bool CM, int G>
+__device__ __forceinline__ void group_rc(int g, int& rr, int& c4) {
+    if (CM) {
+        c4 = g >> 5;
+        rr = g & 31;
+    } else {
+        rr = g / G;
+        c4 = g - rr * G;
+    }
 }
 
 // dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n] on v_mfma_f32_16x16x4_f32.
@@ -154,19 +148,19 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     for (int x = 0; x < MX; ++x)
 #pragma unroll
         for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // every operand is fetched a block ahead (PFX); the write-phase fetch of X is kept for shapes
-    // whose raw registers would not fit beside the accumulators
-    constexpr bool PFX = true;
+    // every operand is fetched a block ahead
     XRaw xr[NGX];
     YRaw yr[NGY];
-    const int64_t xcount = (XM == XM_ROW) ? a.x_count : (XM == XM_EDGE_H1 ? a.RE : a.rows);
-    const int64_t ycount = (YM == YM_ROW) ? a.y_count : a.RE;
+    const int64_t xcount = (XM == XM_ROW || XM == XM_CM) ? a.x_count : a.rows;
+    const int64_t ycount = a.y_count;
+    constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM;
     auto fetch_xs = [&](int64_t r0) {
         const RowBase xb = row_base(r0, xcount);
 #pragma unroll
         for (int k = 0; k < NGX; ++k) {
             const int g = tid + k * kWgThreads;
-            const int rr = g / GX, c4 = g - rr * GX;
+            int rr, c4;
+            group_rc<XCM, GX>(g, rr, c4);
             fetch_x<XM>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
         }
     };
@@ -175,53 +169,33 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
 #pragma unroll
         for (int k = 0; k < NGY; ++k) {
             const int g = tid + k * kWgThreads;
-            const int rr = g / GY, c4 = g - rr * GY;
+            int rr, c4;
+            group_rc<YCM, GY>(g, rr, c4);
             fetch_y<YM>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
         }
     };
     auto fetch = [&](int64_t r0) {
-        if (PFX) fetch_xs(r0);
+        fetch_xs(r0);
         fetch_ys(r0);
     };
     fetch(r_begin);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
-        if (PFX) {
 #pragma unroll
-            for (int k = 0; k < NGX; ++k) {
-                const int g = tid + k * kWgThreads;
-                if (g < 32 * GX) {
-                    const int rr = g / GX, c4 = g - rr * GX;
-                    *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
-                }
-            }
-        } else {
-            // two groups in flight at a time (bounded registers)
-            const RowBase xb = row_base(r0, xcount);
-#pragma unroll
-            for (int k0 = 0; k0 < NGX; k0 += 2) {
-#pragma unroll
-                for (int k = k0; k < k0 + 2 && k < NGX; ++k) {
-                    const int g = tid + k * kWgThreads;
-                    const int rr = g / GX, c4 = g - rr * GX;
-                    fetch_x<XM>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
-                }
-#pragma unroll
-                for (int k = k0; k < k0 + 2 && k < NGX; ++k) {
-                    const int g = tid + k * kWgThreads;
-                    if (g < 32 * GX) {
-                        const int rr = g / GX, c4 = g - rr * GX;
-                        *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
+        for (int k = 0; k < NGX; ++k) {
+            const int g = tid + k * kWgThreads;
+            if (g < 32 * GX) {
+                int rr, c4;
+                group_rc<XCM, GX>(g, rr, c4);
+                *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
             }
         }
 #pragma unroll
         for (int k = 0; k < NGY; ++k) {
             const int g = tid + k * kWgThreads;
             if (g < 32 * GY) {
-                const int rr = g / GY, c4 = g - rr * GY;
+                int rr, c4;
+                group_rc<YCM, GY>(g, rr, c4);
                 *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = finish_y(yr[k]);
             }
         }
@@ -354,7 +328,7 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
     SPW_WG(XM_ROW, YM_ROW, 128, 128)
     SPW_WG(XM_EDGE_D, YM_ROW, 32, 160)
     SPW_WG(XM_NODE_O, YM_ROW, 32, 128)
-    SPW_WG(XM_EDGE_H1, YM_EDGE_DH2, 160, 160)
+    SPW_WG(XM_CM, YM_CM, 160, 160)
 #undef SPW_WG
     return hipErrorInvalidValue;
 }

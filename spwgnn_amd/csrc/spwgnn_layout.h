@@ -1,6 +1,7 @@
 // Shared host/device constants and the parameter table of libspwgnn_hip.
 #pragma once
 #include <cstdint>
+#include <hip/hip_runtime.h>
 #include <cstdio>
 
 namespace spw {
@@ -14,6 +15,14 @@ constexpr int kKhE = 76;    // split-halves contraction: features [76h, 76h+76),
 constexpr int kKhN = 52;    // split-halves contraction for 100-wide inputs (104 = 100 + 4 zero)
 constexpr int kNwMaxLimit = 32;   // max nodes per wave-tile (LDS node accumulators)
 constexpr int kDegCol = 150;      // H2s column 150 holds the in-degree (multiplies the rmp.2 bias)
+
+// ---- chunk-major edge rows ("CM"): a 32-edge block of 152-wide rows stored as
+// [q < 19][h < 2][edge i < 32][4] — feature f = 76h + 4q + c. A wave's 16-byte-per-lane access in
+// either orientation (lane = edge) is 1 KiB contiguous, where row-major rows would touch 64 lines.
+constexpr int kCmBlk = 19 * 2 * 32 * 4;   // 4864 floats per block
+__host__ __device__ constexpr int cm_off(int i, int f) {
+    return (((f >= kKhE ? f - kKhE : f) >> 2) * 2 + (f >= kKhE ? 1 : 0)) * 128 + i * 4 + (f & 3);
+}
 
 constexpr int kNumTensors = 22;
 
