@@ -17,7 +17,7 @@ struct Ws {
     int64_t pk;
     int64_t zo1, co, P, a, o1, U, V, H2s;           // node
     int64_t A, z1, z2, z3, cr;                       // edge
-    int64_t mask1, mask2;                            // u32
+    int64_t mask1, mask2, zmask;                     // u32
     int64_t dx, do1, g, G3, dU, dV, dP, dco, dzo2, dzo1;   // node (bwd)
     int64_t dA, dz4, dz3, dz2, dz1;                  // edge (bwd)
     int64_t H1, DH2;                                 // per step: h1 (fwd) and dh2pre (bwd) rows for the W2 gradient
@@ -81,11 +81,12 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.zo1 = take(nN);
         w.a = take(nN * S);
         w.o1 = take(nN * S);
-        w.z1 = take(eE);
-        w.z2 = take(eE);
-        w.z3 = take(eE);
-        w.cr = take(eE);
+        w.z1 = take(eCM);
+        w.z2 = take(eCM);
+        w.z3 = take(eCM);
+        w.cr = take(eCM);
         w.mask1 = take(w.NB * kLdE * S);
+        w.zmask = take(w.NB * 4 * 3 * 64);
         w.mask2 = take(w.NB * 160 * S);
         w.dx = take(nN * S);
         w.do1 = take(nN * S);
@@ -98,16 +99,16 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.dzo2 = take(nN);
         w.dzo1 = take(nN);
         w.dA = take(eE);
-        w.dz4 = take(eE);
-        w.dz3 = take(eE);
-        w.dz2 = take(eE);
-        w.dz1 = take(eE);
+        w.dz4 = take(eCM);
+        w.dz3 = take(eCM);
+        w.dz2 = take(eCM);
+        w.dz1 = take(eCM);
         w.H1 = take(eCM * S);
         w.DH2 = take(eCM * S);
         w.slab_floats = (int64_t)(kMaxChunks + kReduceGroups) * 160 * 160;
         w.slab = take(w.slab_floats);
     } else {
-        w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = -1;
+        w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = w.zmask = -1;
         w.dx = w.do1 = w.g = w.G3 = w.dU = w.dV = w.dP = w.dco = w.dzo2 = w.dzo1 = -1;
         w.dA = w.dz4 = w.dz3 = w.dz2 = w.dz1 = w.slab = w.H1 = w.DH2 = -1;
         w.slab_floats = 0;
@@ -283,6 +284,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.z3 = c.f(w.z3);
     ee.cr = c.f(w.cr);
     ee.A = c.f(w.A);
+    ee.zmask = r->training ? c.u(w.zmask) : nullptr;
     ee.dropout_on = drop;
     ee.thresh = thresh;
     ee.scale = scale;
@@ -488,10 +490,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     EncEdgeBwdArgs eeb{};
     eeb.n_eblocks = b->n_eblocks;
     eeb.dA = c.f(w.dA);
-    eeb.cr = c.f(w.cr);
-    eeb.z3 = c.f(w.z3);
-    eeb.z2 = c.f(w.z2);
-    eeb.z1 = c.f(w.z1);
+    eeb.zmask = c.u(w.zmask);
     eeb.w1at = c.pk(PK_W1AT);
     eeb.rm3t = c.pk(PK_RM3T);
     eeb.rm2t = c.pk(PK_RM2T);
@@ -526,15 +525,17 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     };
     int32_t e;
     {   // rm.0: X = [d | 1]
-        WgSpec g; g.xmode = XM_EDGE_D; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
+        WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
         if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
-    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
+    auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
+    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, st))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre — chunk-major rows kept by the edge kernels
         WgSpec g; edge_row(g, w.H1, w.DH2, T_RMP1K, T_RMP1B);
         g.xmode = XM_CM; g.ymode = YM_CM;

@@ -75,6 +75,30 @@ __device__ __forceinline__ void load_cm(const float* __restrict__ blk, f32x16 (&
         }
 }
 
+// ---- per-lane activation-sign bits of NT C-layout tiles (bit 16t + r of the lane's words), so a
+// backward pass in the same orientation reads 3 words per lane instead of the activations.
+template <int NT>
+__device__ __forceinline__ void store_pos_bits(uint32_t* __restrict__ words, const f32x16 (&X)[NT], int lane) {
+    uint32_t w[(NT * 16 + 31) / 32] = {};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[(16 * t + r) >> 5] |= (X[t][r] > 0.f ? 1u : 0u) << ((16 * t + r) & 31);
+#pragma unroll
+    for (int k = 0; k < (NT * 16 + 31) / 32; ++k) words[64 * k + lane] = w[k];
+}
+template <int NT>
+__device__ __forceinline__ void apply_pos_bits(const uint32_t* __restrict__ words, f32x16 (&X)[NT], int lane, float scale) {
+    uint32_t w[(NT * 16 + 31) / 32];
+#pragma unroll
+    for (int k = 0; k < (NT * 16 + 31) / 32; ++k) w[k] = words[64 * k + lane];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            X[t][r] = ((w[(16 * t + r) >> 5] >> ((16 * t + r) & 31)) & 1u) ? X[t][r] * scale : 0.f;
+}
+
 // ---- split-halves row chunk: lane half h holds features [KH*h, KH*h+KH) of its row.
 template <int KH>
 __device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh, float (&x)[KH]) {

@@ -39,7 +39,8 @@ struct EncEdgeArgs {
     const float* pos;
     const int32_t *esrc, *edst, *node_tower, *node_local;
     const float *w_rm0, *b_rm0, *w_rm1, *b_rm1, *w_rm2, *b_rm2, *w_rm3, *b_rm3, *w_w1a, *b_w1a;
-    float *z1, *z2, *z3, *cr, *A;
+    float *z1, *z2, *z3, *cr, *A;   // chunk-major blocks
+    uint32_t* zmask;                // [blk][4 layers: z1,z2,z3,cr][3 words][64 lanes] — activation > 0 bits
     int dropout_on;
     uint32_t thresh;
     float scale;
@@ -88,7 +89,8 @@ struct EdgeBwdArgs {
 
 struct EncEdgeBwdArgs {
     int n_eblocks;
-    const float *dA, *cr, *z3, *z2, *z1;
+    const float* dA;                // row-major [e][160] (accumulated by k_edge_bwd)
+    const uint32_t* zmask;          // from k_enc_edge
     const float *w1at, *rm3t, *rm2t, *rm1t;
     float *dz4, *dz3, *dz2, *dz1;
     float scale;   // dropout 1/(1-p) (1 when off)

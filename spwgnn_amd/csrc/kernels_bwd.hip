@@ -319,40 +319,27 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (blk >= a.n_eblocks) return;
     const int64_t e = (int64_t)blk * 32 + j;
-    const int64_t row = e * kLdE;
-    f32x16 D[5], E[5], Z[5];
+    const uint32_t* mb = a.zmask + (int64_t)blk * 4 * 3 * 64;   // z1, z2, z3, cr > 0 bits
+    float* const db = a.dz4 + (int64_t)blk * kCmBlk;          // chunk-major outputs
+    const int64_t cmo = (int64_t)blk * kCmBlk;
+    f32x16 D[5], E[5];
     zero_tiles(D);
-    tgemm_stream_acc<5, kKhE, kLdE>(a.dA + row + kKhE * h, D, a.w1at, lane);  // dc_r = dA·W1aᵀ
-    load_rho<5>(a.cr + row, Z, h);
-#pragma unroll
-    for (int t = 0; t < 5; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) D[t][r] = Z[t][r] > 0.f ? D[t][r] * a.scale : 0.f;  // relu + dropout
-    store_rho<5>(a.dz4 + row, D, h);
+    tgemm_stream_acc<5, kKhE, kLdE>(a.dA + e * kLdE + kKhE * h, D, a.w1at, lane);  // dc_r = dA·W1aᵀ
+    apply_pos_bits<5>(mb + 9 * 64, D, lane, a.scale);   // relu + dropout of c_r
+    store_cm<5>(db, D, lane, true);
     zero_tiles(E);
     tchain_acc<5, 5, 12, kLdE>(D, E, a.rm3t, lane);
-    load_rho<5>(a.z3 + row, Z, h);
-#pragma unroll
-    for (int t = 0; t < 5; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) E[t][r] = Z[t][r] > 0.f ? E[t][r] : 0.f;
-    store_rho<5>(a.dz3 + row, E, h);
+    apply_pos_bits<5>(mb + 6 * 64, E, lane, 1.f);
+    store_cm<5>(a.dz3 + cmo, E, lane, true);
     zero_tiles(D);
     tchain_acc<5, 5, 12, kLdE>(E, D, a.rm2t, lane);
-    load_rho<5>(a.z2 + row, Z, h);
-#pragma unroll
-    for (int t = 0; t < 5; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) D[t][r] = Z[t][r] > 0.f ? D[t][r] : 0.f;
-    store_rho<5>(a.dz2 + row, D, h);
+    apply_pos_bits<5>(mb + 3 * 64, D, lane, 1.f);
+    store_cm<5>(a.dz2 + cmo, D, lane, true);
     zero_tiles(E);
     tchain_acc<5, 5, 12, kLdE>(D, E, a.rm1t, lane);
-    load_rho<5>(a.z1 + row, Z, h);
-#pragma unroll
-    for (int t = 0; t < 5; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) E[t][r] = Z[t][r] > 0.f ? E[t][r] : 0.f;
-    store_rho<5>(a.dz1 + row, E, h);
+    apply_pos_bits<5>(mb, E, lane, 1.f);
+    store_cm<5>(a.dz1 + cmo, E, lane, true);
+    (void)h;
 }
 
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_node_bwd(EncNodeBwdArgs a) {

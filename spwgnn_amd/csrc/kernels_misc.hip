@@ -322,11 +322,11 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
         hipLaunchKernelGGL((k_wgrad_t<XM, YM, KX, NY>), g, b, 0, st, a);                      \
         return hipGetLastError();                                                             \
     }
-    SPW_WG(XM_ROW, YM_ROW, 160, 160)
+    SPW_WG(XM_CM, YM_ROW, 160, 160)
     SPW_WG(XM_ROW, YM_ROW, 128, 160)
     SPW_WG(XM_ROW, YM_ROW, 160, 128)
     SPW_WG(XM_ROW, YM_ROW, 128, 128)
-    SPW_WG(XM_EDGE_D, YM_ROW, 32, 160)
+    SPW_WG(XM_EDGE_D, YM_CM, 32, 160)
     SPW_WG(XM_NODE_O, YM_ROW, 32, 128)
     SPW_WG(XM_CM, YM_CM, 160, 160)
 #undef SPW_WG
