@@ -26,21 +26,22 @@ struct Ws {
     PackSlots ps;
     int sP() const { return training ? S + 1 : 2; }
     int sStep() const { return training ? S : 1; }
-    int64_t P_at(int s) const { return P + (int64_t)(training ? s : (s & 1)) * RN * kLdN; }
-    int64_t U_at(int s) const { return U + (int64_t)(training ? s : 0) * RN * kLdE; }
-    int64_t V_at(int s) const { return V + (int64_t)(training ? s : 0) * RN * kLdE; }
-    int64_t H2s_at(int s) const { return H2s + (int64_t)(training ? s : 0) * RN * kLdE; }
-    int64_t a_at(int s) const { return a + (int64_t)s * RN * kLdN; }
-    int64_t o1_at(int s) const { return o1 + (int64_t)s * RN * kLdN; }
+    // node arrays are chunk-major (104 / 152 floats per row): a step's rows are RN/32 blocks
+    int64_t P_at(int s) const { return P + (int64_t)(training ? s : (s & 1)) * RN * kRowN; }
+    int64_t U_at(int s) const { return U + (int64_t)(training ? s : 0) * RN * kRowE; }
+    int64_t V_at(int s) const { return V + (int64_t)(training ? s : 0) * RN * kRowE; }
+    int64_t H2s_at(int s) const { return H2s + (int64_t)(training ? s : 0) * RN * kRowE; }
+    int64_t a_at(int s) const { return a + (int64_t)s * RN * kRowN; }
+    int64_t o1_at(int s) const { return o1 + (int64_t)s * RN * kRowN; }
     int64_t m1_at(int s) const { return mask1 + (int64_t)s * NB * kLdE; }
     int64_t m2_at(int s) const { return mask2 + (int64_t)s * NB * 160; }
-    int64_t dx_at(int s) const { return dx + (int64_t)s * RN * kLdN; }
-    int64_t do1_at(int s) const { return do1 + (int64_t)s * RN * kLdN; }
-    int64_t g_at(int s) const { return g + (int64_t)s * RN * kLdN; }
-    int64_t G3_at(int s) const { return G3 + (int64_t)s * RN * kLdE; }
-    int64_t dU_at(int s) const { return dU + (int64_t)s * RN * kLdE; }
-    int64_t dV_at(int s) const { return dV + (int64_t)s * RN * kLdE; }
-    int64_t dP_at(int k) const { return dP + (int64_t)(k & 1) * RN * kLdN; }
+    int64_t dx_at(int s) const { return dx + (int64_t)s * RN * kRowN; }
+    int64_t do1_at(int s) const { return do1 + (int64_t)s * RN * kRowN; }
+    int64_t g_at(int s) const { return g + (int64_t)s * RN * kRowN; }
+    int64_t G3_at(int s) const { return G3 + (int64_t)s * RN * kRowE; }
+    int64_t dU_at(int s) const { return dU + (int64_t)s * RN * kRowE; }
+    int64_t dV_at(int s) const { return dV + (int64_t)s * RN * kRowE; }
+    int64_t dP_at(int k) const { return dP + (int64_t)(k & 1) * RN * kRowN; }
     int64_t H1_at(int s) const { return H1 + (int64_t)s * NB * kCmBlk; }
     int64_t DH2_at(int s) const { return DH2 + (int64_t)s * NB * kCmBlk; }
 };
@@ -69,7 +70,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     }
     w.ps.total = poff;
     w.pk = take(poff);
-    const int64_t nN = w.RN * kLdN, nE = w.RN * kLdE, eE = w.RE * kLdE;
+    const int64_t nN = w.RN * kRowN, nE = w.RN * kRowE, eE = w.RE * kLdE;
     w.co = take(nN);
     w.P = take(nN * w.sP());
     w.U = take(nE * w.sStep());
@@ -547,6 +548,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.x = c.f(xoff); g.x_ld = xld; g.x_width = xw; g.x_ones = xones; g.x_count = nN; g.x_stride = xstride;
         g.y = c.f(yoff); g.y_ld = yld; g.y_width = yw; g.y_count = nN; g.y_stride = RN;
         g.rows = nN * S; g.kx_pad = kxp; g.ny_pad = nyp;
+        g.xmode = XM_CM; g.ymode = YM_CM;   // chunk-major node rows
     };
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
@@ -584,7 +586,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         if ((e = run_wgrad(c, b, g, grads, st))) return e;
     }
     {   // om.0: X = [y, w | 1]
-        WgSpec g; g.xmode = XM_NODE_O; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
+        WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
         if ((e = run_wgrad(c, b, g, grads, st))) return e;

@@ -41,25 +41,28 @@ __device__ __forceinline__ void load_rho(const float* __restrict__ row, f32x16 (
         }
 }
 
-// ---- chunk-major block rows (transposed orientation, lane (j, h) = edge j of the block):
-// regs 4q..4q+3 of tile t are features f0 = 32t + 8q + 4h .. +3, one 16-byte piece (f0 < 152).
+// ---- chunk-major block rows (transposed orientation, lane (j, h) = row j of the 32-row block):
+// regs 4q..4q+3 of tile t are features f0 = 32t + 8q + 4h .. +3, one 16-byte piece; NT = 5 tiles
+// ↔ 152-feature blocks (KH 76), NT = 4 ↔ 104-feature blocks (KH 52).
 template <int NT>
 __device__ __forceinline__ void store_cm(float* __restrict__ blk, const f32x16 (&X)[NT], int lane, bool valid) {
+    constexpr int KH = NT == 5 ? kKhE : kKhN;
     const int j = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int f0 = 32 * t + 8 * q + 4 * h;
-            if (32 * t + 8 * q < 2 * kKhE) {   // f0 < 152 (both halves: 8q + 32t ≤ 144)
+            if (32 * t + 8 * q + 4 < 2 * KH) {   // f0 < 2·KH on both halves
                 float4 v = valid ? make_float4(X[t][4 * q], X[t][4 * q + 1], X[t][4 * q + 2], X[t][4 * q + 3])
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-                *reinterpret_cast<float4*>(blk + cm_off(j, f0)) = v;
+                *reinterpret_cast<float4*>(blk + cm_offk<KH>(j, f0)) = v;
             }
         }
 }
 template <int NT>
 __device__ __forceinline__ void load_cm(const float* __restrict__ blk, f32x16 (&X)[NT], int lane) {
+    constexpr int KH = NT == 5 ? kKhE : kKhN;
     const int j = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -67,12 +70,30 @@ __device__ __forceinline__ void load_cm(const float* __restrict__ blk, f32x16 (&
         for (int q = 0; q < 4; ++q) {
             const int f0 = 32 * t + 8 * q + 4 * h;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (32 * t + 8 * q < 2 * kKhE) v = *reinterpret_cast<const float4*>(blk + cm_off(j, f0));
+            if (32 * t + 8 * q + 4 < 2 * KH) v = *reinterpret_cast<const float4*>(blk + cm_offk<KH>(j, f0));
             X[t][4 * q] = v.x;
             X[t][4 * q + 1] = v.y;
             X[t][4 * q + 2] = v.z;
             X[t][4 * q + 3] = v.w;
         }
+}
+// split-halves chunk of a chunk-major row: x[s] = feature KH·h + s of row j
+template <int KH>
+__device__ __forceinline__ void load_half_cm(const float* __restrict__ blk, int lane, float (&x)[KH]) {
+    const float* p = blk + ((lane >> 5) * 32 + (lane & 31)) * 4;
+#pragma unroll
+    for (int q = 0; q < KH / 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(p + 256 * q);
+        x[4 * q] = v.x;
+        x[4 * q + 1] = v.y;
+        x[4 * q + 2] = v.z;
+        x[4 * q + 3] = v.w;
+    }
+}
+// feature f of row `row` in a chunk-major array (block size KH·64 floats)
+template <int KH>
+__device__ __forceinline__ int64_t cm_index(int64_t row, int f) {
+    return (row >> 5) * (KH * 64) + cm_offk<KH>((int)(row & 31), f);
 }
 
 // ---- per-lane activation-sign bits of NT C-layout tiles (bit 16t + r of the lane's words), so a
@@ -186,7 +207,9 @@ __device__ __forceinline__ void tgemm_half_acc(const float (&x)[KH], f32x16 (&ou
 
 // ---- transposed orientation, B operand streamed from a split-halves global row (features
 // KH*h + s, 16 bytes at a time), k4-blocked weight. Rolled loop (bounded registers).
-template <int NT_OUT, int KH, int N>
+// XS = float4 stride between consecutive 4-feature chunks of the row: 1 for row-major rows,
+// 64 for chunk-major blocks (row_khh then points at the lane's (h, j) piece of chunk 0).
+template <int NT_OUT, int KH, int N, int XS = 1>
 __device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_khh, f32x16 (&out)[NT_OUT],
                                                  const float* __restrict__ W4, int lane) {
     static_assert(KH % 4 == 0, "16-byte fragments");
@@ -194,7 +217,7 @@ __device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_k
     const float* wb = W4 + ((KH / 4) * (lane >> 5) * N + (lane & 31)) * 4;
     static_assert((KH / 4) % 2 == 1, "ring schedule below: odd chunk count");
     float4 w0[NT_OUT], w1[NT_OUT];
-    float4 x0 = x4[0], x1;
+    float4 x0 = x4[0], x1;  // chunk q at x4[XS·q]
 #pragma unroll
     for (int t = 0; t < NT_OUT; ++t) w0[t] = *reinterpret_cast<const float4*>(wb + 128 * t);
     // two register slots with static names (loop unrolled by 2): the prefetch of chunk q+1 is
@@ -203,7 +226,7 @@ __device__ __forceinline__ void tgemm_stream_acc(const float* __restrict__ row_k
         const int qn = min(q + 1, KH / 4 - 1);   // unconditional (clamped) prefetch
 #pragma unroll
         for (int t = 0; t < NT_OUT; ++t) nw[t] = *reinterpret_cast<const float4*>(wb + 4 * N * qn + 128 * t);
-        nx = x4[qn];
+        nx = x4[XS * qn];
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < NT_OUT; ++t) {

@@ -20,16 +20,16 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     if (nb * 32 >= a.n_nodes) return;
     const int n = nb * 32 + j;
     const bool valid = n < a.n_nodes;
-    const int64_t nc = valid ? n : a.n_nodes - 1;
-    const int64_t rowN = (int64_t)n * kLdN;
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;   // chunk-major node blocks
+    const int pj = (h * 32 + j) * 4;                                        // this lane's piece
 
     f32x16 D[4];
     if (a.first) {
         zero_tiles(D);
     } else {
-        load_rho<4>(a.dPin + nc * kLdN, D, h);
-        tgemm_stream_acc<4, kKhE, kLdN>(a.dU + nc * kLdE + kKhE * h, D, a.w1bt, lane);
-        tgemm_stream_acc<4, kKhE, kLdN>(a.dV + nc * kLdE + kKhE * h, D, a.w1ct, lane);
+        load_cm<4>(a.dPin + bN, D, lane);
+        tgemm_stream_acc<4, kKhE, kLdN, 64>(a.dU + bE + pj, D, a.w1bt, lane);
+        tgemm_stream_acc<4, kKhE, kLdN, 64>(a.dV + bE + pj, D, a.w1ct, lane);
     }
     if (a.tail) {  // dP0 = d/d 'propagation' (ld 100)
         if (valid) {
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
     {
         f32x16 Pn[4];
-        load_rho<4>(a.Pn + nc * kLdN, Pn, h);
+        load_cm<4>(a.Pn + bN, Pn, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -58,49 +58,49 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
     }
     // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
-    store_rho_masked<4>(a.dPout + rowN, D, h, valid);
+    store_cm<4>(a.dPout + bN, D, lane, valid);
     if (a.first && h == 1) D[3][0] = valid ? a.dlogits[n] : 0.f;  // x' row 100 = logit
-    store_rho_masked<4>(a.dx + rowN, D, h, valid);
+    store_cm<4>(a.dx + bN, D, lane, valid);
 
     f32x16 G[4];
     zero_tiles(G);
     tchain_acc<4, 4, 4, kLdN>(D, G, a.wo2t, lane);
     {
         f32x16 O1[4];
-        load_rho<4>(a.o1 + nc * kLdN, O1, h);
+        load_cm<4>(a.o1 + bN, O1, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) G[t][r] = O1[t][r] > 0.f ? G[t][r] : 0.f;
     }
-    store_rho_masked<4>(a.do1 + rowN, G, h, valid);
+    store_cm<4>(a.do1 + bN, G, lane, valid);
 
     // P part of omp's input → dP_s
     zero_tiles(D);
     tchain_acc<4, 4, 4, kLdN>(G, D, a.wo1pt, lane);
     {
         f32x16 T[4];
-        load_rho<4>(a.dPout + nc * kLdN, T, h);
+        load_cm<4>(a.dPout + bN, T, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t) D[t] += T[t];
     }
-    store_rho_masked<4>(a.dPout + rowN, D, h, valid);
+    store_cm<4>(a.dPout + bN, D, lane, valid);
     // c_o part → dc_o (accumulated over steps in step order S-1..0)
     zero_tiles(D);
     tchain_acc<4, 4, 4, kLdN>(G, D, a.wo1ct, lane);
     if (a.dco_accumulate) {
         f32x16 T[4];
-        load_rho<4>(a.dco + nc * kLdN, T, h);
+        load_cm<4>(a.dco + bN, T, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t) D[t] = T[t] + D[t];
     }
-    store_rho_masked<4>(a.dco + rowN, D, h, valid);
+    store_cm<4>(a.dco + bN, D, lane, valid);
     // effect part → g = da ⊙ (1 - a²) → G3 = g·W3ᵀ
     zero_tiles(D);
     tchain_acc<4, 4, 4, kLdN>(G, D, a.wo1at, lane);
     {
         f32x16 Aa[4];
-        load_rho<4>(a.a + nc * kLdN, Aa, h);
+        load_cm<4>(a.a + bN, Aa, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -109,11 +109,11 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 D[t][r] = D[t][r] * (1.f - v * v);
             }
     }
-    store_rho_masked<4>(a.g + rowN, D, h, valid);
+    store_cm<4>(a.g + bN, D, lane, valid);
     f32x16 H[5];
     zero_tiles(H);
     tchain_acc<5, 4, 4, kLdE>(D, H, a.w3t, lane);
-    store_rho_masked<5>(a.G3 + (int64_t)n * kLdE, H, h, valid);
+    store_cm<5>(a.G3 + bE, H, lane, valid);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -197,7 +197,8 @@ void k_edge_bwd(EdgeBwdArgs a) {
         const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
                                     : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
         const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
-        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + (int64_t)dc * kLdE + kKhE * h);
+        // G3[receiver]: chunk-major node row, chunk q at +64q float4
+        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + cm_index<kKhE>(dc, 0) + h * 128);
         f32x16 acc[5];
         zero_tiles(acc);
         // G3 rows (L2-resident node rows) run one chunk ahead in a 2-slot ring (loop unrolled by
@@ -212,7 +213,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
             xv[2] = (bits & 4u) ? g.z : 0.f;
             xv[3] = (bits & 8u) ? g.w : 0.f;
             *reinterpret_cast<float4*>(dh2cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
-            ahead = G4[min(q + 1, kKhE / 4 - 1)];  // unconditional (clamped) prefetch
+            ahead = G4[64 * min(q + 1, kKhE / 4 - 1)];  // unconditional (clamped) prefetch
             const float* wq = wrow + (ONEHOT ? 4 * q : 4 * q * kLdE);
             float4 wv = ONEHOT ? *reinterpret_cast<const float4*>(wq)
                                : make_float4(wq[0], wq[kLdE], wq[2 * kLdE], wq[3 * kLdE]);
@@ -297,17 +298,20 @@ void k_edge_bwd(EdgeBwdArgs a) {
             const int row = rho(r, 0) + 4 * h;
             const int node = row & 15;
             if (node < nn) {
-                float* o = (row < 16 ? a.dV : a.dU) + (int64_t)(n0 + node) * kLdE + i;
+                float* o = row < 16 ? a.dV : a.dU;   // chunk-major node rows
 #pragma unroll
-                for (int t = 0; t < 5; ++t) o[32 * t] = nacc[t][r];
+                for (int t = 0; t < 5; ++t)
+                    if (32 * t + i < 2 * kKhE) o[cm_index<kKhE>(n0 + node, 32 * t + i)] = nacc[t][r];
             }
         }
     } else {
-        float* oU = a.dU + (int64_t)n0 * kLdE;
-        float* oV = a.dV + (int64_t)n0 * kLdE;
         for (int idx = lane; idx < nn * kLdE; idx += 64) {
-            oU[idx] = naccS[idx];
-            oV[idx] = naccR[idx];
+            const int node = idx / kLdE, f = idx - node * kLdE;
+            if (f < 2 * kKhE) {
+                const int64_t o = cm_index<kKhE>(n0 + node, f);   // chunk-major node rows
+                a.dU[o] = naccS[idx];
+                a.dV[o] = naccR[idx];
+            }
         }
     }
     }
@@ -348,23 +352,23 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     if (nb * 32 >= a.n_nodes) return;
     const int n = nb * 32 + j;
     const bool valid = n < a.n_nodes;
-    const int64_t nc = valid ? n : a.n_nodes - 1;
+    const int64_t bN = (int64_t)nb * kCmBlkN;   // chunk-major node block
     f32x16 D[4], Z[4], E[4];
-    load_rho<4>(a.dco + nc * kLdN, D, h);
-    load_rho<4>(a.co + nc * kLdN, Z, h);
+    load_cm<4>(a.dco + bN, D, lane);
+    load_cm<4>(a.co + bN, Z, lane);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) D[t][r] = Z[t][r] > 0.f ? D[t][r] * a.scale : 0.f;
-    store_rho_masked<4>(a.dzo2 + (int64_t)n * kLdN, D, h, valid);
+    store_cm<4>(a.dzo2 + bN, D, lane, valid);
     zero_tiles(E);
     tchain_acc<4, 4, 4, kLdN>(D, E, a.om1t, lane);
-    load_rho<4>(a.zo1 + nc * kLdN, Z, h);
+    load_cm<4>(a.zo1 + bN, Z, lane);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) E[t][r] = Z[t][r] > 0.f ? E[t][r] : 0.f;
-    store_rho_masked<4>(a.dzo1 + (int64_t)n * kLdN, E, h, valid);
+    store_cm<4>(a.dzo1 + bN, E, lane, valid);
 }
 
 // ------------------------------------------------------------------------------------------------

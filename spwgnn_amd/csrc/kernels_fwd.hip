@@ -57,7 +57,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const int f = rho(r, 0) + 4 * h + 32 * t;
             Z[t][r] = relu(o0 * a.w_om0[f] + o1 * a.w_om0[128 + f] + a.b_om0[f]);
         }
-    if (a.zo1) store_rho_masked<4>(a.zo1 + (int64_t)n * kLdN, Z, h, valid);
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;   // chunk-major node blocks
+    if (a.zo1) store_cm<4>(a.zo1 + bN, Z, lane, valid);
 
     f32x16 C[4];
     zero_tiles(C);
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 C[t][r] = drop_keep(key, (uint32_t)f, a.thresh) ? C[t][r] * a.scale : 0.f;
             }
     }
-    store_rho_masked<4>(a.co + (int64_t)n * kLdN, C, h, valid);
+    store_cm<4>(a.co + bN, C, lane, valid);
 
     // P0: the 'propagation' input (Networks.py:119,169), ld 100 → workspace ld 128
     f32x16 P[4];
@@ -89,15 +90,15 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             P[t][4 * q + 2] = v.z;
             P[t][4 * q + 3] = v.w;
         }
-    store_rho_masked<4>(a.P0 + (int64_t)n * kLdN, P, h, valid);
+    store_cm<4>(a.P0 + bN, P, lane, valid);
 
     f32x16 U[5];
     zero_tiles(U);
     tchain_acc<5, 4, 4, kLdE>(P, U, a.w1b, lane);
-    store_rho_masked<5>(a.U0 + (int64_t)n * kLdE, U, h, valid);
+    store_cm<5>(a.U0 + bE, U, lane, valid);
     zero_tiles(U);
     tchain_acc<5, 4, 4, kLdE>(P, U, a.w1c, lane);
-    store_rho_masked<5>(a.V0 + (int64_t)n * kLdE, U, h, valid);
+    store_cm<5>(a.V0 + bE, U, lane, valid);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -205,15 +206,17 @@ template <> struct NodeSum<true> {
             }
         }
     }
-    // reg r of tile T: node 4·kq + r, feature 16T + (lane&15)
-    __device__ __forceinline__ void store(float* rows, int nn, int lane) const {
-        float* o = rows + (lane & 15);
+    // reg r of tile T: node 4·kq + r, feature 16T + (lane&15); H2s is chunk-major
+    __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int node = 4 * kq + r;
             if (node < nn) {
 #pragma unroll
-                for (int t = 0; t < 10; ++t) o[node * kLdE + 16 * t] = acc[t][r];
+                for (int t = 0; t < 10; ++t) {
+                    const int f = 16 * t + (lane & 15);
+                    if (f < 2 * kKhE) H2s[cm_index<kKhE>(n0 + node, f)] = acc[t][r];
+                }
             }
         }
     }
@@ -235,16 +238,18 @@ template <> struct NodeSum<false> {
             for (int t = 0; t < 5; ++t) acc[t] = mfma32(oh, h2[t][r], acc[t]);
         }
     }
-    // reg r of tile t: node rho(r,h), feature 32t + (lane&31)
-    __device__ __forceinline__ void store(float* rows, int nn, int lane) const {
+    // reg r of tile t: node rho(r,h), feature 32t + (lane&31); H2s is chunk-major
+    __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
         const int h = lane >> 5;
-        float* o = rows + (lane & 31);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int node = rho(r, 0) + 4 * h;
             if (node < nn) {
 #pragma unroll
-                for (int t = 0; t < 5; ++t) o[node * kLdE + 32 * t] = acc[t][r];
+                for (int t = 0; t < 5; ++t) {
+                    const int f = 32 * t + (lane & 31);
+                    if (f < 2 * kKhE) H2s[cm_index<kKhE>(n0 + node, f)] = acc[t][r];
+                }
             }
         }
     }
@@ -281,8 +286,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const uint64_t vmask = __ballot(valid);
         const float vf = valid ? 1.f : 0.f;
         const float* Acm = a.A + (int64_t)blk * kCmBlk + h * 128 + i * 4;   // chunk q at + 256q
-        const float4* U4 = reinterpret_cast<const float4*>(a.U + (int64_t)sc * kLdE + kKhE * h);
-        const float4* V4 = reinterpret_cast<const float4*>(a.V + (int64_t)dc * kLdE + kKhE * h);
+        // U[s], V[r]: chunk-major node rows (chunk q at +256q), gathered per lane
+        const float4* U4 = reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 4 * 0) + h * 128);
+        const float4* V4 = reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 4 * 0) + h * 128);
         // h1 > 0 bits (mask1: word per (block, feature), bit = edge): each chunk's 8 ballots go
         // into lanes 0..7 of one staging register (lanes 0-3: features 4q+c, lanes 4-7: 76+4q+c)
         // and are stored straight away.
@@ -296,7 +302,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         float* h1cm = a.h1_out ? a.h1_out + (int64_t)blk * kCmBlk + h * 128 + i * 4 : nullptr;
         auto ldA = [&](int q) { return *reinterpret_cast<const float4*>(Acm + 256 * q); };
         struct AUV { float4 a, u, v; };
-        AUV b0{ldA(0), U4[0], V4[0]}, b1{ldA(1), U4[1], V4[1]}, b2;
+        AUV b0{ldA(0), U4[0], V4[0]}, b1{ldA(1), U4[64], V4[64]}, b2;
         auto chunk = [&](int q, const AUV& cur, AUV& ahead) {
             float xv[4];
             xv[0] = relu(cur.a.x + cur.u.x + cur.v.x) * vf;
@@ -306,8 +312,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             if (h1cm) *reinterpret_cast<float4*>(h1cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
             const int qn = min(q + 2, kKhE / 4 - 1);   // unconditional (clamped) prefetch
             ahead.a = ldA(qn);
-            ahead.u = U4[qn];
-            ahead.v = V4[qn];
+            ahead.u = U4[64 * qn];
+            ahead.v = V4[64 * qn];
             float4 wv = *reinterpret_cast<const float4*>(wrow + 4 * q);
 #pragma unroll
             for (int t = 0; t < 5; ++t) {
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         nsum.add(acc, d);
     }
     // the wave-tile's node rows (each node is owned by exactly one wave-tile)
-    nsum.store(a.H2s + (int64_t)n0 * kLdE, nn, lane);
+    nsum.store(a.H2s, n0, nn, lane);
     }
 }
 
@@ -386,13 +392,13 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     if (nb * 32 >= a.n_nodes) return;
     const int n = nb * 32 + j;
     const bool valid = n < a.n_nodes;
-    const int64_t nc = valid ? n : a.n_nodes - 1;
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;   // chunk-major node blocks
 
     f32x16 E[4];
     zero_tiles(E);
     {
         float xb[kKhE];
-        load_half<kKhE>(a.H2s + nc * kLdE + kKhE * h, xb);
+        load_half_cm<kKhE>(a.H2s + bE, lane, xb);
         tgemm_half_acc<4, kKhE, kLdN>(xb, E, a.w3a, lane);
     }
 #pragma unroll
@@ -402,23 +408,23 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const int f = rho(r, 0) + 4 * h + 32 * t;
             E[t][r] = f < kFN ? tanhf(E[t][r]) : 0.f;
         }
-    if (a.a_out) store_rho_masked<4>(a.a_out + (int64_t)n * kLdN, E, h, valid);
+    if (a.a_out) store_cm<4>(a.a_out + bN, E, lane, valid);
 
     f32x16 O[4];
     zero_tiles(O);
     {
         float xb[kKhN];
-        load_half<kKhN>(a.co + nc * kLdN + kKhN * h, xb);
+        load_half_cm<kKhN>(a.co + bN, lane, xb);
         tgemm_half_acc<4, kKhN, kLdN>(xb, O, a.wo1c, lane);
     }
     tchain_acc<4, 4, 4, kLdN>(E, O, a.wo1a, lane);
     {
         float xb[kKhN];
-        load_half<kKhN>(a.P + nc * kLdN + kKhN * h, xb);
+        load_half_cm<kKhN>(a.P + bN, lane, xb);
         tgemm_half_acc<4, kKhN, kLdN>(xb, O, a.wo1p, lane);
     }
     bias_act_rho<4, true>(O, a.bo1, h);
-    if (a.o1_out) store_rho_masked<4>(a.o1_out + (int64_t)n * kLdN, O, h, valid);
+    if (a.o1_out) store_cm<4>(a.o1_out + bN, O, lane, valid);
 
     f32x16 X[4];
     zero_tiles(X);
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     bias_act_rho<4, false>(X, a.bo2p, h);
     {
         f32x16 P[4];
-        load_rho<4>(a.P + nc * kLdN, P, h);
+        load_cm<4>(a.P + bN, P, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -436,15 +442,15 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
     }
     if (a.logits && h == 1 && valid) a.logits[n] = X[3][0];  // x' row 100 = rho(0,1) + 96
-    store_rho_masked<4>(a.Pn + (int64_t)n * kLdN, E, h, valid);
+    store_cm<4>(a.Pn + bN, E, lane, valid);
     if (a.U) {
         f32x16 U[5];
         zero_tiles(U);
         tchain_acc<5, 4, 4, kLdE>(E, U, a.w1b, lane);
-        store_rho_masked<5>(a.U + (int64_t)n * kLdE, U, h, valid);
+        store_cm<5>(a.U + bE, U, lane, valid);
         zero_tiles(U);
         tchain_acc<5, 4, 4, kLdE>(E, U, a.w1c, lane);
-        store_rho_masked<5>(a.V + (int64_t)n * kLdE, U, h, valid);
+        store_cm<5>(a.V + bE, U, lane, valid);
     }
 }
 

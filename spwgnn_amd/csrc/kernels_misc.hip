@@ -48,12 +48,14 @@ __device__ __forceinline__ int64_t phys_row(const RowBase& b, int rr, int64_t st
     row_at(b, rr, s, n);
     return (stride ? s * stride : 0) + n;
 }
-// chunk-major rows: block = row / 32 (32-row blocks never straddle a step: RE % 32 == 0)
+// chunk-major rows: block = row / 32 (32-row blocks never straddle a step: RE, RN % 32 == 0);
+// 160-wide operands are 152-feature blocks (KH 76), 128-wide ones 104-feature blocks (KH 52)
+template <int W>
 __device__ __forceinline__ const float* cm_piece(const float* base, int64_t row, int f0) {
-    return base + (row >> 5) * kCmBlk + cm_off((int)(row & 31), f0);
+    return base + cm_index<W == 160 ? kKhE : kKhN>(row, f0);
 }
 
-template <int XM>
+template <int XM, int W>
 __device__ __forceinline__ void fetch_x(const WgradArgs& a, const RowBase& rb, int rr, int f0, bool in, XRaw& r) {
     r.flag = 0;
     if (!in) return;
@@ -61,8 +63,8 @@ __device__ __forceinline__ void fetch_x(const WgradArgs& a, const RowBase& rb, i
         r.a = *reinterpret_cast<const float4*>(a.x_ptr + phys_row(rb, rr, a.x_stride) * a.x_ld + f0);
         r.flag = 1;
     } else if (XM == XM_CM) {
-        if (f0 < 2 * kKhE) {
-            r.a = *reinterpret_cast<const float4*>(cm_piece(a.x_ptr, phys_row(rb, rr, a.x_stride), f0));
+        if (f0 < 2 * (W == 160 ? kKhE : kKhN)) {
+            r.a = *reinterpret_cast<const float4*>(cm_piece<W>(a.x_ptr, phys_row(rb, rr, a.x_stride), f0));
             r.flag = 1;
         }
     } else if (XM == XM_EDGE_D) {
@@ -94,15 +96,15 @@ __device__ __forceinline__ float4 finish_x(const WgradArgs& a, int f0, const XRa
     }
 }
 
-template <int YM>
+template <int YM, int W>
 __device__ __forceinline__ void fetch_y(const WgradArgs& a, const RowBase& rb, int rr, int f0, bool in, YRaw& r) {
     r.flag = 0;
     if (!in) return;
     if (YM == YM_ROW) {
         r.g = *reinterpret_cast<const float4*>(a.y_ptr + phys_row(rb, rr, a.y_stride) * a.y_ld + f0);
         r.flag = 1;
-    } else if (f0 < 2 * kKhE) {  // YM_CM
-        r.g = *reinterpret_cast<const float4*>(cm_piece(a.y_ptr, phys_row(rb, rr, a.y_stride), f0));
+    } else if (f0 < 2 * (W == 160 ? kKhE : kKhN)) {  // YM_CM
+        r.g = *reinterpret_cast<const float4*>(cm_piece<W>(a.y_ptr, phys_row(rb, rr, a.y_stride), f0));
         r.flag = 1;
     }
 }
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
             const int g = tid + k * kWgThreads;
             int rr, c4;
             group_rc<XCM, GX>(g, rr, c4);
-            fetch_x<XM>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
+            fetch_x<XM, KXP>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
         }
     };
     auto fetch_ys = [&](int64_t r0) {
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
             const int g = tid + k * kWgThreads;
             int rr, c4;
             group_rc<YCM, GY>(g, rr, c4);
-            fetch_y<YM>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
+            fetch_y<YM, NYP>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
         }
     };
     auto fetch = [&](int64_t r0) {
@@ -323,11 +325,11 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
         return hipGetLastError();                                                             \
     }
     SPW_WG(XM_CM, YM_ROW, 160, 160)
-    SPW_WG(XM_ROW, YM_ROW, 128, 160)
-    SPW_WG(XM_ROW, YM_ROW, 160, 128)
-    SPW_WG(XM_ROW, YM_ROW, 128, 128)
+    SPW_WG(XM_CM, YM_CM, 128, 160)
+    SPW_WG(XM_CM, YM_CM, 160, 128)
+    SPW_WG(XM_CM, YM_CM, 128, 128)
     SPW_WG(XM_EDGE_D, YM_CM, 32, 160)
-    SPW_WG(XM_NODE_O, YM_ROW, 32, 128)
+    SPW_WG(XM_NODE_O, YM_CM, 32, 128)
     SPW_WG(XM_CM, YM_CM, 160, 160)
 #undef SPW_WG
     return hipErrorInvalidValue;

@@ -19,10 +19,17 @@ constexpr int kDegCol = 150;      // H2s column 150 holds the in-degree (multipl
 // ---- chunk-major edge rows ("CM"): a 32-edge block of 152-wide rows stored as
 // [q < 19][h < 2][edge i < 32][4] — feature f = 76h + 4q + c. A wave's 16-byte-per-lane access in
 // either orientation (lane = edge) is 1 KiB contiguous, where row-major rows would touch 64 lines.
-constexpr int kCmBlk = 19 * 2 * 32 * 4;   // 4864 floats per block
-__host__ __device__ constexpr int cm_off(int i, int f) {
-    return (((f >= kKhE ? f - kKhE : f) >> 2) * 2 + (f >= kKhE ? 1 : 0)) * 128 + i * 4 + (f & 3);
+// Node rows use the same scheme per 32-node block: 160-wide arrays with KH = 76 (152 features),
+// 128-wide (100-feature) arrays with KH = 52 (104 features).
+template <int KH>
+__host__ __device__ constexpr int cm_offk(int i, int f) {
+    return (((f >= KH ? f - KH : f) >> 2) * 2 + (f >= KH ? 1 : 0)) * 128 + i * 4 + (f & 3);
 }
+constexpr int kCmBlk = kKhE * 64;    // 4864 floats per 32-row block of a 152-feature array
+constexpr int kCmBlkN = kKhN * 64;   // 3328 floats per 32-row block of a 104-feature array
+constexpr int kRowE = 2 * kKhE;      // floats per row of a chunk-major 152-feature array
+constexpr int kRowN = 2 * kKhN;      // floats per row of a chunk-major 104-feature array
+__host__ __device__ constexpr int cm_off(int i, int f) { return cm_offk<kKhE>(i, f); }
 
 constexpr int kNumTensors = 22;
 
