@@ -106,14 +106,25 @@ def cpu_baseline(n_objects: int, S: int, seconds: float):
                       f"{el:.1f}s, torch CPU threads={threads}"}
 
 
+# device kernel whose PMC summary (profiles/pmc_summary.json, tools/pmcsum.py) holds the HBM
+# bytes of a bench kernel
+PMC_NAMES = {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true>", "enc_edge": "k_enc_edge",
+             "enc_edge_bwd": "k_enc_edge_bwd"}
+
+
 def load_pmc(kernel: str):
+    """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) from the committed PMC
+    summary, or None when absent."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if not os.path.exists(path):
+    name = PMC_NAMES.get(kernel)
+    if name is None or not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+            d = json.load(f).get(name, {})
+        if "hbm_read_bytes" not in d or "hbm_write_bytes" not in d:
+            return None
+        return float(d["hbm_read_bytes"] + d["hbm_write_bytes"])
     except Exception:
         return None
 

@@ -125,6 +125,45 @@ __device__ __forceinline__ void group_rc(int g, int& rr, int& c4) {
     }
 }
 
+// Chunk-major operand staging: thread tid always stages row rr = tid & 31 of a 32-row block and
+// the column groups c4 = (tid >> 5) + 8k (k < W/32), so the in-block offsets are fixed per thread
+// and a block costs one row map plus W/32 16-byte loads (the 32 lanes of a column group read 512
+// contiguous bytes).
+template <int W>
+struct CmStage {
+    static constexpr int KH = W == 160 ? kKhE : kKhN, BLK = KH * 64, NG = W / 32;
+    int off[NG];     // in-block offset of group k for in-block row 0, -1 for padding columns (≥ 2·KH)
+    int ones_k, ones_c;
+    float4 raw[NG];
+    __device__ __forceinline__ void init(int tid, int ones) {
+        const int c0 = tid >> 5;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int f0 = 4 * (c0 + 8 * k);
+            off[k] = f0 < 2 * KH ? cm_offk<KH>(0, f0) : -1;
+        }
+        ones_k = (ones >= 0 && ((ones >> 2) & 7) == c0) ? (ones >> 5) : -1;
+        ones_c = ones & 3;
+    }
+    __device__ __forceinline__ void fetch(const float* __restrict__ base, int64_t phys, bool in) {
+        // the physical row's own position in its block (logical and physical 32-row blocks differ
+        // when a step's row count is not a multiple of 32)
+        const float* b = base + (phys >> 5) * BLK + (phys & 31) * 4;
+#pragma unroll
+        for (int k = 0; k < NG; ++k)
+            raw[k] = (in && off[k] >= 0) ? *reinterpret_cast<const float4*>(b + off[k]) : f4zero();
+    }
+    __device__ __forceinline__ void write(float* S, int ld, int tid) const {
+        float* row = S + (tid & 31) * ld + 4 * (tid >> 5);
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            float4 v = raw[k];
+            if (k == ones_k) f4set(v, ones_c, 1.f);   // the bias' ones column
+            *reinterpret_cast<float4*>(row + 32 * k) = v;
+        }
+    }
+};
+
 // dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n] on v_mfma_f32_16x16x4_f32.
 // The (KXP/16)×(NYP/16) output tiles split 2×2 over the 4 waves (5×5 tiles of 16×16 per wave at
 // 160×160, so every SIMD gets the same work); per k-step (4 rows) a wave reads MX + MY fragments
@@ -151,29 +190,43 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
 #pragma unroll
         for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
     // every operand is fetched a block ahead
-    XRaw xr[NGX];
-    YRaw yr[NGY];
+    constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM;
+    XRaw xr[XCM ? 1 : NGX];
+    YRaw yr[YCM ? 1 : NGY];
+    CmStage<KXP> xc;
+    CmStage<NYP> yc;
+    if (XCM) xc.init(tid, a.x_ones);
+    if (YCM) yc.init(tid, -1);
     const int64_t xcount = (XM == XM_ROW || XM == XM_CM) ? a.x_count : a.rows;
     const int64_t ycount = a.y_count;
-    constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM;
     auto fetch_xs = [&](int64_t r0) {
         const RowBase xb = row_base(r0, xcount);
+        if constexpr (XCM) {
+            const int rr = tid & 31;
+            xc.fetch(a.x_ptr, phys_row(xb, rr, a.x_stride), r0 + rr < r_end);
+        } else {
 #pragma unroll
-        for (int k = 0; k < NGX; ++k) {
-            const int g = tid + k * kWgThreads;
-            int rr, c4;
-            group_rc<XCM, GX>(g, rr, c4);
-            fetch_x<XM, KXP>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
+            for (int k = 0; k < NGX; ++k) {
+                const int g = tid + k * kWgThreads;
+                int rr, c4;
+                group_rc<false, GX>(g, rr, c4);
+                fetch_x<XM, KXP>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
+            }
         }
     };
     auto fetch_ys = [&](int64_t r0) {
         const RowBase yb = row_base(r0, ycount);
+        if constexpr (YCM) {
+            const int rr = tid & 31;
+            yc.fetch(a.y_ptr, phys_row(yb, rr, a.y_stride), r0 + rr < r_end);
+        } else {
 #pragma unroll
-        for (int k = 0; k < NGY; ++k) {
-            const int g = tid + k * kWgThreads;
-            int rr, c4;
-            group_rc<YCM, GY>(g, rr, c4);
-            fetch_y<YM, NYP>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
+            for (int k = 0; k < NGY; ++k) {
+                const int g = tid + k * kWgThreads;
+                int rr, c4;
+                group_rc<false, GY>(g, rr, c4);
+                fetch_y<YM, NYP>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
+            }
         }
     };
     auto fetch = [&](int64_t r0) {
@@ -183,22 +236,30 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     fetch(r_begin);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
+        if constexpr (XCM) {
+            xc.write(Xs, LDX, tid);
+        } else {
 #pragma unroll
-        for (int k = 0; k < NGX; ++k) {
-            const int g = tid + k * kWgThreads;
-            if (g < 32 * GX) {
-                int rr, c4;
-                group_rc<XCM, GX>(g, rr, c4);
-                *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
+            for (int k = 0; k < NGX; ++k) {
+                const int g = tid + k * kWgThreads;
+                if (g < 32 * GX) {
+                    int rr, c4;
+                    group_rc<false, GX>(g, rr, c4);
+                    *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
+                }
             }
         }
+        if constexpr (YCM) {
+            yc.write(Ys, LDY, tid);
+        } else {
 #pragma unroll
-        for (int k = 0; k < NGY; ++k) {
-            const int g = tid + k * kWgThreads;
-            if (g < 32 * GY) {
-                int rr, c4;
-                group_rc<YCM, GY>(g, rr, c4);
-                *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = finish_y(yr[k]);
+            for (int k = 0; k < NGY; ++k) {
+                const int g = tid + k * kWgThreads;
+                if (g < 32 * GY) {
+                    int rr, c4;
+                    group_rc<false, GY>(g, rr, c4);
+                    *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = finish_y(yr[k]);
+                }
             }
         }
         __syncthreads();

@@ -21,3 +21,7 @@ print("dlogit", float(np.abs(z.cpu().numpy().reshape(z_ref.shape) - z_ref).max()
 g = P.from_flat(grads)
 for k, ref in g_ref.items():
     print(f"{k:14s} rel={np.abs(g[k]-ref).max()/(np.abs(ref).max()+1e-30):.3e}")
+k = "rmp.0.kernel"
+d = np.abs(g[k] - g_ref[k]).max(axis=1)
+for lo, hi in ((0, 150), (150, 250), (250, 350)):
+    print(k, lo, hi, f"{d[lo:hi].max():.3e}", f"ref {np.abs(g_ref[k][lo:hi]).max():.3e}")
