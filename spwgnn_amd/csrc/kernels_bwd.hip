@@ -154,7 +154,7 @@ __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint
 // dA (Σ over steps of dh1pre) is written by the first backward step and accumulated by the later
 // ones with no-return float atomics (one add per element per launch, launches stream-ordered:
 // the summation order is fixed, so the result stays deterministic).
-template <bool ONEHOT>
+template <bool ONEHOT, bool ACCUM>
 __global__ __launch_bounds__(ONEHOT ? 512 : 256, ONEHOT ? 1 : 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_edge_bwd(EdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
@@ -251,17 +251,13 @@ void k_edge_bwd(EdgeBwdArgs a) {
                 acc[t][r] = ((mw >> row) & 1u) ? acc[t][r] : 0.f;
             }
         }
-        if (a.dA_accumulate) {
-#pragma unroll
-            for (int t = 0; t < 5; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) unsafeAtomicAdd(dArow + (rho(r, 0) + 4 * h) * kLdE + 32 * t, acc[t][r]);
-        } else {
-#pragma unroll
-            for (int t = 0; t < 5; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) dArow[(rho(r, 0) + 4 * h) * kLdE + 32 * t] = acc[t][r];
-        }
+        // dA: plain stores on the first backward step, no-return atomics after (ACCUM); in the
+        // one-hot path they are issued beside the segment-sum MFMAs (same basic block)
+        auto put_dA = [&](int t, int r) {
+            float* p = dArow + (rho(r, 0) + 4 * h) * kLdE + 32 * t;
+            if (ACCUM) unsafeAtomicAdd(p, acc[t][r]);
+            else *p = acc[t][r];
+        };
         if (ONEHOT) {  // segment sums on the matrix core (padding edges: src = dst = -1, no match)
             const int s = a.esrc[e];
 #pragma unroll
@@ -271,9 +267,16 @@ void k_edge_bwd(EdgeBwdArgs a) {
                 const int node = i < 16 ? (h ? d1 : d0) : (h ? s1 : s0);
                 const float oh = node == key ? 1.f : 0.f;
 #pragma unroll
-                for (int t = 0; t < 5; ++t) nacc[t] = mfma32(oh, acc[t][r], nacc[t]);
+                for (int t = 0; t < 5; ++t) {
+                    nacc[t] = mfma32(oh, acc[t][r], nacc[t]);
+                    put_dA(t, r);
+                }
             }
-        } else {  // segment sums: receiver → dV, sender → dU
+        } else {
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) put_dA(t, r);  // segment sums: receiver → dV, sender → dU
             const uint32_t csrw = reinterpret_cast<const uint32_t*>(a.csr)[(int64_t)blk * 32 + i];
 #pragma unroll
             for (int rd = 0; rd < 3; ++rd) {
@@ -379,10 +382,16 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
 }
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st) {
     if (a.nw_max <= 16) {
-        hipLaunchKernelGGL(k_edge_bwd<true>, dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
+        if (a.dA_accumulate)
+            hipLaunchKernelGGL((k_edge_bwd<true, true>), dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
+        else
+            hipLaunchKernelGGL((k_edge_bwd<true, false>), dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
     } else {
         const size_t lds = edge_bwd_lds_per_wave(a.nw_max) * a.wpg;
-        hipLaunchKernelGGL(k_edge_bwd<false>, dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+        if (a.dA_accumulate)
+            hipLaunchKernelGGL((k_edge_bwd<false, true>), dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+        else
+            hipLaunchKernelGGL((k_edge_bwd<false, false>), dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
     }
     return hipGetLastError();
 }
