@@ -166,9 +166,26 @@ void k_edge_bwd(EdgeBwdArgs a) {
     if (ONEHOT) wl_fill(wl, a.w2t);
     const float* wrow = ONEHOT ? wl + i * kWlK + kKhE * h : a.w2t + (kKhE * h) * kLdE + i;
     const int wstep = ONEHOT ? gridDim.x * kEdgeWaves : a.n_wtiles;
-    for (int wt = ONEHOT ? blockIdx.x * kEdgeWaves + wave : blockIdx.x * a.wpg + wave; wt < a.n_wtiles; wt += wstep) {
-    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
+    // per-block indices and h2>0 words run one block ahead (across wave-tiles too): the G3
+    // gathers of a block depend on them
+    struct Pre { int d, s; uint32_t w[5]; };
+    auto load_pre = [&](int blk) {
+        Pre p;
+        const int64_t e = (int64_t)blk * 32 + i;
+        p.d = a.edst[e];
+        p.s = a.esrc[e];
+        const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) p.w[t] = m2[32 * t];
+        return p;
+    };
+    int wt = ONEHOT ? blockIdx.x * kEdgeWaves + wave : blockIdx.x * a.wpg + wave;
+    int4 info = wtiles[min(wt, a.n_wtiles - 1)];
+    Pre pre = load_pre(info.x);
+    for (; wt < a.n_wtiles; wt += wstep) {
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];   // next wave-tile (clamped)
     float* st = smem + wave * (2112 + 2 * a.nw_max * kLdE);
     float* naccR = st + 2112;
     float* naccS = naccR + a.nw_max * kLdE;
@@ -185,14 +202,20 @@ void k_edge_bwd(EdgeBwdArgs a) {
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
         const int64_t e = (int64_t)blk * 32 + i;
-        const int d = a.edst[e];
+        const Pre cur = pre;
+        pre = load_pre(bb + 1 < nb ? blk + 1 : ninfo.x);   // unconditional (clamped at the end)
+        const int d = cur.d;
         const bool valid = d >= 0;
         const int dc = valid ? d : n0;
+        // dh1 mask words (used after the GEMM: the load has the whole GEMM to land)
+        const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
+        uint32_t m1w[5];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) m1w[t] = m1[32 * t];
         // dh2pre (A operand, lane = edge, split halves): G3[receiver] ⊙ [h2 > 0]
-        const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
         uint32_t w[5];
 #pragma unroll
-        for (int t = 0; t < 5; ++t) w[t] = valid ? m2[32 * t] : 0u;
+        for (int t = 0; t < 5; ++t) w[t] = valid ? cur.w[t] : 0u;
         // this lane's 76 feature bits (features 76h + 0..75) as a 64-bit low part and 12-bit tail
         const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
                                     : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
@@ -240,11 +263,10 @@ void k_edge_bwd(EdgeBwdArgs a) {
         }
         chunk(18, g0, g1);
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
-        const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
         float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-            const uint32_t mw = m1[32 * t];
+            const uint32_t mw = m1w[t];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = rho(r, 0) + 4 * h;
@@ -259,7 +281,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
             else *p = acc[t][r];
         };
         if (ONEHOT) {  // segment sums on the matrix core (padding edges: src = dst = -1, no match)
-            const int s = a.esrc[e];
+            const int s = cur.s;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int d0 = __builtin_amdgcn_readlane(d, rho(r, 0)), d1 = __builtin_amdgcn_readlane(d, rho(r, 1));
@@ -317,6 +339,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
             }
         }
     }
+    info = ninfo;
     }
 }
 

@@ -269,16 +269,26 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const float* wrow = wl + i * kWlK + kKhE * h;
-    for (int wt = blockIdx.x * kEdgeWaves + wave; wt < a.n_wtiles; wt += gridDim.x * kEdgeWaves) {
-    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
+    const int wstep = gridDim.x * kEdgeWaves;
+    // the per-block edge indices run one block ahead (across wave-tiles too): the U/V gathers of
+    // a block depend on them
+    auto load_sd = [&](int blk) { return make_int2(a.esrc[(int64_t)blk * 32 + i], a.edst[(int64_t)blk * 32 + i]); };
+    int wt = blockIdx.x * kEdgeWaves + wave;
+    int4 info = wtiles[min(wt, a.n_wtiles - 1)];
+    int2 pre = load_sd(info.x);
+    for (; wt < a.n_wtiles; wt += wstep) {
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];   // next wave-tile (clamped)
     NodeSum<NW16> nsum;
     nsum.init(n0, lane);
 
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
         const int64_t e = (int64_t)blk * 32 + i;
-        const int s = a.esrc[e], d = a.edst[e];
+        const int2 cur = pre;
+        pre = load_sd(bb + 1 < nb ? blk + 1 : ninfo.x);   // unconditional (clamped at the end)
+        const int s = cur.x, d = cur.y;
         const bool valid = s >= 0;
         const int sc = valid ? s : n0, dc = valid ? d : n0;
         // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:174-177), lane = edge, split
@@ -376,6 +386,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
     // the wave-tile's node rows (each node is owned by exactly one wave-tile)
     nsum.store(a.H2s, n0, nn, lane);
+    info = ninfo;
     }
 }
 
