@@ -98,13 +98,15 @@ __device__ __forceinline__ int64_t cm_index(int64_t row, int f) {
 
 // ---- per-lane activation-sign bits of NT C-layout tiles (bit 16t + r of the lane's words), so a
 // backward pass in the same orientation reads 3 words per lane instead of the activations.
+// X must be ≥ +0 (post-relu): then X > 0 ⟺ its bit pattern is non-zero, min(bits, 1) is the bit.
 template <int NT>
 __device__ __forceinline__ void store_pos_bits(uint32_t* __restrict__ words, const f32x16 (&X)[NT], int lane) {
     uint32_t w[(NT * 16 + 31) / 32] = {};
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) w[(16 * t + r) >> 5] |= (X[t][r] > 0.f ? 1u : 0u) << ((16 * t + r) & 31);
+        for (int r = 0; r < 16; ++r)
+            w[(16 * t + r) >> 5] |= min(__float_as_uint(X[t][r]), 1u) << ((16 * t + r) & 31);
 #pragma unroll
     for (int k = 0; k < (NT * 16 + 31) / 32; ++k) words[64 * k + lane] = w[k];
 }

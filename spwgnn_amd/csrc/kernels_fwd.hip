@@ -127,25 +127,24 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const int f = rho(r, 0) + 4 * h + 32 * t;
             X[t][r] = relu(dx * a.w_rm0[f] + dy * a.w_rm0[160 + f] + a.b_rm0[f]);
         }
-    float* zrow = nullptr;
     float* const zb = a.z1 ? a.z1 + (int64_t)blk * kCmBlk : nullptr;   // chunk-major blocks
     uint32_t* const mb = a.zmask ? a.zmask + (int64_t)blk * 4 * 3 * 64 : nullptr;
     if (zb) {
-        store_cm<5>(zb, X, lane, valid);
+        store_cm<5>(zb, X, lane, true);   // padding-edge rows: finite, met only by zero gradients
         store_pos_bits<5>(mb, X, lane);
     }
     zero_tiles(Y);
     tchain_acc<5, 5, 12, kLdE>(X, Y, a.w_rm1, lane);
     bias_act_rho<5, true>(Y, a.b_rm1, h);
     if (zb) {
-        store_cm<5>(a.z2 + (int64_t)blk * kCmBlk, Y, lane, valid);
+        store_cm<5>(a.z2 + (int64_t)blk * kCmBlk, Y, lane, true);
         store_pos_bits<5>(mb + 3 * 64, Y, lane);
     }
     zero_tiles(X);
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_rm2, lane);
     bias_act_rho<5, true>(X, a.b_rm2, h);
     if (zb) {
-        store_cm<5>(a.z3 + (int64_t)blk * kCmBlk, X, lane, valid);
+        store_cm<5>(a.z3 + (int64_t)blk * kCmBlk, X, lane, true);
         store_pos_bits<5>(mb + 6 * 64, X, lane);
     }
     zero_tiles(Y);
@@ -163,14 +162,13 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
     }
     if (zb) {
-        store_cm<5>(a.cr + (int64_t)blk * kCmBlk, Y, lane, valid);
+        store_cm<5>(a.cr + (int64_t)blk * kCmBlk, Y, lane, true);
         store_pos_bits<5>(mb + 9 * 64, Y, lane);
     }
     zero_tiles(X);
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_w1a, lane);
     bias_act_rho<5, false>(X, a.b_w1a, h);
-    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, valid);   // chunk-major (k_edge_fwd streams it)
-    (void)zrow;
+    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, true);   // chunk-major; k_edge_fwd masks padding edges
 }
 
 // ------------------------------------------------------------------------------------------------
