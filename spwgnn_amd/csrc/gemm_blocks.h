@@ -60,6 +60,16 @@ __device__ __forceinline__ void store_cm(float* __restrict__ blk, const f32x16 (
             }
         }
 }
+// one 16-byte piece p = 4t + q of store_cm (pieces with f0 ≥ 2·KH do not exist: NT = 5 has 19,
+// NT = 4 has 13 — exactly the group count of a chain whose input is X)
+template <int NT>
+__device__ __forceinline__ void store_cm_piece(float* __restrict__ blk, const f32x16 (&X)[NT], int lane, int p) {
+    constexpr int KH = NT == 5 ? kKhE : kKhN;
+    const int j = lane & 31, h = lane >> 5, t = p >> 2, q = p & 3;
+    if (32 * t + 8 * q + 4 < 2 * KH)
+        *reinterpret_cast<float4*>(blk + cm_offk<KH>(j, 32 * t + 8 * q + 4 * h)) =
+            make_float4(X[t][4 * q], X[t][4 * q + 1], X[t][4 * q + 2], X[t][4 * q + 3]);
+}
 template <int NT>
 __device__ __forceinline__ void load_cm(const float* __restrict__ blk, f32x16 (&X)[NT], int lane) {
     constexpr int KH = NT == 5 ? kKhE : kKhN;
@@ -145,9 +155,14 @@ __device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh
 // tools/mb/chain.hip.) The next group's fragments load while this group's MFMAs issue.
 // in: C layout of the previous layer; k-steps (tp, r) for tp < NT_IN, r < LAST_R in the last
 // input tile (LAST_R % 4 == 0; rows beyond are zero padding).
-template <int NT_OUT, int NT_IN, int LAST_R, int N>
+// `side(gi)` runs after group gi's MFMAs: independent work (e.g. the previous layer's stores,
+// store_cm_piece) issued beside the matrix pipe instead of before the chain.
+struct NoSide {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <int NT_OUT, int NT_IN, int LAST_R, int N, class Side = NoSide>
 __device__ __forceinline__ void tchain_acc(const f32x16 (&in)[NT_IN], f32x16 (&out)[NT_OUT],
-                                           const float* __restrict__ W4, int lane) {
+                                           const float* __restrict__ W4, int lane, Side side = Side()) {
     static_assert(LAST_R % 4 == 0, "16-byte fragments");
     const float* wb = W4 + ((lane >> 5) * N + (lane & 31)) * 4;   // k-block h, column i
     constexpr int NG = (NT_IN - 1) * 4 + LAST_R / 4;   // groups of 4 k-steps: k-block 2gi + h
@@ -169,6 +184,7 @@ __device__ __forceinline__ void tchain_acc(const f32x16 (&in)[NT_IN], f32x16 (&o
             out[t] = mfma32(cur[t].z, in[tp][r0 + 2], out[t]);
             out[t] = mfma32(cur[t].w, in[tp][r0 + 3], out[t]);
         }
+        side(gi);
         if (gi + 1 < NG) {
 #pragma unroll
             for (int t = 0; t < NT_OUT; ++t) cur[t] = nxt[t];

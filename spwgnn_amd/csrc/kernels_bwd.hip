@@ -356,17 +356,15 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     zero_tiles(D);
     tgemm_stream_acc<5, kKhE, kLdE>(a.dA + e * kLdE + kKhE * h, D, a.w1at, lane);  // dc_r = dA·W1aᵀ
     apply_pos_bits<5>(mb + 9 * 64, D, lane, a.scale);   // relu + dropout of c_r
-    store_cm<5>(db, D, lane, true);
+    // each gradient is stored piecewise beside the next layer's MFMAs
     zero_tiles(E);
-    tchain_acc<5, 5, 12, kLdE>(D, E, a.rm3t, lane);
+    tchain_acc<5, 5, 12, kLdE>(D, E, a.rm3t, lane, [&](int p) { store_cm_piece<5>(db, D, lane, p); });
     apply_pos_bits<5>(mb + 6 * 64, E, lane, 1.f);
-    store_cm<5>(a.dz3 + cmo, E, lane, true);
     zero_tiles(D);
-    tchain_acc<5, 5, 12, kLdE>(E, D, a.rm2t, lane);
+    tchain_acc<5, 5, 12, kLdE>(E, D, a.rm2t, lane, [&](int p) { store_cm_piece<5>(a.dz3 + cmo, E, lane, p); });
     apply_pos_bits<5>(mb + 3 * 64, D, lane, 1.f);
-    store_cm<5>(a.dz2 + cmo, D, lane, true);
     zero_tiles(E);
-    tchain_acc<5, 5, 12, kLdE>(D, E, a.rm1t, lane);
+    tchain_acc<5, 5, 12, kLdE>(D, E, a.rm1t, lane, [&](int p) { store_cm_piece<5>(a.dz2 + cmo, D, lane, p); });
     apply_pos_bits<5>(mb, E, lane, 1.f);
     store_cm<5>(a.dz1 + cmo, E, lane, true);
     (void)h;

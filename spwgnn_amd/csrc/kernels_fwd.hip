@@ -105,6 +105,9 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // rm encoder (transposed orientation, one 32-edge block per wave): d = pos[r]-pos[s] (2 feats)
 // → 150 → 150 → 150 → 150 (+relu, dropout) = c_r; A = c_r·W1a + b1 (step-invariant first-layer
 // term of rmp: W1·[c_r|P_s|P_r] = (c_r·W1a + b1) + P_s·W1b + P_r·W1c).
+// TRAIN: the activations/sign bits for the backward are stored (a compile-time switch: a branch
+// inside the chains would split the MFMA blocks the stores are scheduled into)
+template <bool TRAIN>
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_edge(EncEdgeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -127,24 +130,26 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const int f = rho(r, 0) + 4 * h + 32 * t;
             X[t][r] = relu(dx * a.w_rm0[f] + dy * a.w_rm0[160 + f] + a.b_rm0[f]);
         }
-    float* const zb = a.z1 ? a.z1 + (int64_t)blk * kCmBlk : nullptr;   // chunk-major blocks
-    uint32_t* const mb = a.zmask ? a.zmask + (int64_t)blk * 4 * 3 * 64 : nullptr;
+    constexpr bool zb = TRAIN;
+    uint32_t* const mb = TRAIN ? a.zmask + (int64_t)blk * 4 * 3 * 64 : nullptr;
+    // saved activations (padding-edge rows unmasked: finite, and met only by zero gradients)
+    const int64_t cmo = (int64_t)blk * kCmBlk;
     if (zb) {
-        store_cm<5>(zb, X, lane, true);   // padding-edge rows: finite, met only by zero gradients
+        store_cm<5>(a.z1 + cmo, X, lane, true);
         store_pos_bits<5>(mb, X, lane);
     }
     zero_tiles(Y);
     tchain_acc<5, 5, 12, kLdE>(X, Y, a.w_rm1, lane);
     bias_act_rho<5, true>(Y, a.b_rm1, h);
     if (zb) {
-        store_cm<5>(a.z2 + (int64_t)blk * kCmBlk, Y, lane, true);
+        store_cm<5>(a.z2 + cmo, Y, lane, true);
         store_pos_bits<5>(mb + 3 * 64, Y, lane);
     }
     zero_tiles(X);
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_rm2, lane);
     bias_act_rho<5, true>(X, a.b_rm2, h);
     if (zb) {
-        store_cm<5>(a.z3 + (int64_t)blk * kCmBlk, X, lane, true);
+        store_cm<5>(a.z3 + cmo, X, lane, true);
         store_pos_bits<5>(mb + 6 * 64, X, lane);
     }
     zero_tiles(Y);
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
     }
     if (zb) {
-        store_cm<5>(a.cr + (int64_t)blk * kCmBlk, Y, lane, true);
+        store_cm<5>(a.cr + cmo, Y, lane, true);
         store_pos_bits<5>(mb + 9 * 64, Y, lane);
     }
     zero_tiles(X);
@@ -486,7 +491,10 @@ hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_enc_edge, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
+    if (a.z1)
+        hipLaunchKernelGGL(k_enc_edge<true>, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_enc_edge<false>, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st) {
