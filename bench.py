@@ -108,7 +108,7 @@ def cpu_baseline(n_objects: int, S: int, seconds: float):
 
 # device kernel whose PMC summary (profiles/pmc_summary.json, tools/pmcsum.py) holds the HBM
 # bytes of a bench kernel
-PMC_NAMES = {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true>", "enc_edge": "k_enc_edge",
+PMC_NAMES = {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true, true>", "enc_edge": "k_enc_edge<true>",
              "enc_edge_bwd": "k_enc_edge_bwd"}
 
 
