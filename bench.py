@@ -75,11 +75,20 @@ class HipEvents:
             self.hip.hipEventDestroy(C.c_void_p(e))
 
 
-def cpu_baseline(n_objects: int, S: int, seconds: float):
+def cpu_baseline_pair(n_objects: int, S: int, seconds: float):
+    """The oracle at up to 16 host threads (the reported baseline) and at 1 thread."""
+    many = cpu_baseline(n_objects, S, seconds)
+    one = cpu_baseline(n_objects, S, max(3.0, seconds / 3), threads=1)
+    many["value_1thread"] = one["value"]
+    many["sample"] += f"; 1 thread: {one['value']:.1f} towers/s ({one['sample'].split(', ')[2]})"
+    return many
+
+
+def cpu_baseline(n_objects: int, S: int, seconds: float, threads=None):
     """The oracle (torch-CPU restatement of Networks.py, literal dense one-hot form, fp32 like
     Keras floatx) timed fwd+bwd on a bounded sample on this host's cores."""
     from oracle import model as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = max(1, min(16, len(os.sched_getaffinity(0)))) if threads is None else threads
     torch.set_num_threads(threads)
     B = 256
     obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, n_objects, seed=123, fully_connected=True)
@@ -129,6 +138,29 @@ def load_pmc(kernel: str):
         return None
 
 
+def step_hbm(ms_per_step: float):
+    """Whole-step HBM bytes from the committed PMC summary (one entry per kernel: mean bytes per
+    dispatch × dispatches; the summary's run covers as many steps as k_adam dispatches)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        steps = d.get("k_adam", {}).get("dispatches", 0)
+        if not steps:
+            return None
+        tot = sum(v.get("hbm_read_bytes", 0.0) * v["dispatches"] + v.get("hbm_write_bytes", 0.0) * v["dispatches"]
+                  for v in d.values() if "dispatches" in v)
+        per = tot / steps
+        gbs = per / (ms_per_step * 1e-3) / 1e9
+        return {"bytes_per_step": round(per), "achieved_gbs": round(gbs, 1), "peak_gbs": PEAK_HBM_GBS,
+                "frac": round(gbs / PEAK_HBM_GBS, 4),
+                "source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per kernel)"}
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,6 +173,9 @@ def main():
     ap.add_argument("--roofline-kernel", default="edge_bwd", choices=sorted(KERNELS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--infer", action="store_true",
+                    help="BASELINE config 5: forward-only inference replayed from a hipGraph "
+                         "(defaults: 32-block towers, S=10, 8192 towers/GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -151,6 +186,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
 
+    if args.infer:
+        return run_infer(args, world, rank, device)
     B, N, S = args.towers, args.nodes, args.mp_steps
     raw = D.synthetic_towers(B, N, seed=1000 + rank)
     objects = (raw / D.RELATION_THRESHOLD).astype(np.float32)
@@ -225,8 +262,86 @@ def main():
                      "traffic": load_pmc(args.roofline_kernel)},
         "cpu_baseline": None,
     }
+    out["hbm"] = step_hbm(out["ms_per_step"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(N, S, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline_pair(N, S, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+INFER_METRIC = "towers/sec fwd (inference), 32-block towers, 10 MP steps, hipGraph-captured forward"
+
+
+def run_infer(args, world, rank, device):
+    """Config 5: the forward of a whole batch captured once into a hipGraph (torch.cuda.CUDAGraph
+    over the library's launches on the capture stream) and replayed; weak scaling, replicas."""
+    from spwgnn_amd import engine as E
+    B = args.towers if args.towers != 65536 else 8192
+    N = args.nodes if args.nodes != 6 else 32
+    S = args.mp_steps if args.mp_steps != 5 else 10
+    raw = D.synthetic_towers(B, N, seed=5000 + rank)
+    batch = TowerBatch.fully_connected((raw / D.RELATION_THRESHOLD).astype(np.float32), device=device)
+    params = P.to_flat(P.glorot_uniform(0), device=device)
+    run = E.RunConfig(S, training=False)
+    ws = E.Workspace(device)
+    z = torch.empty(batch.n_nodes, dtype=torch.float32, device=device)
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        E.forward(params, batch, run, ws, logits=z)      # sizes the workspace before capture
+    torch.cuda.current_stream(device).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        E.forward(params, batch, run, ws, logits=z)
+    for _ in range(args.warmup):
+        graph.replay()
+    torch.cuda.synchronize()
+    # dominant kernel timed with HIP events on an un-captured pass (same stream, same launches)
+    kid, flops_fn = _lib.K_EDGE_FWD, KERNELS["edge_fwd"][1]
+    ev = HipEvents(2 * S)
+    prun = E.RunConfig(S, training=False, prof_kernel=kid, prof_events=ev.ev)
+    E.forward(params, batch, prun, ws, logits=z)
+    torch.cuda.synchronize()
+    kern_ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(S)]
+    ev.close()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    Ne, Nn = batch.n_edges, batch.n_nodes
+    avg_ms = float(np.mean(kern_ms))
+    kflops = flops_fn(Ne, Nn, S)
+    achieved = kflops / (avg_ms * 1e-3) / 1e12
+    # forward FLOPs as the kernels compute them (rmp layer 3 behind the receiver sum; DESIGN.md §7)
+    fwd_flops = 2.0 * (Ne * (2 * 150 + 4 * 150 * 150) + Nn * (2 * 100 + 100 * 100)
+                       + S * (Ne * 150 * 150 + Nn * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150))
+                       - Nn * 2 * 100 * 150)
+    out = {
+        "metric": INFER_METRIC, "value": round(world * B * args.steps / el, 1), "unit": "towers/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (Jenga-geometry towers, glorot weights)",
+        "config": {"workload": f"forward, {N}-block towers fully connected (E={N * (N - 1)}), {B} towers/GPU, "
+                               f"{S} MP steps, hipGraph replay", "towers_per_gpu": B, "global_batch": B * world,
+                   "nodes_per_tower": N, "mp_steps": S, "parallelism": f"replicas{world}"},
+        "step_tflops": round(fwd_flops * world * args.steps / el / 1e12, 2),
+        "roofline": {"kernel": "edge_fwd", "bound": "mfma", "achieved": round(achieved, 2),
+                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                     "avg_launch_ms": round(avg_ms, 4), "launches": S, "flop_per_launch": kflops, "traffic": None},
+        "cpu_baseline": None,
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -58,6 +58,9 @@ def jenga_tower(n: int, rng: random.Random) -> np.ndarray:
             left_edge += rng.randint(0, MAX_SPACE_RECTS)
             w = rng.randint(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE)
             left_edge += w
+        if not boxes[layer]:   # a first box wider than the narrow layer below: centre one box on it
+            boxes[layer].append(((left_edge - w + right_edge) / 2, y, float(w)))
+            n -= 1
     return np.array([b for layer_boxes in boxes for b in layer_boxes], dtype=np.float64)
 
 

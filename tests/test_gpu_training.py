@@ -208,3 +208,36 @@ def test_graph_network_module_autograd():
     got = P.from_flat(net.flat.grad)
     for k in g:
         assert np.abs(got[k] - g[k]).max() <= 1e-5 * np.abs(g[k]).max() + 1e-7, k
+
+
+def test_forward_hipgraph_capture_replays_identically():
+    """BASELINE config 5's path: the inference forward captured into a hipGraph (all launches on
+    the capture stream, no host sync inside the library) replays bit-identically to eager."""
+    params = O.random_params(21)
+    raw = D.synthetic_towers(3, 32, seed=4)
+    batch = TowerBatch.fully_connected((raw / D.RELATION_THRESHOLD).astype(np.float32), device="cuda")
+    flat = P.to_flat(params, device="cuda")
+    run = E.RunConfig(10)
+    ws = E.Workspace("cuda")
+    eager = E.forward(flat, batch, run, ws).clone()
+    z = torch.empty_like(eager)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        E.forward(flat, batch, run, ws, logits=z)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        E.forward(flat, batch, run, ws, logits=z)
+    z.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(z, eager)
+    # and the 32-block, 10-step forward matches the oracle (config 5's shape)
+    tp = O.to_torch(params)
+    obj = (raw / D.RELATION_THRESHOLD).astype(np.float32)
+    Rs, Rr = O.relation_matrices(raw, None)   # fully connected
+    ref = O.forward_dense(tp, torch.tensor(obj, dtype=torch.float64), torch.tensor(Rs, dtype=torch.float64),
+                          torch.tensor(Rr, dtype=torch.float64), torch.zeros(3, 32, 100, dtype=torch.float64), 10).numpy()
+    got = z.cpu().numpy().reshape(ref.shape)
+    assert np.all(np.abs(got - ref) <= 1e-5 + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
