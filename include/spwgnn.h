@@ -156,6 +156,22 @@ int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64
 /* Sigmoid readout (Networks.py:183-186) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream);
 
+/* Per-tower readout over contiguous node ranges [tower_offsets[t], tower_offsets[t+1]):
+ *   SUM_PROB   out[t] = Σ sigmoid(z)  — the stability sum of JengaBuilder.remove_to_demolish /
+ *              TowerCreator.drop_to_demolish (JengaBuilder.py:252-256, TowerCreator.py:298-301),
+ *              evaluated for a whole batch of candidate towers in one call;
+ *   MEAN_PROB  the optional GlobalBlock-style mean pool (not in the reference);
+ *   SUM_LOGIT / MEAN_LOGIT on the logits.
+ * Summed sequentially in node order (deterministic). tower_offsets: n_towers + 1 int32, device. */
+enum {
+    SPWGNN_READOUT_SUM_PROB = 0,
+    SPWGNN_READOUT_MEAN_PROB = 1,
+    SPWGNN_READOUT_SUM_LOGIT = 2,
+    SPWGNN_READOUT_MEAN_LOGIT = 3
+};
+int32_t spwgnn_tower_readout(const float* logits, const int32_t* tower_offsets, int32_t n_towers, int32_t mode,
+                             float* out, spwgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

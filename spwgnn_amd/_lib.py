@@ -42,6 +42,7 @@ class RunC(C.Structure):
 
 
 K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WGRAD_W2 = 1, 2, 3, 4, 5, 6, 7
+READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 
 
 def _declare(lib: C.CDLL) -> None:
@@ -63,6 +64,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_bce": (i32, [vp, vp, i64, vp, vp, vp, vp]),
         "spwgnn_adam": (i32, [vp, vp, vp, vp, i64, i32, f32, f32, f32, f32, f32, f32, vp]),
         "spwgnn_sigmoid": (i32, [vp, vp, i64, vp]),
+        "spwgnn_tower_readout": (i32, [vp, vp, i32, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

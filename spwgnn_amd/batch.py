@@ -61,6 +61,16 @@ class TowerBatch:
     def n_edges(self) -> int:
         return int(len(self.src))
 
+    @property
+    def tower_offsets(self) -> torch.Tensor:
+        """(T+1,) int32 device node offsets of the towers (built on first use)."""
+        t = getattr(self, "_tower_offsets", None)
+        if t is None:
+            off = np.concatenate([[0], np.cumsum(self.tower_nodes)]).astype(np.int32)
+            t = torch.from_numpy(off).to(self.device)
+            object.__setattr__(self, "_tower_offsets", t)
+        return t
+
     # ------------------------------------------------------------------ constructors
     @staticmethod
     def from_edges(pos: np.ndarray, tower_nodes, src, dst, tower_edges, prop=None, device="cuda",

@@ -681,4 +681,13 @@ int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stre
     return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
 }
 
+int32_t spwgnn_tower_readout(const float* logits, const int32_t* tower_offsets, int32_t n_towers, int32_t mode,
+                             float* out, spwgnn_stream_t stream) {
+    if (!logits || !tower_offsets || !out || n_towers < 1 || mode < SPWGNN_READOUT_SUM_PROB ||
+        mode > SPWGNN_READOUT_MEAN_LOGIT)
+        return SPWGNN_E_ARG;
+    hipError_t e = launch_tower_readout(logits, tower_offsets, n_towers, mode, out, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
 }  // extern "C"

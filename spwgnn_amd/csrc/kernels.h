@@ -173,6 +173,7 @@ hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, 
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);
+hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers, int mode, float* out, hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
 // persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)

@@ -377,6 +377,17 @@ __global__ void k_sigmoid(const float* z, float* p, int64_t n) {
         p[i] = 1.f / (1.f + expf(-z[i]));
 }
 
+// per-tower readout (one thread per tower, node order): modes as SPWGNN_READOUT_*
+__global__ void k_tower_readout(const float* __restrict__ z, const int32_t* __restrict__ off, int n_towers, int mode,
+                                float* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_towers) return;
+    const int b = off[t], e = off[t + 1];
+    float s = 0.f;
+    for (int n = b; n < e; ++n) s += (mode <= 1) ? 1.f / (1.f + expf(-z[n])) : z[n];
+    out[t] = ((mode & 1) && e > b) ? s / (float)(e - b) : s;
+}
+
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
     const dim3 g(chunks), b(kWgThreads);
@@ -416,6 +427,10 @@ hipError_t launch_bce(const BceArgs& a, hipStream_t st) {
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
     const int64_t blocks = std::min<int64_t>((a.n + 255) / 256, 2048);
     hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers, int mode, float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_tower_readout, dim3((n_towers + 255) / 256), dim3(256), 0, st, z, off, n_towers, mode, out);
     return hipGetLastError();
 }
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st) {

@@ -139,3 +139,24 @@ def sigmoid(logits: torch.Tensor) -> torch.Tensor:
     st = _lib.lib().spwgnn_sigmoid(logits.data_ptr(), out.data_ptr(), logits.numel(), _stream(logits.device))
     _lib.check(st, "spwgnn_sigmoid")
     return out
+
+
+READOUT_MODES = {"sum_prob": _lib.READOUT_SUM_PROB, "mean_prob": _lib.READOUT_MEAN_PROB,
+                 "sum_logit": _lib.READOUT_SUM_LOGIT, "mean_logit": _lib.READOUT_MEAN_LOGIT}
+
+
+def tower_readout(logits: torch.Tensor, batch: TowerBatch, mode: str = "sum_prob") -> torch.Tensor:
+    """(T,) per-tower reduction of the node logits on device: "sum_prob" is the Σŷ stability score of
+    JengaBuilder.remove_to_demolish (JengaBuilder.py:252-256); "mean_prob" the optional GlobalBlock
+    mean pool (not in the reference)."""
+    if mode not in READOUT_MODES:
+        raise ValueError(f"readout mode must be one of {sorted(READOUT_MODES)}")
+    _require_gpu(logits, "logits")
+    logits = logits.reshape(-1).contiguous().to(torch.float32)
+    if logits.numel() != batch.n_nodes:
+        raise ValueError("logits must hold one value per node of the batch")
+    out = torch.empty(batch.n_towers, dtype=torch.float32, device=logits.device)
+    st = _lib.lib().spwgnn_tower_readout(logits.data_ptr(), batch.tower_offsets.data_ptr(), batch.n_towers,
+                                         READOUT_MODES[mode], out.data_ptr(), _stream(logits.device))
+    _lib.check(st, "spwgnn_tower_readout")
+    return out

@@ -97,3 +97,13 @@ class GraphNetwork(nn.Module):
     def forward(self, objects, sender_relations, receiver_relations, propagation=None) -> torch.Tensor:
         """(B, N, 1) probabilities: sigmoid(x[:, :, :1]) of the last step (Networks.py:183-186)."""
         return torch.sigmoid(self.forward_logits(objects, sender_relations, receiver_relations, propagation))[..., None]
+
+    def forward_pooled(self, objects, sender_relations, receiver_relations, propagation=None,
+                       mode: str = "mean_prob") -> torch.Tensor:
+        """(B,) per-tower pooled output — the optional GlobalBlock-style readout (not in the
+        reference): "mean_prob" / "sum_prob" (Σŷ of JengaBuilder.py:252-256) /
+        "mean_logit" / "sum_logit", reduced on device. Inference only (no autograd)."""
+        batch = TowerBatch.from_dense(objects, sender_relations, receiver_relations, propagation, device=self.device)
+        with torch.no_grad():
+            z = E.forward(self.flat.detach(), batch, E.RunConfig(self.mp_steps, training=False), E.Workspace(self.device))
+            return E.tower_readout(z, batch, mode)

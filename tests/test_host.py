@@ -166,3 +166,12 @@ def test_training_arrays_layout():
     assert x["objects"].shape == (3, 5, 3) and x["sender_relations"].shape == (3, 5, 20)
     assert np.all(y["target"] == 1.0)                 # static trajectories are stable
     assert np.allclose(x["objects"] * 170, boxes[:, 0])
+
+
+def test_removal_candidates_order():
+    from spwgnn_amd.demolish import removal_candidates
+    boxes = np.arange(15, dtype=np.float64).reshape(5, 3)
+    c = removal_candidates(boxes)
+    assert c.shape == (5, 4, 3)
+    for i in range(5):
+        assert np.array_equal(c[i], np.delete(boxes, i, axis=0))   # JengaBuilder.py:244-249 order
