@@ -104,8 +104,6 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.dz3 = take(eCM);
         w.dz2 = take(eCM);
         w.dz1 = take(eCM);
-        w.H1 = take(eCM * S);
-        w.DH2 = take(eCM * S);
         w.slab_floats = (int64_t)(kMaxChunks + kReduceGroups) * 160 * 160;
         w.slab = take(w.slab_floats);
     } else {
@@ -315,7 +313,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.b2 = c.pk(PB_W2);
         ef.H2s = c.f(w.H2s_at(s));
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
-        ef.h1_out = r->training ? c.f(w.H1_at(s)) : nullptr;
+        ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
         SPW_CHECK(launch_edge_fwd(ef, st));
@@ -360,6 +358,7 @@ struct WgSpec {
     int kx_pad = 0, ny_pad = 0;
     // reduce target
     int tk = -1, tb = -1, k_rows = 0, k_row0 = 0, bias_row = -1, perm = 0;
+    bool recompute = false;   // XM_H1 / YM_DH2 context below
 };
 
 static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, hipStream_t st,
@@ -392,6 +391,15 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     a.esrc = b->edge_src;
     a.edst = b->edge_dst;
     a.slab = c.f(w.slab);
+    if (g.recompute) {
+        a.A = c.f(w.A);
+        a.U = c.f(w.U);
+        a.V = c.f(w.V);
+        a.G3 = c.f(w.G3);
+        a.mask2 = c.u(w.mask2);
+        a.RE = w.RE;
+        a.RN = w.RN;
+    }
     if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
     SPW_CHECK(launch_wgrad(a, (int)chunks, st));
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
@@ -465,7 +473,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.csr = reinterpret_cast<const uint32_t*>(b->blk_csr);
         eb.mask1 = c.u(w.m1_at(s));
         eb.mask2 = c.u(w.m2_at(s));
-        eb.dh2_out = c.f(w.DH2_at(s));
+        eb.dh2_out = nullptr;  // the W2 gradient recomputes dh2pre (YM_DH2)
         eb.G3 = c.f(w.G3_at(s));
         eb.w2t = c.pk(PK_W2T);
         eb.dA = c.f(w.dA);
@@ -537,10 +545,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
     { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
     { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre — chunk-major rows kept by the edge kernels
-        WgSpec g; edge_row(g, w.H1, w.DH2, T_RMP1K, T_RMP1B);
-        g.xmode = XM_CM; g.ymode = YM_CM;
+    {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
+        // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
+        WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
+        g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
+        g.recompute = true;
         if ((e = run_wgrad(c, b, g, grads, st, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,

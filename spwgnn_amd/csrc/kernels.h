@@ -109,10 +109,12 @@ enum XMode : int {
     XM_EDGE_D,      // (pos[dst] - pos[src])[f] for f < 2, f == 2 → 1; padding edge → 0
     XM_NODE_O,      // pos[n][1 + f] for f < 2, f == 2 → 1
     XM_CM,          // chunk-major edge blocks (kCmBlk per 32 rows, f < 152); f == ones_col → 1
+    XM_H1,          // relu(A[e] + U_s[src] + V_s[dst]) recomputed (row = s·RE + e), f == ones_col → 1
 };
 enum YMode : int {
     YM_ROW = 0,
     YM_CM,          // chunk-major edge blocks
+    YM_DH2,         // G3_s[dst] ⊙ [h2_s > 0] recomputed from the node rows and mask2 (row = s·RE + e)
 };
 struct WgradArgs {
     int64_t rows;          // logical rows L = s*count + n
@@ -130,6 +132,9 @@ struct WgradArgs {
     // edge/node context
     const float* pos;
     const int32_t *esrc, *edst;
+    const float *A, *U, *V, *G3;   // chunk-major; U, V, G3 per step at s·RN·kRowE
+    const uint32_t* mask2;         // per step at s·(RE/32)·160
+    int64_t RE, RN;
     float* slab;           // [chunks][kx_pad][ny_pad]
 };
 struct ReduceArgs {

@@ -227,7 +227,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
         // G3 rows (L2-resident node rows) run one chunk ahead in a 2-slot ring (loop unrolled by
         // 2, no register copies); W2ᵀ fragments come from the LDS image (ONEHOT) or global
         float4 g0 = G4[0], g1;
-        float* dh2cm = a.dh2_out + (int64_t)blk * kCmBlk + h * 128 + i * 4;   // dh2pre rows (chunk-major)
+        float* dh2cm = a.dh2_out ? a.dh2_out + (int64_t)blk * kCmBlk + h * 128 + i * 4 : nullptr;   // optional dh2pre rows
         auto chunk = [&](int q, const float4& g, float4& ahead) {
             const uint32_t bits = (uint32_t)(q < 16 ? mlo >> (4 * q) : (uint64_t)(mhi >> (4 * q - 64)));
             float xv[4];
@@ -235,7 +235,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
             xv[1] = (bits & 2u) ? g.y : 0.f;
             xv[2] = (bits & 4u) ? g.z : 0.f;
             xv[3] = (bits & 8u) ? g.w : 0.f;
-            *reinterpret_cast<float4*>(dh2cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+            if (a.dh2_out) *reinterpret_cast<float4*>(dh2cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
             ahead = G4[64 * min(q + 1, kKhE / 4 - 1)];  // unconditional (clamped) prefetch
             const float* wq = wrow + (ONEHOT ? 4 * q : 4 * q * kLdE);
             float4 wv = ONEHOT ? *reinterpret_cast<const float4*>(wq)

@@ -164,6 +164,81 @@ struct CmStage {
     }
 };
 
+// Recomputed edge operands of the W2 gradient (XM_H1 / YM_DH2): thread tid stages edge rr = tid & 31
+// of the 32-edge block and the column groups c4 = (tid >> 5) + 8k, like CmStage; the gathered node
+// rows (U[src], V[dst], G3[dst]) are chunk-major, so a group's 32 lanes read ≤ 16 distinct nodes'
+// contiguous pieces. X = [relu(A + U[src] + V[dst]) | 1], Y = G3[dst] ⊙ [h2 > 0].
+struct EdgeStage {
+    static constexpr int NG = 5;
+    int off[NG];                 // in-block offset of group k for row 0 (-1: padding ≥ 152)
+    int ones_k, ones_c;
+    float4 ra[NG], ru[NG], rv[NG];
+    uint32_t mw[NG];
+    bool in;
+    __device__ __forceinline__ void init(int tid, int ones) {
+        const int c0 = tid >> 5;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int f0 = 4 * (c0 + 8 * k);
+            off[k] = f0 < 2 * kKhE ? cm_offk<kKhE>(0, f0) : -1;
+        }
+        ones_k = (ones >= 0 && ((ones >> 2) & 7) == c0) ? (ones >> 5) : -1;
+        ones_c = ones & 3;
+    }
+    // rows r0..r0+31 of step s: edges e0 + rr of block blk
+    template <bool X>
+    __device__ __forceinline__ void fetch(const WgradArgs& a, int64_t r0, int64_t r_end, int tid) {
+        const int rr = tid & 31;
+        const int64_t s = r0 / a.RE, e = r0 - s * a.RE + rr;
+        const int src = a.esrc[e], dst = a.edst[e];
+        in = (r0 + rr < r_end) && src >= 0;
+        const int sn = in ? src : 0, dn = in ? dst : 0;
+        const int64_t nstep = s * a.RN * kRowE;
+        const float* pu = (X ? a.U : a.G3) + nstep + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
+        if (X) {
+            const float* pa = a.A + (e >> 5) * kCmBlk + rr * 4;
+            const float* ps = a.U + nstep + (int64_t)(sn >> 5) * kCmBlk + (sn & 31) * 4;
+            const float* pv = a.V + nstep + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const int o = off[k] < 0 ? 0 : off[k];
+                ra[k] = *reinterpret_cast<const float4*>(pa + o);
+                ru[k] = *reinterpret_cast<const float4*>(ps + o);
+                rv[k] = *reinterpret_cast<const float4*>(pv + o);
+            }
+        } else {
+            const uint32_t* pm = a.mask2 + (s * (a.RE >> 5) + (e >> 5)) * 160 + rr;
+            const int c0 = tid >> 5;
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const int o = off[k] < 0 ? 0 : off[k];
+                ru[k] = *reinterpret_cast<const float4*>(pu + o);
+                mw[k] = pm[((4 * (c0 + 8 * k)) >> 5) * 32];   // word (tile of f0, edge rr)
+            }
+        }
+    }
+    template <bool X>
+    __device__ __forceinline__ void write(float* S, int ld, int tid) const {
+        float* row = S + (tid & 31) * ld + 4 * (tid >> 5);
+        const int c0 = tid >> 5;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            float4 v = f4zero();
+            if (in && off[k] >= 0) {
+                if (X) {
+                    v = f4relu(f4add3(ra[k], ru[k], rv[k]));
+                } else {
+                    const uint32_t b = mw[k] >> ((4 * (c0 + 8 * k)) & 31);
+                    v = make_float4((b & 1u) ? ru[k].x : 0.f, (b & 2u) ? ru[k].y : 0.f, (b & 4u) ? ru[k].z : 0.f,
+                                    (b & 8u) ? ru[k].w : 0.f);
+                }
+            }
+            if (X && k == ones_k) f4set(v, ones_c, 1.f);   // the b2 ones column (padding rows too: dh2 = 0)
+            *reinterpret_cast<float4*>(row + 32 * k) = v;
+        }
+    }
+};
+
 // dW[k][n] (slab per chunk) = Σ_{rows of the chunk} X[row][k] · Y[row][n] on v_mfma_f32_16x16x4_f32.
 // The (KXP/16)×(NYP/16) output tiles split 2×2 over the 4 waves (5×5 tiles of 16×16 per wave at
 // 160×160, so every SIMD gets the same work); per k-step (4 rows) a wave reads MX + MY fragments
@@ -190,16 +265,23 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
 #pragma unroll
         for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
     // every operand is fetched a block ahead
-    constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM;
-    XRaw xr[XCM ? 1 : NGX];
-    YRaw yr[YCM ? 1 : NGY];
+    constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM, XH1 = XM == XM_H1, YD2 = YM == YM_DH2;
+    XRaw xr[(XCM || XH1) ? 1 : NGX];
+    YRaw yr[(YCM || YD2) ? 1 : NGY];
     CmStage<KXP> xc;
     CmStage<NYP> yc;
+    EdgeStage xe, ye;
     if (XCM) xc.init(tid, a.x_ones);
     if (YCM) yc.init(tid, -1);
+    if (XH1) xe.init(tid, a.x_ones);
+    if (YD2) ye.init(tid, -1);
     const int64_t xcount = (XM == XM_ROW || XM == XM_CM) ? a.x_count : a.rows;
     const int64_t ycount = a.y_count;
     auto fetch_xs = [&](int64_t r0) {
+        if constexpr (XH1) {
+            xe.fetch<true>(a, r0, r_end, tid);
+            return;
+        }
         const RowBase xb = row_base(r0, xcount);
         if constexpr (XCM) {
             const int rr = tid & 31;
@@ -215,6 +297,10 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
         }
     };
     auto fetch_ys = [&](int64_t r0) {
+        if constexpr (YD2) {
+            ye.fetch<false>(a, r0, r_end, tid);
+            return;
+        }
         const RowBase yb = row_base(r0, ycount);
         if constexpr (YCM) {
             const int rr = tid & 31;
@@ -236,7 +322,9 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     fetch(r_begin);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
-        if constexpr (XCM) {
+        if constexpr (XH1) {
+            xe.write<true>(Xs, LDX, tid);
+        } else if constexpr (XCM) {
             xc.write(Xs, LDX, tid);
         } else {
 #pragma unroll
@@ -249,7 +337,9 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
                 }
             }
         }
-        if constexpr (YCM) {
+        if constexpr (YD2) {
+            ye.write<false>(Ys, LDY, tid);
+        } else if constexpr (YCM) {
             yc.write(Ys, LDY, tid);
         } else {
 #pragma unroll
@@ -403,6 +493,7 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
     SPW_WG(XM_EDGE_D, YM_CM, 32, 160)
     SPW_WG(XM_NODE_O, YM_CM, 32, 128)
     SPW_WG(XM_CM, YM_CM, 160, 160)
+    SPW_WG(XM_H1, YM_DH2, 160, 160)
 #undef SPW_WG
     return hipErrorInvalidValue;
 }
