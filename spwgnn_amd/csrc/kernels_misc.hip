@@ -175,6 +175,14 @@ struct EdgeStage {
     float4 ra[NG], ru[NG], rv[NG];
     uint32_t mw[NG];
     bool in;
+    int pre_src, pre_dst;        // edge indices of the block after the one being fetched
+    // the edge indices run one block ahead of the gathers that depend on them
+    __device__ __forceinline__ void fetch_idx(const WgradArgs& a, int64_t r0, int tid) {
+        const int64_t s = r0 / a.RE, e = r0 - s * a.RE + (tid & 31);
+        const int64_t ec = r0 < a.rows ? e : 0;
+        pre_src = a.esrc[ec];
+        pre_dst = a.edst[ec];
+    }
     __device__ __forceinline__ void init(int tid, int ones) {
         const int c0 = tid >> 5;
 #pragma unroll
@@ -190,7 +198,8 @@ struct EdgeStage {
     __device__ __forceinline__ void fetch(const WgradArgs& a, int64_t r0, int64_t r_end, int tid) {
         const int rr = tid & 31;
         const int64_t s = r0 / a.RE, e = r0 - s * a.RE + rr;
-        const int src = a.esrc[e], dst = a.edst[e];
+        const int src = pre_src, dst = pre_dst;
+        fetch_idx(a, r0 + 32, tid);
         in = (r0 + rr < r_end) && src >= 0;
         const int sn = in ? src : 0, dn = in ? dst : 0;
         const int64_t nstep = s * a.RN * kRowE;
@@ -273,8 +282,14 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     EdgeStage xe, ye;
     if (XCM) xc.init(tid, a.x_ones);
     if (YCM) yc.init(tid, -1);
-    if (XH1) xe.init(tid, a.x_ones);
-    if (YD2) ye.init(tid, -1);
+    if (XH1) {
+        xe.init(tid, a.x_ones);
+        xe.fetch_idx(a, r_begin, tid);
+    }
+    if (YD2) {
+        ye.init(tid, -1);
+        ye.fetch_idx(a, r_begin, tid);
+    }
     const int64_t xcount = (XM == XM_ROW || XM == XM_CM) ? a.x_count : a.rows;
     const int64_t ycount = a.y_count;
     auto fetch_xs = [&](int64_t r0) {
