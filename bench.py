@@ -173,6 +173,8 @@ def main():
     ap.add_argument("--roofline-kernel", default="edge_bwd", choices=sorted(KERNELS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--math", default="x6", choices=["x6", "f32"],
+                    help="matrix-product arithmetic (spwgnn.h SPWGNN_MATH_*)")
     ap.add_argument("--infer", action="store_true",
                     help="BASELINE config 5: forward-only inference replayed from a hipGraph "
                          "(defaults: 32-block towers, S=10, 8192 towers/GPU)")
@@ -197,7 +199,7 @@ def main():
     params = P.to_flat(P.glorot_uniform(0), device=device)
     if world > 1:
         dist.broadcast(params, 0)
-    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7)
+    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=args.math)
 
     for _ in range(args.warmup):
         trainer.step(batch, target)

@@ -104,7 +104,7 @@ typedef struct spwgnn_run {
     int32_t mp_steps;   /* propagation steps; the reference hard-codes 5 (Networks.py:173)      */
     int32_t training;   /* 1: keep activations for backward + apply dropout                      */
     float dropout;      /* Dropout rate on the two encodings (Networks.py:167-168); 0 = off      */
-    int32_t pad0;
+    int32_t math;       /* SPWGNN_MATH_*: how the fp32 matrix products run on the matrix cores   */
     uint64_t seed;      /* dropout mask key                                                       */
     /* Optional timing hook (bench/profiling): for each launch of kernel `prof_kernel`
      * (SPWGNN_K_*), the library records caller-created hipEvent_t prof_events[2k] before and
@@ -113,6 +113,13 @@ typedef struct spwgnn_run {
     int32_t prof_count;
     void** prof_events;
 } spwgnn_run;
+
+/* Matrix-product arithmetic. Both give fp32-class results:
+ *   F32  v_mfma_f32_*_f32: one fp32 fma chain per output (the f32 MFMA rate, 157 TF)
+ *   X6   each fp32 operand split into three bf16 parts, six bf16 MFMA products per fp32 product,
+ *        fp32 accumulation (6/16 of the f32 MFMA cost; error O(2^-24) per product)            */
+#define SPWGNN_MATH_F32 0
+#define SPWGNN_MATH_X6 1
 
 #define SPWGNN_K_NONE 0
 #define SPWGNN_K_EDGE_FWD 1

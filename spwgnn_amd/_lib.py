@@ -36,12 +36,13 @@ class BatchC(C.Structure):
 
 
 class RunC(C.Structure):
-    _fields_ = [("mp_steps", C.c_int32), ("training", C.c_int32), ("dropout", C.c_float), ("pad0", C.c_int32),
+    _fields_ = [("mp_steps", C.c_int32), ("training", C.c_int32), ("dropout", C.c_float), ("math", C.c_int32),
                 ("seed", C.c_uint64), ("prof_kernel", C.c_int32), ("prof_count", C.c_int32),
                 ("prof_events", C.c_void_p)]
 
 
 K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WGRAD_W2 = 1, 2, 3, 4, 5, 6, 7
+MATH_F32, MATH_X6 = 0, 1
 READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 
 

@@ -3,6 +3,7 @@
 #include <cstring>
 #include "kernels.h"
 #include "../../include/spwgnn.h"
+static_assert(SPWGNN_MATH_F32 == spw::MATH_F32 && SPWGNN_MATH_X6 == spw::MATH_X6, "math ids");
 
 namespace spw {
 
@@ -195,6 +196,7 @@ static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
     if (r->mp_steps < 1 || r->mp_steps > 64) return SPWGNN_E_SHAPE;
     if (!b->pos || !b->wtile || !b->edge_src || !b->edge_dst || !b->blk_csr) return SPWGNN_E_ARG;
     if (r->dropout < 0.f || r->dropout >= 1.f) return SPWGNN_E_ARG;
+    if (r->math != SPWGNN_MATH_F32 && r->math != SPWGNN_MATH_X6) return SPWGNN_E_ARG;
     if (r->training && r->dropout > 0.f && (!b->node_tower || !b->node_local)) return SPWGNN_E_ARG;
     return SPWGNN_OK;
 }
@@ -361,7 +363,7 @@ struct WgSpec {
     bool recompute = false;   // XM_H1 / YM_DH2 context below
 };
 
-static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, hipStream_t st,
+static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, int math, hipStream_t st,
                          const Prof* prof = nullptr) {
     const Ws& w = c.w;
     if (g.rows <= 0) return SPWGNN_OK;
@@ -399,9 +401,10 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.mask2 = c.u(w.mask2);
         a.RE = w.RE;
         a.RN = w.RN;
+        a.S = (int)(g.rows / w.RE);
     }
     if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
-    SPW_CHECK(launch_wgrad(a, (int)chunks, st));
+    SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     const ParamTable& pt = param_table();
     ReduceArgs ra{};
@@ -537,21 +540,21 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
-    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, st))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, st))) return e; }
+    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
         // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
         g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
-        if ((e = run_wgrad(c, b, g, grads, st, &prof))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {
@@ -563,49 +566,49 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)
         WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
         g.rows = nN; g.y_stride = 0;
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
     }
     return SPWGNN_OK;
 }

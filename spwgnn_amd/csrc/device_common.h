@@ -29,6 +29,58 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 }
 __device__ __forceinline__ constexpr int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 products ("x6" math). gfx950's bf16 MFMA runs 16× the f32 MFMA rate;
+// an fp32 operand x is split (round-to-nearest at each stage) into x = h + m + l + O(2^-25·|x|)
+// with h, m, l bf16, and x·y ≈ hh + hm + mh + mm + hl + lh (the dropped ml, lm, ll terms are
+// O(2^-26)): six bf16 products with exact fp32 accumulation = fp32-class results at 6/16 of the
+// f32 MFMA cost.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    const bf2 r = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ float bf16_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+// (a, b) → three packed bf16 pairs h, m, l (element 0 = a in the low half)
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+    h = pk_bf16(a, b);
+    const float ra = a - bf16_lo(h), rb = b - bf16_hi(h);
+    m = pk_bf16(ra, rb);
+    l = pk_bf16(ra - bf16_lo(m), rb - bf16_hi(m));
+}
+__device__ __forceinline__ bf16x8 as_bf16x8(i16x4 lo, i16x4 hi) {
+    const i16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+// acc += a·b over the six split products (a[p], b[p]: parts h, m, l); small terms first
+__device__ __forceinline__ f32x4 mfma16_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+}
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, 16-bit columns 4p..4p+3 of a
+// 4×16 block; lane i of the group receives column i of the 4 rows (row q in element q)
+__device__ __forceinline__ i16x4 lds_tr16(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
+}
+
 __device__ __forceinline__ f32x16 zero16() {
     f32x16 z;
 #pragma unroll

@@ -135,6 +135,7 @@ struct WgradArgs {
     const float *A, *U, *V, *G3;   // chunk-major; U, V, G3 per step at s·RN·kRowE
     const uint32_t* mask2;         // per step at s·(RE/32)·160
     int64_t RE, RN;
+    int S;                         // steps (XM_H1 / YM_DH2 walk rows as (edge block, step) stages)
     float* slab;           // [chunks][kx_pad][ny_pad]
 };
 struct ReduceArgs {
@@ -173,7 +174,8 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
-hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st);
+enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.h)
+hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
 hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);

@@ -153,14 +153,18 @@ struct CmStage {
         for (int k = 0; k < NG; ++k)
             raw[k] = (in && off[k] >= 0) ? *reinterpret_cast<const float4*>(b + off[k]) : f4zero();
     }
-    __device__ __forceinline__ void write(float* S, int ld, int tid) const {
-        float* row = S + (tid & 31) * ld + 4 * (tid >> 5);
+    // f(rr, c4, v): the staged float4 of row rr, column group c4
+    template <class F>
+    __device__ __forceinline__ void emit(int tid, F&& f) const {
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             float4 v = raw[k];
             if (k == ones_k) f4set(v, ones_c, 1.f);   // the bias' ones column
-            *reinterpret_cast<float4*>(row + 32 * k) = v;
+            f(tid & 31, (tid >> 5) + 8 * k, v);
         }
+    }
+    __device__ __forceinline__ void write(float* S, int ld, int tid) const {
+        emit(tid, [&](int rr, int c4, float4 v) { *reinterpret_cast<float4*>(S + rr * ld + 4 * c4) = v; });
     }
 };
 
@@ -168,6 +172,8 @@ struct CmStage {
 // of the 32-edge block and the column groups c4 = (tid >> 5) + 8k, like CmStage; the gathered node
 // rows (U[src], V[dst], G3[dst]) are chunk-major, so a group's 32 lanes read ≤ 16 distinct nodes'
 // contiguous pieces. X = [relu(A + U[src] + V[dst]) | 1], Y = G3[dst] ⊙ [h2 > 0].
+// Rows are walked as 32-row stages t = r0/32 = (edge block b = t / S, step s = t % S): the S steps
+// of an edge block are consecutive, so its A rows (the same at every step) are fetched once.
 struct EdgeStage {
     static constexpr int NG = 5;
     int off[NG];                 // in-block offset of group k for row 0 (-1: padding ≥ 152)
@@ -175,10 +181,10 @@ struct EdgeStage {
     float4 ra[NG], ru[NG], rv[NG];
     uint32_t mw[NG];
     bool in;
-    int pre_src, pre_dst;        // edge indices of the block after the one being fetched
-    // the edge indices run one block ahead of the gathers that depend on them
+    int pre_src, pre_dst;        // edge indices of the stage after the one being fetched
+    // the edge indices run one stage ahead of the gathers that depend on them
     __device__ __forceinline__ void fetch_idx(const WgradArgs& a, int64_t r0, int tid) {
-        const int64_t s = r0 / a.RE, e = r0 - s * a.RE + (tid & 31);
+        const int64_t b = (r0 >> 5) / a.S, e = 32 * b + (tid & 31);
         const int64_t ec = r0 < a.rows ? e : 0;
         pre_src = a.esrc[ec];
         pre_dst = a.edst[ec];
@@ -195,9 +201,9 @@ struct EdgeStage {
     }
     // rows r0..r0+31 of step s: edges e0 + rr of block blk
     template <bool X>
-    __device__ __forceinline__ void fetch(const WgradArgs& a, int64_t r0, int64_t r_end, int tid) {
+    __device__ __forceinline__ void fetch(const WgradArgs& a, int64_t r0, int64_t r_begin, int64_t r_end, int tid) {
         const int rr = tid & 31;
-        const int64_t s = r0 / a.RE, e = r0 - s * a.RE + rr;
+        const int64_t t = r0 >> 5, b = t / a.S, s = t - b * a.S, e = 32 * b + rr;
         const int src = pre_src, dst = pre_dst;
         fetch_idx(a, r0 + 32, tid);
         in = (r0 + rr < r_end) && src >= 0;
@@ -205,13 +211,16 @@ struct EdgeStage {
         const int64_t nstep = s * a.RN * kRowE;
         const float* pu = (X ? a.U : a.G3) + nstep + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
         if (X) {
-            const float* pa = a.A + (e >> 5) * kCmBlk + rr * 4;
+            if (s == 0 || r0 == r_begin) {   // wave-uniform: a new edge block
+                const float* pa = a.A + b * kCmBlk + rr * 4;
+#pragma unroll
+                for (int k = 0; k < NG; ++k) ra[k] = *reinterpret_cast<const float4*>(pa + (off[k] < 0 ? 0 : off[k]));
+            }
             const float* ps = a.U + nstep + (int64_t)(sn >> 5) * kCmBlk + (sn & 31) * 4;
             const float* pv = a.V + nstep + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
 #pragma unroll
             for (int k = 0; k < NG; ++k) {
                 const int o = off[k] < 0 ? 0 : off[k];
-                ra[k] = *reinterpret_cast<const float4*>(pa + o);
                 ru[k] = *reinterpret_cast<const float4*>(ps + o);
                 rv[k] = *reinterpret_cast<const float4*>(pv + o);
             }
@@ -226,9 +235,8 @@ struct EdgeStage {
             }
         }
     }
-    template <bool X>
-    __device__ __forceinline__ void write(float* S, int ld, int tid) const {
-        float* row = S + (tid & 31) * ld + 4 * (tid >> 5);
+    template <bool X, class F>
+    __device__ __forceinline__ void emit(int tid, F&& f) const {
         const int c0 = tid >> 5;
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
@@ -243,7 +251,115 @@ struct EdgeStage {
                 }
             }
             if (X && k == ones_k) f4set(v, ones_c, 1.f);   // the b2 ones column (padding rows too: dh2 = 0)
-            *reinterpret_cast<float4*>(row + 32 * k) = v;
+            f(tid & 31, c0 + 8 * k, v);
+        }
+    }
+    template <bool X>
+    __device__ __forceinline__ void write(float* S, int ld, int tid) const {
+        emit<X>(tid, [&](int rr, int c4, float4 v) { *reinterpret_cast<float4*>(S + rr * ld + 4 * c4) = v; });
+    }
+};
+
+// Operand staging shared by the wgrad kernels: every operand is fetched a 32-row block ahead into
+// registers (fetch), then handed out as float4 groups (emit_x / emit_y: f(row rr, column group c4, v)).
+template <int XM, int YM, int KXP, int NYP>
+struct WgStage {
+    static constexpr int GX = KXP / 4, GY = NYP / 4;
+    static constexpr int NGX = (32 * GX + kWgThreads - 1) / kWgThreads;   // float4 groups per thread
+    static constexpr int NGY = (32 * GY + kWgThreads - 1) / kWgThreads;
+    static constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM, XH1 = XM == XM_H1, YD2 = YM == YM_DH2;
+    XRaw xr[(XCM || XH1) ? 1 : NGX];
+    YRaw yr[(YCM || YD2) ? 1 : NGY];
+    CmStage<KXP> xc;
+    CmStage<NYP> yc;
+    EdgeStage xe, ye;
+    int64_t xcount, ycount, r_begin, r_end;
+    __device__ __forceinline__ void init(const WgradArgs& a, int64_t r_begin_, int64_t r_end_, int tid) {
+        r_begin = r_begin_;
+        r_end = r_end_;
+        if (XCM) xc.init(tid, a.x_ones);
+        if (YCM) yc.init(tid, -1);
+        if (XH1) {
+            xe.init(tid, a.x_ones);
+            xe.fetch_idx(a, r_begin, tid);
+        }
+        if (YD2) {
+            ye.init(tid, -1);
+            ye.fetch_idx(a, r_begin, tid);
+        }
+        xcount = (XM == XM_ROW || XM == XM_CM) ? a.x_count : a.rows;
+        ycount = a.y_count;
+    }
+    __device__ __forceinline__ void fetch(const WgradArgs& a, int64_t r0, int tid) {
+        if constexpr (XH1) {
+            xe.fetch<true>(a, r0, r_begin, r_end, tid);
+        } else {
+            const RowBase xb = row_base(r0, xcount);
+            if constexpr (XCM) {
+                const int rr = tid & 31;
+                xc.fetch(a.x_ptr, phys_row(xb, rr, a.x_stride), r0 + rr < r_end);
+            } else {
+#pragma unroll
+                for (int k = 0; k < NGX; ++k) {
+                    const int g = tid + k * kWgThreads;
+                    int rr, c4;
+                    group_rc<false, GX>(g, rr, c4);
+                    fetch_x<XM, KXP>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
+                }
+            }
+        }
+        if constexpr (YD2) {
+            ye.fetch<false>(a, r0, r_begin, r_end, tid);
+        } else {
+            const RowBase yb = row_base(r0, ycount);
+            if constexpr (YCM) {
+                const int rr = tid & 31;
+                yc.fetch(a.y_ptr, phys_row(yb, rr, a.y_stride), r0 + rr < r_end);
+            } else {
+#pragma unroll
+                for (int k = 0; k < NGY; ++k) {
+                    const int g = tid + k * kWgThreads;
+                    int rr, c4;
+                    group_rc<false, GY>(g, rr, c4);
+                    fetch_y<YM, NYP>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
+                }
+            }
+        }
+    }
+    template <class F>
+    __device__ __forceinline__ void emit_x(const WgradArgs& a, int tid, F&& f) const {
+        if constexpr (XH1) {
+            xe.emit<true>(tid, f);
+        } else if constexpr (XCM) {
+            xc.emit(tid, f);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NGX; ++k) {
+                const int g = tid + k * kWgThreads;
+                if (g < 32 * GX) {
+                    int rr, c4;
+                    group_rc<false, GX>(g, rr, c4);
+                    f(rr, c4, finish_x<XM>(a, 4 * c4, xr[k]));
+                }
+            }
+        }
+    }
+    template <class F>
+    __device__ __forceinline__ void emit_y(int tid, F&& f) const {
+        if constexpr (YD2) {
+            ye.emit<false>(tid, f);
+        } else if constexpr (YCM) {
+            yc.emit(tid, f);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NGY; ++k) {
+                const int g = tid + k * kWgThreads;
+                if (g < 32 * GY) {
+                    int rr, c4;
+                    group_rc<false, GY>(g, rr, c4);
+                    f(rr, c4, finish_y(yr[k]));
+                }
+            }
         }
     }
 };
@@ -258,9 +374,6 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     constexpr int MX = KXP / 32, MY = NYP / 32;    // 16×16 tiles per wave along X / Y features
     constexpr int LDX = KXP + 16, LDY = NYP + 16;  // ≡ 16 (mod 32): the 4 rows of a fragment read
                                                    // fall in alternate bank halves (no conflicts)
-    constexpr int GX = KXP / 4, GY = NYP / 4;
-    constexpr int NGX = (32 * GX + kWgThreads - 1) / kWgThreads;   // float4 groups per thread
-    constexpr int NGY = (32 * GY + kWgThreads - 1) / kWgThreads;
     __shared__ __attribute__((aligned(16))) float Xs[32 * LDX];
     __shared__ __attribute__((aligned(16))) float Ys[32 * LDY];
     const int tid = threadIdx.x, lane = tid & 63, c16 = lane & 15, kq = lane >> 4;
@@ -273,102 +386,15 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
     for (int x = 0; x < MX; ++x)
 #pragma unroll
         for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // every operand is fetched a block ahead
-    constexpr bool XCM = XM == XM_CM, YCM = YM == YM_CM, XH1 = XM == XM_H1, YD2 = YM == YM_DH2;
-    XRaw xr[(XCM || XH1) ? 1 : NGX];
-    YRaw yr[(YCM || YD2) ? 1 : NGY];
-    CmStage<KXP> xc;
-    CmStage<NYP> yc;
-    EdgeStage xe, ye;
-    if (XCM) xc.init(tid, a.x_ones);
-    if (YCM) yc.init(tid, -1);
-    if (XH1) {
-        xe.init(tid, a.x_ones);
-        xe.fetch_idx(a, r_begin, tid);
-    }
-    if (YD2) {
-        ye.init(tid, -1);
-        ye.fetch_idx(a, r_begin, tid);
-    }
-    const int64_t xcount = (XM == XM_ROW || XM == XM_CM) ? a.x_count : a.rows;
-    const int64_t ycount = a.y_count;
-    auto fetch_xs = [&](int64_t r0) {
-        if constexpr (XH1) {
-            xe.fetch<true>(a, r0, r_end, tid);
-            return;
-        }
-        const RowBase xb = row_base(r0, xcount);
-        if constexpr (XCM) {
-            const int rr = tid & 31;
-            xc.fetch(a.x_ptr, phys_row(xb, rr, a.x_stride), r0 + rr < r_end);
-        } else {
-#pragma unroll
-            for (int k = 0; k < NGX; ++k) {
-                const int g = tid + k * kWgThreads;
-                int rr, c4;
-                group_rc<false, GX>(g, rr, c4);
-                fetch_x<XM, KXP>(a, xb, rr, 4 * c4, g < 32 * GX && r0 + rr < r_end, xr[k]);
-            }
-        }
-    };
-    auto fetch_ys = [&](int64_t r0) {
-        if constexpr (YD2) {
-            ye.fetch<false>(a, r0, r_end, tid);
-            return;
-        }
-        const RowBase yb = row_base(r0, ycount);
-        if constexpr (YCM) {
-            const int rr = tid & 31;
-            yc.fetch(a.y_ptr, phys_row(yb, rr, a.y_stride), r0 + rr < r_end);
-        } else {
-#pragma unroll
-            for (int k = 0; k < NGY; ++k) {
-                const int g = tid + k * kWgThreads;
-                int rr, c4;
-                group_rc<false, GY>(g, rr, c4);
-                fetch_y<YM, NYP>(a, yb, rr, 4 * c4, g < 32 * GY && r0 + rr < r_end, yr[k]);
-            }
-        }
-    };
-    auto fetch = [&](int64_t r0) {
-        fetch_xs(r0);
-        fetch_ys(r0);
-    };
-    fetch(r_begin);
+    WgStage<XM, YM, KXP, NYP> st;
+    st.init(a, r_begin, r_end, tid);
+    st.fetch(a, r_begin, tid);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
-        if constexpr (XH1) {
-            xe.write<true>(Xs, LDX, tid);
-        } else if constexpr (XCM) {
-            xc.write(Xs, LDX, tid);
-        } else {
-#pragma unroll
-            for (int k = 0; k < NGX; ++k) {
-                const int g = tid + k * kWgThreads;
-                if (g < 32 * GX) {
-                    int rr, c4;
-                    group_rc<false, GX>(g, rr, c4);
-                    *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = finish_x<XM>(a, 4 * c4, xr[k]);
-                }
-            }
-        }
-        if constexpr (YD2) {
-            ye.write<false>(Ys, LDY, tid);
-        } else if constexpr (YCM) {
-            yc.write(Ys, LDY, tid);
-        } else {
-#pragma unroll
-            for (int k = 0; k < NGY; ++k) {
-                const int g = tid + k * kWgThreads;
-                if (g < 32 * GY) {
-                    int rr, c4;
-                    group_rc<false, GY>(g, rr, c4);
-                    *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = finish_y(yr[k]);
-                }
-            }
-        }
+        st.emit_x(a, tid, [&](int rr, int c4, float4 v) { *reinterpret_cast<float4*>(&Xs[rr * LDX + 4 * c4]) = v; });
+        st.emit_y(tid, [&](int rr, int c4, float4 v) { *reinterpret_cast<float4*>(&Ys[rr * LDY + 4 * c4]) = v; });
         __syncthreads();
-        if (r0 + 32 < r_end) fetch(r0 + 32);
+        if (r0 + 32 < r_end) st.fetch(a, r0 + 32, tid);
         const float* xs = Xs + kq * LDX + 16 * MX * wx + c16;
         const float* ys = Ys + kq * LDY + 16 * MY * wy + c16;
 #pragma unroll 2
@@ -385,6 +411,95 @@ __global__ __launch_bounds__(kWgThreads, 2) void k_wgrad_t(WgradArgs a) {
         }
     }
     // C layout of a 16×16 tile: reg r of lane l = row 4(l>>4) + r, col l&15
+    float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
+#pragma unroll
+    for (int x = 0; x < MX; ++x)
+#pragma unroll
+        for (int y = 0; y < MY; ++y)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(int64_t)(16 * (MX * wx + x) + 4 * kq + r) * NYP + 16 * (MY * wy + y) + c16] = acc[x][y][r];
+}
+
+// Split-bf16 LDS image of a staged [32 rows][W] operand: three parts (h, m, l), each [row][W] bf16,
+// read back transposed with ds_read_b64_tr_b16. 16-column units (32 B) are XOR-swizzled per row so
+// that the 8 rows one 32-lane half reads land on 64 distinct banks (row pitch W·2 bytes: 80 dwords
+// ≡ 16 (mod 64) at W = 160 and 32 → swizzle by row bit 2; 64 dwords at W = 128 → by row & 7).
+template <int W>
+struct X6Img {
+    static constexpr int ROWB = W * 2, PART = 32 * ROWB;
+    __device__ static __forceinline__ int sigma(int r) { return (ROWB % 256 == 0) ? (r & 7) : ((r >> 2) & 1); }
+    __device__ static __forceinline__ int woff(int rr, int c4) {
+        return rr * ROWB + 32 * ((c4 >> 2) ^ sigma(rr)) + 8 * (c4 & 3);
+    }
+    // lane's read offset for 16-column tile t: group g = lane>>4 reads rows 4g..4g+3 (elements 0-3)
+    // and 16+4g..16+4g+3 (elements 4-7, at + 16·ROWB) — the k order of the 16x16x32 operand, the
+    // same for both operands of a product
+    __device__ static __forceinline__ int roff(int lane, int t) {
+        const int li = lane & 15, row = 4 * (lane >> 4) + (li >> 2);
+        return row * ROWB + 32 * (t ^ sigma(row)) + 8 * (li & 3);
+    }
+    __device__ static __forceinline__ void put(char* S, int rr, int c4, float4 v) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split2(v.x, v.y, h0, m0, l0);
+        split2(v.z, v.w, h1, m1, l1);
+        char* p = S + woff(rr, c4);
+        *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(p + PART) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(p + 2 * PART) = make_uint2(l0, l1);
+    }
+    __device__ static __forceinline__ void get(const char* S, int off, bf16x8 (&f)[3]) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            f[p] = as_bf16x8(lds_tr16(S + p * PART + off), lds_tr16(S + p * PART + off + 16 * ROWB));
+    }
+};
+
+// The same gradient in split-bf16 math (x6): operands are split once when staged (every element
+// feeds MX or MY tiles), 16x16x32 bf16 MFMAs, one k-step per 32-row block: 6·MX·MY MFMAs of 16
+// cycles per wave per block instead of 8·MX·MY f32 MFMAs of 32.
+template <int XM, int YM, int KXP, int NYP, int OCC>
+__global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
+    constexpr int MX = KXP / 32, MY = NYP / 32;
+    using IX = X6Img<KXP>;
+    using IY = X6Img<NYP>;
+    __shared__ __attribute__((aligned(16))) char Xs[3 * IX::PART];
+    __shared__ __attribute__((aligned(16))) char Ys[3 * IY::PART];
+    const int tid = threadIdx.x, lane = tid & 63, c16 = lane & 15, kq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wx = wave >> 1, wy = wave & 1;
+    const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
+    const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
+    f32x4 acc[MX][MY];
+#pragma unroll
+    for (int x = 0; x < MX; ++x)
+#pragma unroll
+        for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int ox[MX], oy[MY];
+#pragma unroll
+    for (int x = 0; x < MX; ++x) ox[x] = IX::roff(lane, MX * wx + x);
+#pragma unroll
+    for (int y = 0; y < MY; ++y) oy[y] = IY::roff(lane, MY * wy + y);
+    WgStage<XM, YM, KXP, NYP> st;
+    st.init(a, r_begin, r_end, tid);
+    st.fetch(a, r_begin, tid);
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
+        __syncthreads();
+        st.emit_x(a, tid, [&](int rr, int c4, float4 v) { IX::put(Xs, rr, c4, v); });
+        st.emit_y(tid, [&](int rr, int c4, float4 v) { IY::put(Ys, rr, c4, v); });
+        __syncthreads();
+        if (r0 + 32 < r_end) st.fetch(a, r0 + 32, tid);
+        bf16x8 yb[MY][3];
+#pragma unroll
+        for (int y = 0; y < MY; ++y) IY::get(Ys, oy[y], yb[y]);
+#pragma unroll
+        for (int x = 0; x < MX; ++x) {
+            bf16x8 xa[3];
+            IX::get(Xs, ox[x], xa);
+#pragma unroll
+            for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6(xa, yb[y], acc[x][y]);
+        }
+    }
     float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
 #pragma unroll
     for (int x = 0; x < MX; ++x)
@@ -494,11 +609,14 @@ __global__ void k_tower_readout(const float* __restrict__ z, const int32_t* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_wgrad(const WgradArgs& a, int chunks, hipStream_t st) {
+hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st) {
     const dim3 g(chunks), b(kWgThreads);
 #define SPW_WG(XM, YM, KX, NY)                                                               \
     if (a.xmode == XM && a.ymode == YM && a.kx_pad == KX && a.ny_pad == NY) {                 \
-        hipLaunchKernelGGL((k_wgrad_t<XM, YM, KX, NY>), g, b, 0, st, a);                      \
+        if (math == MATH_X6)                                                           \
+            hipLaunchKernelGGL((k_wgrad_x6<XM, YM, KX, NY, (XM == XM_H1 || YM == YM_ROW) ? 1 : 2>), g, b, 0, st, a); \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_wgrad_t<XM, YM, KX, NY>), g, b, 0, st, a);                  \
         return hipGetLastError();                                                             \
     }
     SPW_WG(XM_CM, YM_ROW, 160, 160)

@@ -27,12 +27,16 @@ def _require_gpu(t: torch.Tensor, what: str):
         raise _lib.SpwgnnError(f"{what} must be a HIP device tensor (got {t.device}); the HIP path has no CPU fallback")
 
 
+MATH_MODES = {"f32": _lib.MATH_F32, "x6": _lib.MATH_X6}
+
+
 @dataclass
 class RunConfig:
     mp_steps: int = REF_MP_STEPS
     training: bool = False
     dropout: float = 0.0
     seed: int = 0
+    math: str = "x6"                     # "x6" split-bf16 matrix products | "f32" f32 MFMA (spwgnn.h)
     prof_kernel: int = 0                 # SPWGNN_K_* to bracket with HIP events (bench only)
     prof_events: Optional[list] = None   # raw hipEvent_t handles, 2 per launch
 
@@ -42,6 +46,9 @@ class RunConfig:
         r.training = 1 if self.training else 0
         r.dropout = float(self.dropout)
         r.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        if self.math not in MATH_MODES:
+            raise ValueError(f"math must be one of {sorted(MATH_MODES)}")
+        r.math = MATH_MODES[self.math]
         if self.prof_kernel and self.prof_events:
             arr = (C.c_void_p * len(self.prof_events))(*self.prof_events)
             self._prof_arr = arr   # keep alive for the call

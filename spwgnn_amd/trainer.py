@@ -50,12 +50,12 @@ class Trainer:
 
     def __init__(self, params: torch.Tensor, engine=None, mp_steps: int = E.REF_MP_STEPS,
                  dropout: float = E.REF_DROPOUT, seed: int = 0, lr: float = 5e-4, beta1: float = 0.9,
-                 beta2: float = 0.999, eps: float = 1e-7, l2: float = 0.0, group=None):
+                 beta2: float = 0.999, eps: float = 1e-7, l2: float = 0.0, group=None, math: str = "x6"):
         self.params = params
         self.engine = engine if engine is not None else HipEngine(params.device)
         self.m = torch.zeros_like(params)
         self.v = torch.zeros_like(params)
-        self.mp_steps, self.dropout, self.seed = mp_steps, dropout, seed
+        self.mp_steps, self.dropout, self.seed, self.math = mp_steps, dropout, seed, math
         self.lr, self.b1, self.b2, self.eps, self.l2 = lr, beta1, beta2, eps, l2
         self.iterations = 0
         self.group = group
@@ -68,7 +68,7 @@ class Trainer:
     def run_config(self) -> E.RunConfig:
         # distinct dropout keys per step and per rank (a rank's towers are different towers)
         key = (self.seed * 1_000_003 + self.iterations) * 4099 + self.rank
-        return E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, seed=key,
+        return E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, seed=key, math=self.math,
                            prof_kernel=self.prof_kernel, prof_events=self.prof_events)
 
     def step(self, batch: TowerBatch, target: torch.Tensor):

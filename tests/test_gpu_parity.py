@@ -23,21 +23,22 @@ def _oracle_logits(params, obj, Rs, Rr, prop, S):
     return z.numpy()
 
 
-def _gpu_forward(params, batch, S, training=False):
+def _gpu_forward(params, batch, S, training=False, math="x6"):
     flat = P.to_flat(params, device="cuda")
     ws = E.Workspace("cuda")
-    z = E.forward(flat, batch, E.RunConfig(S, training=training), ws)
+    z = E.forward(flat, batch, E.RunConfig(S, training=training, math=math), ws)
     torch.cuda.synchronize()
     return flat, ws, z
 
 
+@pytest.mark.parametrize("math", ["x6", "f32"])
 @pytest.mark.parametrize("S", [1, 3, 5])
 @pytest.mark.parametrize("fully", [True, False])
-def test_forward_parity_small(S, fully):
+def test_forward_parity_small(S, fully, math):
     params = O.random_params(seed=3)
     obj, Rs, Rr, prop, _ = D.synthetic_batch(8, 6, seed=11, fully_connected=fully)
     batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
-    _, _, z = _gpu_forward(params, batch, S)
+    _, _, z = _gpu_forward(params, batch, S, math=math)
     ref = _oracle_logits(params, obj, Rs, Rr, prop, S)
     got = z.cpu().numpy().reshape(ref.shape)
     err = np.abs(got - ref)
@@ -60,17 +61,18 @@ def test_forward_parity_sizes(N):
 
 # (towers, nodes, nw_max): nw_max <= 16 runs the backward segment sums as a one-hot matrix product,
 # larger wave-tiles walk the block csr through LDS — both paths, single- and multi-tower tiles.
+@pytest.mark.parametrize("math", ["x6", "f32"])
 @pytest.mark.parametrize("T,N,nw", [(6, 6, None), (6, 6, 6), (5, 16, None), (7, 5, 32), (3, 20, None), (2, 32, None)])
-def test_backward_parity_small(T, N, nw):
+def test_backward_parity_small(T, N, nw, math):
     params = O.random_params(seed=7)
     obj, Rs, Rr, prop, tgt = D.synthetic_batch(T, N, seed=2, fully_connected=False)
     S = 5
     loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, S)
     batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda", nw_max=nw)
-    flat, ws, z = _gpu_forward(params, batch, S, training=True)
+    flat, ws, z = _gpu_forward(params, batch, S, training=True, math=math)
     scratch = E.BceScratch("cuda")
     out3, dz = E.bce(z, torch.tensor(tgt, device="cuda").reshape(-1), scratch)
-    grads, _ = E.backward(flat, batch, E.RunConfig(S, training=True), ws, dz)
+    grads, _ = E.backward(flat, batch, E.RunConfig(S, training=True, math=math), ws, dz)
     torch.cuda.synchronize()
     assert abs(float(out3[0]) - loss_ref) < 1e-5
     got = P.from_flat(grads)
