@@ -25,6 +25,8 @@ struct Ws {
     int64_t slab, bce;
     int64_t slab_floats;
     PackSlots ps;
+    int64_t x6;                                      // split-bf16 weight images (uint4 units below)
+    int64_t x6off[X6_COUNT];
     int sP() const { return training ? S + 1 : 2; }
     int sStep() const { return training ? S : 1; }
     // node arrays are chunk-major (104 / 152 floats per row): a step's rows are RN/32 blocks
@@ -71,6 +73,15 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     }
     w.ps.total = poff;
     w.pk = take(poff);
+    {   // x6 images (uint4 = 4 floats each)
+        const int nt_nkb[X6_COUNT][2] = {{5, 10}, {5, 10}, {5, 10}, {5, 10}};
+        int64_t o = 0;
+        for (int id = 0; id < X6_COUNT; ++id) {
+            w.x6off[id] = o;
+            o += x6_chain_uint4(nt_nkb[id][0], nt_nkb[id][1]);
+        }
+        w.x6 = take(o * 4);
+    }
     const int64_t nN = w.RN * kRowN, nE = w.RN * kRowE, eE = w.RE * kLdE;
     w.co = take(nN);
     w.P = take(nN * w.sP());
@@ -187,6 +198,7 @@ struct Ctx {
     float* f(int64_t off) const { return off < 0 ? nullptr : reinterpret_cast<float*>(base) + off; }
     uint32_t* u(int64_t off) const { return off < 0 ? nullptr : reinterpret_cast<uint32_t*>(base) + off; }
     const float* pk(int id) const { return reinterpret_cast<const float*>(base) + w.pk + w.ps.off[id]; }
+    const uint4* x6(int id) const { return reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + w.x6) + w.x6off[id]; }
 };
 
 static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
@@ -231,6 +243,24 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     pa.pk = c.f(w.pk);
     build_packs(w, pa);
     SPW_CHECK(launch_prep_weights(pa, st));
+    if (r->math == MATH_X6) {
+        PrepX6Args xa{};
+        xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
+        auto chain = [&](int id, int pid, int nt_out, int nkb) {
+            X6Desc& d = xa.d[id];
+            d.src = c.pk(pid);
+            d.cols = pack_cols(pid);
+            d.k4 = pa.desc[pid].k4;
+            d.nt_out = nt_out;
+            d.nkb = nkb;
+            d.dst = w.x6off[id];
+        };
+        chain(X6_RM1, PK_RM1, 5, 10);
+        chain(X6_RM2, PK_RM2, 5, 10);
+        chain(X6_RM3, PK_RM3, 5, 10);
+        chain(X6_W1A, PK_W1A, 5, 10);
+        SPW_CHECK(launch_prep_x6(xa, st));
+    }
     // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
     // (k4-blocked: element (150, c) sits at ((150/4)·128 + c)·4 + 150%4, a 16-byte stride)
     SPW_CHECK(hipMemcpy2DAsync(c.f(w.pk + w.ps.off[PK_W3A] + ((150 / 4) * kLdN) * 4 + 150 % 4), 4 * sizeof(float),
@@ -280,6 +310,12 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.b_rm3 = c.pk(PB_RM3);
     ee.w_w1a = c.pk(PK_W1A);
     ee.b_w1a = c.pk(PB_W1A);
+    if (r->math == MATH_X6) {
+        ee.x_rm1 = c.x6(X6_RM1);
+        ee.x_rm2 = c.x6(X6_RM2);
+        ee.x_rm3 = c.x6(X6_RM3);
+        ee.x_w1a = c.x6(X6_W1A);
+    }
     ee.z1 = c.f(w.z1);
     ee.z2 = c.f(w.z2);
     ee.z3 = c.f(w.z3);
@@ -293,7 +329,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     {
         Prof p0{r, st};
         SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
-        SPW_CHECK(launch_enc_edge(ee, st));
+        SPW_CHECK(launch_enc_edge(ee, r->math, st));
         SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
     }
 

@@ -97,6 +97,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+// The 2-input first Dense of the encoders with one explicit rounding order: left to the compiler,
+// unrolled copies of x0·w0 + x1·w1 + b were contracted / paired differently, so an edge's value
+// depended on which copy (column tile) processed it.
+__device__ __forceinline__ float dense2(float x0, float x1, float w0, float w1, float b) {
+    return __builtin_fmaf(x1, w1, __builtin_fmaf(x0, w0, b));
+}
 
 // Put a wave-uniform 32-bit value into lane `ln` of `old` (v_cmp + v_cndmask; no exec branch).
 __device__ __forceinline__ uint32_t writelane(uint32_t val, int ln, uint32_t old) {

@@ -20,6 +20,22 @@ struct PrepArgs {
     PackDesc desc[PK_COUNT];  // by value (kernel-argument memory): no host→device copy, capturable
 };
 
+// Split-bf16 (x6) operand images of the weights, built from the fp32 packs after k_prep_weights.
+// X6_CHAIN: A operand of tchain_x6, [step u = kb·nt_out + T][part][lane] uint4 (8 bf16) with
+// element e of lane (i, h) = W[16kb + 8(e>>2) + 4h + (e&3)][32T + i].
+enum X6Id : int { X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A, X6_COUNT };
+struct X6Desc {
+    const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
+    int32_t cols, k4;
+    int32_t nt_out, nkb;
+    int64_t dst;        // uint4 offset into the image buffer
+};
+struct PrepX6Args {
+    uint4* img;
+    X6Desc d[X6_COUNT];
+};
+inline int64_t x6_chain_uint4(int nt_out, int nkb) { return (int64_t)nkb * nt_out * 3 * 64; }
+
 struct EncNodeArgs {
     int n_nodes;
     const float* pos;
@@ -39,6 +55,7 @@ struct EncEdgeArgs {
     const float* pos;
     const int32_t *esrc, *edst, *node_tower, *node_local;
     const float *w_rm0, *b_rm0, *w_rm1, *b_rm1, *w_rm2, *b_rm2, *w_rm3, *b_rm3, *w_w1a, *b_w1a;
+    const uint4 *x_rm1, *x_rm2, *x_rm3, *x_w1a;   // x6 images (math == MATH_X6)
     float *z1, *z2, *z3, *cr, *A;   // chunk-major blocks
     uint32_t* zmask;                // [blk][4 layers: z1,z2,z3,cr][3 words][64 lanes] — activation > 0 bits
     int dropout_on;
@@ -167,7 +184,8 @@ struct AdamArgs {
 // Host launchers (defined next to their kernels; each returns hipGetLastError()).
 hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st);
 hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st);
-hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st);
+hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st);
+hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st);
 hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st);
 hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);

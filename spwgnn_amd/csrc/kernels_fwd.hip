@@ -36,6 +36,29 @@ __global__ void k_prep_weights(PrepArgs a) {
     }
 }
 
+// x6 operand images (kernels.h X6Desc): one thread per (step, lane) splits its 8 weights once.
+__global__ void k_prep_x6(PrepX6Args a) {
+    const X6Desc& d = a.d[blockIdx.y];
+    const int n = d.nkb * d.nt_out * 64;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+        const int lane = idx & 63, u = idx >> 6, kb = u / d.nt_out, T = u - kb * d.nt_out;
+        const int col = 32 * T + (lane & 31), h = lane >> 5;
+        float w[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 16 * kb + 8 * (e >> 2) + 4 * h + (e & 3);
+            w[e] = d.src[d.k4 ? ((k >> 2) * d.cols + col) * 4 + (k & 3) : k * d.cols + col];
+        }
+        uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) split2(w[2 * m], w[2 * m + 1], hw[m], mw[m], lw[m]);
+        uint4* o = a.img + d.dst + (int64_t)u * 3 * 64 + lane;
+        o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        o[64] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+        o[128] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // om encoder: c_o = dropout(relu(om(y, w))), P0, U0 = P0·W1b, V0 = P0·W1c (transposed orientation,
 // 32 nodes per wave).
@@ -55,7 +78,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * t;
-            Z[t][r] = relu(o0 * a.w_om0[f] + o1 * a.w_om0[128 + f] + a.b_om0[f]);
+            Z[t][r] = relu(dense2(o0, o1, a.w_om0[f], a.w_om0[128 + f], a.b_om0[f]));
         }
     const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;   // chunk-major node blocks
     if (a.zo1) store_cm<4>(a.zo1 + bN, Z, lane, valid);
@@ -128,7 +151,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * t;
-            X[t][r] = relu(dx * a.w_rm0[f] + dy * a.w_rm0[160 + f] + a.b_rm0[f]);
+            X[t][r] = relu(dense2(dx, dy, a.w_rm0[f], a.w_rm0[160 + f], a.b_rm0[f]));
         }
     constexpr bool zb = TRAIN;
     uint32_t* const mb = TRAIN ? a.zmask + (int64_t)blk * 4 * 3 * 64 : nullptr;
@@ -174,6 +197,87 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_w1a, lane);
     bias_act_rho<5, false>(X, a.b_w1a, h);
     store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, true);   // chunk-major; k_edge_fwd masks padding edges
+}
+
+// The rm encoder in split-bf16 math: two 32-edge blocks per wave (column tiles c), so each 16-byte
+// weight fragment feeds two MFMAs (the x6 images stream from L2 at half the per-MFMA rate);
+// 1 wave per SIMD (in + out activations: 320 registers).
+template <bool TRAIN, int NC>
+__global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
+    if (blk0 >= a.n_eblocks) return;
+    f32x16 X[NC][5], Y[NC][5];
+    int src[NC], dst[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int blk = blk0 + c;
+        const int64_t e = (int64_t)min(blk, a.n_eblocks - 1) * 32 + j;
+        src[c] = blk < a.n_eblocks ? a.esrc[e] : -1;
+        dst[c] = blk < a.n_eblocks ? a.edst[e] : -1;
+        float dx = 0.f, dy = 0.f;
+        if (src[c] >= 0) {
+            const float4 ps = reinterpret_cast<const float4*>(a.pos)[src[c]];
+            const float4 pd = reinterpret_cast<const float4*>(a.pos)[dst[c]];
+            dx = pd.x - ps.x;  // Networks.py:148-152 (receiver − sender), (x, y)
+            dy = pd.y - ps.y;
+        }
+#pragma unroll
+        for (int t = 0; t < 5; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                X[c][t][r] = relu(dense2(dx, dy, a.w_rm0[f], a.w_rm0[160 + f], a.b_rm0[f]));
+            }
+    }
+    const bool has1 = NC > 1 && blk0 + 1 < a.n_eblocks;
+    auto save = [&](float* base, uint32_t* words, const f32x16 (&Z)[NC][5]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c == 1 && !has1) break;
+            const int blk = blk0 + c;
+            if (base) store_cm<5>(base + (int64_t)blk * kCmBlk, Z[c], lane, true);
+            if (words) store_pos_bits<5>(words + (int64_t)blk * 4 * 3 * 64, Z[c], lane);
+        }
+    };
+    auto zero2 = [&](f32x16 (&Z)[NC][5]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) zero_tiles(Z[c]);
+    };
+    if (TRAIN) save(a.z1, a.zmask, X);
+    zero2(Y);
+    tchain_x6<5, 10, 5, NC>(X, Y, a.x_rm1, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bias_act_rho<5, true>(Y[c], a.b_rm1, h);
+    if (TRAIN) save(a.z2, a.zmask + 3 * 64, Y);
+    zero2(X);
+    tchain_x6<5, 10, 5, NC>(Y, X, a.x_rm2, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bias_act_rho<5, true>(X[c], a.b_rm2, h);
+    if (TRAIN) save(a.z3, a.zmask + 6 * 64, X);
+    zero2(Y);
+    tchain_x6<5, 10, 5, NC>(X, Y, a.x_rm3, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        bias_act_rho<5, true>(Y[c], a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:165
+        if (a.dropout_on && src[c] >= 0) {         // Networks.py:167
+            const uint32_t tw = (uint32_t)a.node_tower[src[c]];
+            const uint32_t key = drop_row_key(a.seed, 1u, tw, (uint32_t)a.node_local[src[c]], (uint32_t)a.node_local[dst[c]]);
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int f = rho(r, 0) + 4 * h + 32 * t;
+                    Y[c][t][r] = drop_keep(key, (uint32_t)f, a.thresh) ? Y[c][t][r] * a.scale : 0.f;
+                }
+        }
+    }
+    if (TRAIN) save(a.cr, a.zmask + 9 * 64, Y);
+    zero2(X);
+    tchain_x6<5, 10, 5, NC>(Y, X, a.x_w1a, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bias_act_rho<5, false>(X[c], a.b_w1a, h);
+    save(a.A, nullptr, X);   // chunk-major; k_edge_fwd masks padding edges
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -490,7 +594,20 @@ hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_enc_node, dim3((waves + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
-hipError_t launch_enc_edge(const EncEdgeArgs& a, hipStream_t st) {
+hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_prep_x6, dim3(16, X6_COUNT), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
+    if (math == MATH_X6) {   // NC blocks per wave, 4 waves per workgroup
+        constexpr int NC = 2;
+        const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
+        if (a.z1)
+            hipLaunchKernelGGL((k_enc_edge_x6<true, NC>), g, dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((k_enc_edge_x6<false, NC>), g, dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (a.z1)
         hipLaunchKernelGGL(k_enc_edge<true>, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
     else
