@@ -74,7 +74,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     w.ps.total = poff;
     w.pk = take(poff);
     {   // x6 images (uint4 = 4 floats each)
-        const int nt_nkb[X6_COUNT][2] = {{5, 10}, {5, 10}, {5, 10}, {5, 10}};
+        const int nt_nkb[X6_COUNT][2] = {{5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}};
         int64_t o = 0;
         for (int id = 0; id < X6_COUNT; ++id) {
             w.x6off[id] = o;
@@ -246,19 +246,24 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     if (r->math == MATH_X6) {
         PrepX6Args xa{};
         xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
-        auto chain = [&](int id, int pid, int nt_out, int nkb) {
+        auto img = [&](int id, int pid, int nt_out, int nkb, int kh) {
             X6Desc& d = xa.d[id];
             d.src = c.pk(pid);
             d.cols = pack_cols(pid);
             d.k4 = pa.desc[pid].k4;
             d.nt_out = nt_out;
             d.nkb = nkb;
+            d.kh = kh;
             d.dst = w.x6off[id];
         };
-        chain(X6_RM1, PK_RM1, 5, 10);
-        chain(X6_RM2, PK_RM2, 5, 10);
-        chain(X6_RM3, PK_RM3, 5, 10);
-        chain(X6_W1A, PK_W1A, 5, 10);
+        img(X6_RM1, PK_RM1, 5, 10, 0);
+        img(X6_RM2, PK_RM2, 5, 10, 0);
+        img(X6_RM3, PK_RM3, 5, 10, 0);
+        img(X6_W1A, PK_W1A, 5, 10, 0);
+        img(X6_W1AT, PK_W1AT, 5, 10, kKhE);
+        img(X6_RM3T, PK_RM3T, 5, 10, 0);
+        img(X6_RM2T, PK_RM2T, 5, 10, 0);
+        img(X6_RM1T, PK_RM1T, 5, 10, 0);
         SPW_CHECK(launch_prep_x6(xa, st));
     }
     // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
@@ -543,13 +548,19 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     eeb.rm3t = c.pk(PK_RM3T);
     eeb.rm2t = c.pk(PK_RM2T);
     eeb.rm1t = c.pk(PK_RM1T);
+    if (r->math == MATH_X6) {
+        eeb.x_w1at = c.x6(X6_W1AT);
+        eeb.x_rm3t = c.x6(X6_RM3T);
+        eeb.x_rm2t = c.x6(X6_RM2T);
+        eeb.x_rm1t = c.x6(X6_RM1T);
+    }
     eeb.dz4 = c.f(w.dz4);
     eeb.dz3 = c.f(w.dz3);
     eeb.dz2 = c.f(w.dz2);
     eeb.dz1 = c.f(w.dz1);
     eeb.scale = scale;
     SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
-    SPW_CHECK(launch_enc_edge_bwd(eeb, st));
+    SPW_CHECK(launch_enc_edge_bwd(eeb, r->math, st));
     SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
 
     EncNodeBwdArgs enb{};

@@ -311,17 +311,14 @@ __device__ __forceinline__ void bias_act_rho(f32x16 (&X)[NT], const float* __res
 }
 
 // ---- transposed orientation in split-bf16 math (x6), NC column tiles of 32 rows per wave:
-// out[c][T] += Wᵀ·in[c]. k-block kb (16 input features) of tile t = kb>>1 is registers
-// 8(kb&1) .. 8(kb&1)+7 of in[c][t]: element e of lane half h = feature 16kb + 8(e>>2) + 4h + (e&3)
-// (the C layout read as a 32x32x16 B operand), split into three bf16 parts once per layer.
-// The weight image (k_prep_x6, X6_CHAIN) holds, per step u = kb·NT_OUT + T, the three A-operand
-// parts of lane (i, h): W[that feature][32T + i], 16 bytes each: [u][part][lane] uint4.
-// Steps stream through a D-deep ring of static slots (fully unrolled; the loads of step u + D
-// issue before step u's MFMAs).
-template <int NT_OUT, int NKB, int NT_IN, int NC, int D = 3>
-__device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
-                                          const uint4* __restrict__ img, int lane) {
-    static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");
+// out[c][T] += Wᵀ·B[c] over NKB k-blocks of 16. getb(c, kb, v) supplies the 8 fp32 B values of
+// lane (j, h) for k-block kb (split into three bf16 parts here, once per k-block); the weight image
+// (k_prep_x6) holds, per step u = kb·NT_OUT + T, the three matching A-operand parts of lane (i, h),
+// 16 bytes each: [u][part][lane] uint4. Steps stream through a D-deep ring of static slots (fully
+// unrolled; the loads of step u + D issue before step u's MFMAs).
+template <int NT_OUT, int NKB, int NC, int D = 3, class GetB>
+__device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
+                                         int lane) {
     constexpr int NS = NKB * NT_OUT;
     const uint4* wb = img + lane;
     uint4 ring[D][3];
@@ -336,10 +333,11 @@ __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 
         if (T == 0) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
+                float v[8];
+                getb(c, kb, v);
                 uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    split2(in[c][kb >> 1][8 * (kb & 1) + 2 * m], in[c][kb >> 1][8 * (kb & 1) + 2 * m + 1], hw[m], mw[m], lw[m]);
+                for (int m = 0; m < 4; ++m) split2(v[2 * m], v[2 * m + 1], hw[m], mw[m], lw[m]);
                 bq[c][0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
                 bq[c][1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
                 bq[c][2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
@@ -356,6 +354,20 @@ __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 
 #pragma unroll
         for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6(a, bq[c], out[c][T]);
     }
+}
+// Chain layer: B = the C layout of the previous layer; k-block kb of tile t = kb>>1 is registers
+// 8(kb&1) .. +7 of in[c][t] (element e of lane half h = feature 16kb + 8(e>>2) + 4h + (e&3): image
+// kind X6_CHAIN).
+template <int NT_OUT, int NKB, int NT_IN, int NC, int D = 3>
+__device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
+                                          const uint4* __restrict__ img, int lane) {
+    static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");
+    tgemm_x6<NT_OUT, NKB, NC, D>(
+        [&](int c, int kb, float (&v)[8]) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = in[c][kb >> 1][8 * (kb & 1) + e];
+        },
+        out, img, lane);
 }
 
 }  // namespace spw

@@ -21,13 +21,16 @@ struct PrepArgs {
 };
 
 // Split-bf16 (x6) operand images of the weights, built from the fp32 packs after k_prep_weights.
-// X6_CHAIN: A operand of tchain_x6, [step u = kb·nt_out + T][part][lane] uint4 (8 bf16) with
-// element e of lane (i, h) = W[16kb + 8(e>>2) + 4h + (e&3)][32T + i].
-enum X6Id : int { X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A, X6_COUNT };
+// Transposed-orientation A operands of tgemm_x6: [step u = kb·nt_out + T][part][lane] uint4 (8 bf16),
+// element e of lane (i, h) = W[k(kb, e, h)][32T + i] with
+//   kh == 0 (chain: B is a C layout)          k = 16kb + 8(e>>2) + 4h + (e&3)
+//   kh > 0  (half rows: lane half h holds features kh·h ..)  k = kh·h + 8kb + e, zero if 8kb + e ≥ kh
+enum X6Id : int { X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A, X6_W1AT, X6_RM3T, X6_RM2T, X6_RM1T, X6_COUNT };
 struct X6Desc {
     const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
     int32_t cols, k4;
     int32_t nt_out, nkb;
+    int32_t kh, pad0;
     int64_t dst;        // uint4 offset into the image buffer
 };
 struct PrepX6Args {
@@ -109,6 +112,7 @@ struct EncEdgeBwdArgs {
     const float* dA;                // row-major [e][160] (accumulated by k_edge_bwd)
     const uint32_t* zmask;          // from k_enc_edge
     const float *w1at, *rm3t, *rm2t, *rm1t;
+    const uint4 *x_w1at, *x_rm3t, *x_rm2t, *x_rm1t;   // x6 images (math == MATH_X6)
     float *dz4, *dz3, *dz2, *dz1;
     float scale;   // dropout 1/(1-p) (1 when off)
 };
@@ -190,7 +194,7 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st);
 hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st);
 hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st);
-hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st);
+hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);

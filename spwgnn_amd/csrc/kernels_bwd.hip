@@ -370,6 +370,70 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     (void)h;
 }
 
+// The same backward chain in split-bf16 math: two 32-edge column tiles per wave (kernels_fwd.hip
+// k_enc_edge_x6). dA rows (row-major) are loaded whole up front as half rows (lane half h: features
+// 76h .. 76h+75, image kind kh = 76), into the registers the second layer's output uses later.
+template <int NC>
+__global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
+    if (blk0 >= a.n_eblocks) return;
+    f32x16 D[NC][5], E[NC][5];
+    {
+        float4 raw[NC][kKhE / 4];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int64_t e = (int64_t)min(blk0 + c, a.n_eblocks - 1) * 32 + j;
+            const float4* row = reinterpret_cast<const float4*>(a.dA + e * kLdE + kKhE * h);
+#pragma unroll
+            for (int q = 0; q < kKhE / 4; ++q) raw[c][q] = row[q];
+            zero_tiles(D[c]);
+        }
+        tgemm_x6<5, (kKhE + 7) / 8, NC>(
+            [&](int c, int kb, float (&v)[8]) {
+                const float4 x = raw[c][2 * kb];
+                const float4 y = 2 * kb + 1 < kKhE / 4 ? raw[c][2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+                v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+            },
+            D, a.x_w1at, lane);   // dc_r = dA·W1aᵀ
+    }
+    const bool has1 = NC > 1 && blk0 + 1 < a.n_eblocks;
+    auto save = [&](float* base, const f32x16 (&Z)[NC][5]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c == 1 && !has1) break;
+            store_cm<5>(base + (int64_t)(blk0 + c) * kCmBlk, Z[c], lane, true);
+        }
+    };
+    auto bits = [&](int layer, f32x16 (&Z)[NC][5], float scale) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int blk = min(blk0 + c, a.n_eblocks - 1);
+            apply_pos_bits<5>(a.zmask + (int64_t)blk * 4 * 3 * 64 + layer * 3 * 64, Z[c], lane, scale);
+        }
+    };
+    auto zero2 = [&](f32x16 (&Z)[NC][5]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) zero_tiles(Z[c]);
+    };
+    bits(3, D, a.scale);   // relu + dropout of c_r
+    save(a.dz4, D);
+    zero2(E);
+    tchain_x6<5, 10, 5, NC>(D, E, a.x_rm3t, lane);
+    bits(2, E, 1.f);
+    save(a.dz3, E);
+    zero2(D);
+    tchain_x6<5, 10, 5, NC>(E, D, a.x_rm2t, lane);
+    bits(1, D, 1.f);
+    save(a.dz2, D);
+    zero2(E);
+    tchain_x6<5, 10, 5, NC>(D, E, a.x_rm1t, lane);
+    bits(0, E, 1.f);
+    save(a.dz1, E);
+    (void)h;
+}
+
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_enc_node_bwd(EncNodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -416,7 +480,12 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st) {
     }
     return hipGetLastError();
 }
-hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, hipStream_t st) {
+hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st) {
+    if (math == MATH_X6) {
+        constexpr int NC = 2;
+        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC>), dim3((a.n_eblocks + 4 * NC - 1) / (4 * NC)), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_enc_edge_bwd, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }

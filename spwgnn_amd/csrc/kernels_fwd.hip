@@ -46,8 +46,9 @@ __global__ void k_prep_x6(PrepX6Args a) {
         float w[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int k = 16 * kb + 8 * (e >> 2) + 4 * h + (e & 3);
-            w[e] = d.src[d.k4 ? ((k >> 2) * d.cols + col) * 4 + (k & 3) : k * d.cols + col];
+            const int k = d.kh ? d.kh * h + 8 * kb + e : 16 * kb + 8 * (e >> 2) + 4 * h + (e & 3);
+            const bool in = !d.kh || 8 * kb + e < d.kh;
+            w[e] = in ? d.src[d.k4 ? ((k >> 2) * d.cols + col) * 4 + (k & 3) : k * d.cols + col] : 0.f;
         }
         uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
