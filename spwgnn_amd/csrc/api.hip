@@ -74,7 +74,8 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     w.ps.total = poff;
     w.pk = take(poff);
     {   // x6 images (uint4 = 4 floats each)
-        const int nt_nkb[X6_COUNT][2] = {{5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}};
+        const int nt_nkb[X6_COUNT][2] = {{5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10},
+                                         {5, 10}, {5, 10}};
         int64_t o = 0;
         for (int id = 0; id < X6_COUNT; ++id) {
             w.x6off[id] = o;
@@ -264,6 +265,8 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         img(X6_RM3T, PK_RM3T, 5, 10, 0);
         img(X6_RM2T, PK_RM2T, 5, 10, 0);
         img(X6_RM1T, PK_RM1T, 5, 10, 0);
+        img(X6_W2, PK_W2, 5, 10, kKhE);     // edge-side B operands (LDS images)
+        img(X6_W2T, PK_W2T, 5, 10, kKhE);
         SPW_CHECK(launch_prep_x6(xa, st));
     }
     // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
@@ -354,12 +357,13 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.V = c.f(w.V_at(s));
         ef.w2 = c.pk(PK_W2);
         ef.b2 = c.pk(PB_W2);
+        ef.x_w2 = r->math == MATH_X6 ? c.x6(X6_W2) : nullptr;
         ef.H2s = c.f(w.H2s_at(s));
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
-        SPW_CHECK(launch_edge_fwd(ef, st));
+        SPW_CHECK(launch_edge_fwd(ef, r->math, st));
         SPW_CHECK(prof.after(SPWGNN_K_EDGE_FWD));
 
         NodeFwdArgs nf{};

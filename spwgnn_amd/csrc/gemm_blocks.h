@@ -310,45 +310,55 @@ __device__ __forceinline__ void bias_act_rho(f32x16 (&X)[NT], const float* __res
         }
 }
 
+constexpr int kX6Ring = 3;
+constexpr int kEdgeWavesX6 = 4;   // edge kernels in x6 math: one wave per SIMD   // weight-fragment steps in flight (tgemm_x6)
+
 // ---- transposed orientation in split-bf16 math (x6), NC column tiles of 32 rows per wave:
 // out[c][T] += Wᵀ·B[c] over NKB k-blocks of 16. getb(c, kb, v) supplies the 8 fp32 B values of
 // lane (j, h) for k-block kb (split into three bf16 parts here, once per k-block); the weight image
 // (k_prep_x6) holds, per step u = kb·NT_OUT + T, the three matching A-operand parts of lane (i, h),
 // 16 bytes each: [u][part][lane] uint4. Steps stream through a D-deep ring of static slots (fully
 // unrolled; the loads of step u + D issue before step u's MFMAs).
-template <int NT_OUT, int NKB, int NC, int D = 3, class GetB>
+template <int NT_OUT, int NKB, int NC, int D = kX6Ring, class GetB>
 __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
                                          int lane) {
-    constexpr int NS = NKB * NT_OUT;
+    constexpr int NS = NKB * NT_OUT, NP = 4 * NC;   // pair-splits per k-block
     const uint4* wb = img + lane;
     uint4 ring[D][3];
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
         for (int p = 0; p < 3; ++p) ring[d][p] = wb[(d * 3 + p) * 64];
-    bf16x8 bq[NC][3];
+    // split parts of k-block kb in slot kb & 1; the next k-block's pair-splits are spread over
+    // this k-block's steps, so the VALU work interleaves with the MFMAs
+    uint32_t sp[2][NC][3][4];
+    auto split_pair = [&](int kb, int q) {
+        const int c = q >> 2, m = q & 3;
+        float v[8];
+        getb(c, kb, v);
+        split2(v[2 * m], v[2 * m + 1], sp[kb & 1][c][0][m], sp[kb & 1][c][1][m], sp[kb & 1][c][2][m]);
+    };
+#pragma unroll
+    for (int q = 0; q < NP; ++q) split_pair(0, q);
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
         const int kb = u / NT_OUT, T = u - kb * NT_OUT;
-        if (T == 0) {
+        bf16x8 bq[NC][3];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                float v[8];
-                getb(c, kb, v);
-                uint32_t hw[4], mw[4], lw[4];
+        for (int c = 0; c < NC; ++c)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) split2(v[2 * m], v[2 * m + 1], hw[m], mw[m], lw[m]);
-                bq[c][0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
-                bq[c][1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
-                bq[c][2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
-            }
-        }
+            for (int p = 0; p < 3; ++p)
+                bq[c][p] = as_bf16x8(make_uint4(sp[kb & 1][c][p][0], sp[kb & 1][c][p][1], sp[kb & 1][c][p][2], sp[kb & 1][c][p][3]));
         bf16x8 a[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = as_bf16x8(ring[u % D][p]);
         if (u + D < NS) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) ring[u % D][p] = wb[((u + D) * 3 + p) * 64];
+        }
+        if (kb + 1 < NKB) {
+#pragma unroll
+            for (int q = NP * T / NT_OUT; q < NP * (T + 1) / NT_OUT; ++q) split_pair(kb + 1, q);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -358,7 +368,7 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
 // Chain layer: B = the C layout of the previous layer; k-block kb of tile t = kb>>1 is registers
 // 8(kb&1) .. +7 of in[c][t] (element e of lane half h = feature 16kb + 8(e>>2) + 4h + (e&3): image
 // kind X6_CHAIN).
-template <int NT_OUT, int NKB, int NT_IN, int NC, int D = 3>
+template <int NT_OUT, int NKB, int NT_IN, int NC, int D = kX6Ring>
 __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
                                           const uint4* __restrict__ img, int lane) {
     static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");

@@ -25,7 +25,7 @@ struct PrepArgs {
 // element e of lane (i, h) = W[k(kb, e, h)][32T + i] with
 //   kh == 0 (chain: B is a C layout)          k = 16kb + 8(e>>2) + 4h + (e&3)
 //   kh > 0  (half rows: lane half h holds features kh·h ..)  k = kh·h + 8kb + e, zero if 8kb + e ≥ kh
-enum X6Id : int { X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A, X6_W1AT, X6_RM3T, X6_RM2T, X6_RM1T, X6_COUNT };
+enum X6Id : int { X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A, X6_W1AT, X6_RM3T, X6_RM2T, X6_RM1T, X6_W2, X6_W2T, X6_COUNT };
 struct X6Desc {
     const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
     int32_t cols, k4;
@@ -75,6 +75,7 @@ struct EdgeFwdArgs {
     float* H2s;
     uint32_t *mask1, *mask2;
     float* h1_out;     // training: h1 rows, chunk-major blocks (kCmBlk), for the W2 gradient
+    const uint4* x_w2; // x6 image of W2 (half rows, kh 76) — the LDS B operand (math == MATH_X6)
 };
 
 struct NodeFwdArgs {
@@ -190,7 +191,7 @@ hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st);
 hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st);
 hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st);
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st);
-hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st);
+hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st);
 hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st);
@@ -206,7 +207,7 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
 // persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)
-int edge_grid(int n_wtiles);
+int edge_grid(int n_wtiles, int waves = kEdgeWaves);
 inline size_t edge_fwd_lds_per_wave(int nw_max) { return (size_t)(2112 + nw_max * kLdE) * 4; }
 inline size_t edge_bwd_lds_per_wave(int nw_max) { return (size_t)(2112 + 2 * nw_max * kLdE) * 4; }
 inline int edge_wpg(size_t lds_per_wave) {

@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
             for (int q = 0; q < kKhE / 4; ++q) raw[c][q] = row[q];
             zero_tiles(D[c]);
         }
-        tgemm_x6<5, (kKhE + 7) / 8, NC>(
+        tgemm_x6<5, (kKhE + 7) / 8, NC, 6>(
             [&](int c, int kb, float (&v)[8]) {
                 const float4 x = raw[c][2 * kb];
                 const float4 y = 2 * kb + 1 < kKhE / 4 ? raw[c][2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -420,15 +420,15 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
     bits(3, D, a.scale);   // relu + dropout of c_r
     save(a.dz4, D);
     zero2(E);
-    tchain_x6<5, 10, 5, NC>(D, E, a.x_rm3t, lane);
+    tchain_x6<5, 10, 5, NC, 6>(D, E, a.x_rm3t, lane);
     bits(2, E, 1.f);
     save(a.dz3, E);
     zero2(D);
-    tchain_x6<5, 10, 5, NC>(E, D, a.x_rm2t, lane);
+    tchain_x6<5, 10, 5, NC, 6>(E, D, a.x_rm2t, lane);
     bits(1, D, 1.f);
     save(a.dz2, D);
     zero2(E);
-    tchain_x6<5, 10, 5, NC>(D, E, a.x_rm1t, lane);
+    tchain_x6<5, 10, 5, NC, 6>(D, E, a.x_rm1t, lane);
     bits(0, E, 1.f);
     save(a.dz1, E);
     (void)h;

@@ -574,7 +574,217 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 // ------------------------------------------------------------------------------------------------
-int edge_grid(int n_wtiles) {
+// ------------------------------------------------------------------------------------------------
+// One propagation step, edge side, in split-bf16 math (x6). Natural orientation as k_edge_fwd:
+// lane (i, h) of a block holds edge i, features 76h + 8kb + e of k-block kb (two 4-feature chunks
+// of the chunk-major A/U/V rows), so h1 = relu(A + U[s] + V[r]) is built, split and used as the A
+// operand straight from the loads; W2 (x6 image, 150 KB) is the LDS B operand. The receiver sum
+// runs as one-hot [node][edge] (exact in bf16) × h2 parts: 3 MFMAs per 16 edges per feature tile.
+// 4 waves (one per SIMD: 512 registers) per CU, A/U/V prefetched kX6Pf k-blocks ahead.
+struct NodeSumX6 {
+    f32x16 acc[5];
+    int key;
+    __device__ __forceinline__ void init(int n0, int lane) {
+        key = n0 + (lane & 31);
+        zero_tiles(acc);
+    }
+    // h2: C layout (reg r of lane (j, h) = edge rho(r, h), feature 32t + j); d: this lane's edge's receiver
+    __device__ __forceinline__ void add(const f32x16 (&h2)[5], int d, int h) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            // A[node i][edge k], element e of half h ↔ edge 16s + 8(e>>2) + 4h + (e&3) = rho(8s+e, h)
+            uint32_t oh[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                uint32_t w = 0u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int e = 2 * m + q;
+                    const int d0 = __builtin_amdgcn_readlane(d, rho(8 * s + e, 0));
+                    const int d1 = __builtin_amdgcn_readlane(d, rho(8 * s + e, 1));
+                    w |= ((h ? d1 : d0) == key ? 0x3F80u : 0u) << (16 * q);
+                }
+                oh[m] = w;
+            }
+            bf16x8 a[1];
+            a[0] = as_bf16x8(make_uint4(oh[0], oh[1], oh[2], oh[3]));
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+                uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) split2(h2[t][8 * s + 2 * m], h2[t][8 * s + 2 * m + 1], hw[m], mw[m], lw[m]);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3])), acc[t], 0, 0, 0);
+            }
+        }
+    }
+    // reg r of tile t: node rho(r, h), feature 32t + (lane&31)
+    __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
+        const int h = lane >> 5;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int node = rho(r, h);
+            if (node < nn) {
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                    const int f = 32 * t + (lane & 31);
+                    if (f < 2 * kKhE) H2s[cm_index<kKhE>(n0 + node, f)] = acc[t][r];
+                }
+            }
+        }
+    }
+};
+
+constexpr int kX6Pf = 5;   // A/U/V k-blocks in flight (edge_fwd x6); divides the 10 k-blocks
+
+__global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_fwd_x6(EdgeFwdArgs a) {
+    static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
+    __shared__ uint4 wl[50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
+    for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
+    const int wstep = gridDim.x * kEdgeWavesX6;
+    const uint4* wlp = wl + lane;
+    auto load_sd = [&](int blk) { return make_int2(a.esrc[(int64_t)blk * 32 + i], a.edst[(int64_t)blk * 32 + i]); };
+    // a block's h1 operand sources: A rows and the gathered U[s], V[r] rows (chunk q at +256q / +64q)
+    struct Src { const float* A; const float4 *U, *V; };
+    auto src_of = [&](int blk, int2 sd, int n0) {
+        const int sc = sd.x >= 0 ? sd.x : n0, dc = sd.x >= 0 ? sd.y : n0;
+        return Src{a.A + (int64_t)blk * kCmBlk + h * 128 + i * 4,
+                   reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128),
+                   reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128)};
+    };
+    // k-block kb = chunks 2kb, 2kb+1 (chunk 19 does not exist: clamped, its W2 rows are zero)
+    struct KB { float4 a[2], u[2], v[2]; };
+    auto ld = [&](const Src& sr, int kb, KB& r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int q = min(2 * kb + c, kKhE / 4 - 1);
+            r.a[c] = *reinterpret_cast<const float4*>(sr.A + 256 * q);
+            r.u[c] = sr.U[64 * q];
+            r.v[c] = sr.V[64 * q];
+        }
+    };
+    int wt = blockIdx.x * kEdgeWavesX6 + wave;
+    if (wt >= a.n_wtiles) return;
+    int4 info = wtiles[wt];
+    // the first block's sources and its first kX6Pf k-blocks; later blocks' arrive during the
+    // previous block (the ring carries over)
+    int2 cur_sd = load_sd(info.x);
+    Src cur = src_of(info.x, cur_sd, info.z);
+    KB ring[kX6Pf];
+#pragma unroll
+    for (int k = 0; k < kX6Pf; ++k) ld(cur, k, ring[k]);
+    for (; wt < a.n_wtiles; wt += wstep) {
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];
+    NodeSumX6 nsum;
+    nsum.init(n0, lane);
+    for (int bb = 0; bb < nb; ++bb) {
+        const int blk = fb + bb;
+        const int nblk = bb + 1 < nb ? blk + 1 : ninfo.x;   // the next block (clamped at the end)
+        const int nn0 = bb + 1 < nb ? n0 : ninfo.z;
+        const int2 nsd = load_sd(nblk);
+        const int s = cur_sd.x, d = cur_sd.y;
+        const bool valid = s >= 0;
+        const uint64_t vmask = __ballot(valid);
+        const float vf = valid ? 1.f : 0.f;
+        uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
+        const int m1off = lane < 4 ? lane : kKhE + lane - 4;
+        Src nxt;
+        f32x16 acc[5];
+        zero_tiles(acc);
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % kX6Pf];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
+                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
+                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
+                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
+            }
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            if (kb + kX6Pf < 10) {
+                ld(cur, kb + kX6Pf, cr);
+            } else {
+                if (kb + kX6Pf == 10) nxt = src_of(nblk, nsd, nn0);
+                ld(nxt, kb + kX6Pf - 10, cr);
+            }
+            bf16x8 ap[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+            if (mrow) {   // h1 > 0 bits of the block's real chunks
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int q = 2 * kb + c;
+                    if (q < kKhE / 4) {
+                        uint32_t stg = 0u;
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) {
+                            const uint64_t bal = __ballot(xv[4 * c + f] > 0.f);
+                            stg = writelane_imm((uint32_t)bal, f, stg);
+                            stg = writelane_imm((uint32_t)(bal >> 32), 4 + f, stg);
+                        }
+                        if (lane < 8) mrow[m1off + 4 * q] = stg;
+                    }
+                }
+            }
+#pragma unroll
+            for (int T = 0; T < 5; ++T) {
+                const uint4* wp = wlp + (kb * 5 + T) * 3 * 64;
+                bf16x8 bp[3];
+                bp[0] = as_bf16x8(wp[0]);
+                bp[1] = as_bf16x8(wp[64]);
+                bp[2] = as_bf16x8(wp[128]);
+                acc[T] = mfma32_x6(ap, bp, acc[T]);
+            }
+        }
+        if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const float b = a.b2[32 * t + i];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = relu(acc[t][r] + b);
+                if (t == 4 && i == kDegCol - 128) v = 1.f;  // degree column (multiplies b3)
+                const bool rv = (vmask >> (rho(r, 0) + 4 * h)) & 1;
+                acc[t][r] = rv ? v : 0.f;
+            }
+        }
+        if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
+            uint32_t* m2row = a.mask2 + (int64_t)blk * 160;
+            uint32_t mw2[3] = {0u, 0u, 0u};
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint64_t bal = __ballot(acc[t][r] > 0.f);
+                    const int w0 = t * 32 + rho(r, 0), w1 = t * 32 + rho(r, 1);
+                    mw2[w0 >> 6] = writelane_imm((uint32_t)bal, w0 & 63, mw2[w0 >> 6]);
+                    mw2[w1 >> 6] = writelane_imm((uint32_t)(bal >> 32), w1 & 63, mw2[w1 >> 6]);
+                }
+            m2row[lane] = mw2[0];
+            m2row[64 + lane] = mw2[1];
+            if (lane < 32) m2row[128 + lane] = mw2[2];
+        }
+        nsum.add(acc, d, h);
+        cur_sd = nsd;
+        cur = nxt;
+    }
+    nsum.store(a.H2s, n0, nn, lane);
+    info = ninfo;
+    }
+}
+
+int edge_grid(int n_wtiles, int waves) {
     static int cus = 0;  // compute units of the device (all devices of a node are alike)
     if (cus <= 0) {
         int dev = 0, v = 0;
@@ -582,7 +792,7 @@ int edge_grid(int n_wtiles) {
             v = 256;
         cus = v;
     }
-    const int need = (n_wtiles + kEdgeWaves - 1) / kEdgeWaves;
+    const int need = (n_wtiles + waves - 1) / waves;
     return need < 1 ? 1 : (need < cus ? need : cus);
 }
 
@@ -615,8 +825,12 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
         hipLaunchKernelGGL(k_enc_edge<false>, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
-hipError_t launch_edge_fwd(const EdgeFwdArgs& a, hipStream_t st) {
+hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
+    if (math == MATH_X6) {
+        hipLaunchKernelGGL(k_edge_fwd_x6, dim3(edge_grid(a.n_wtiles, kEdgeWavesX6)), dim3(64 * kEdgeWavesX6), 0, st, a);
+        return hipGetLastError();
+    }
     if (a.nw_max <= 16)
         hipLaunchKernelGGL(k_edge_fwd<true>, dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
     else

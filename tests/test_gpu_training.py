@@ -94,16 +94,19 @@ def test_bitwise_deterministic():
         assert np.array_equal(a[2][k], b[2][k]), k
 
 
-def test_full_size_towers_are_independent():
+@pytest.mark.parametrize("math", ["f32", "x6"])
+def test_full_size_towers_are_independent(math):
     """B = 65,536 towers (the bench config): every tower's logits equal the oracle on that tower
-    alone (sampled), and are identical to a run of the same tower in a small batch."""
+    alone (sampled), and match a run of the same tower in a small batch — bit-identical in f32
+    math; in x6 math the receiver sums add a node's messages in 16-edge k-blocks whose grouping
+    follows the tower's position, so the two runs agree to rounding."""
     B, N, S = 65536, 6, 5
     params = O.random_params(6)
     raw = D.synthetic_towers(B, N, seed=17)
     obj = (raw / 170).astype(np.float32)
     big = TowerBatch.fully_connected(obj, device="cuda")
     flat = P.to_flat(params, device="cuda")
-    z = E.forward(flat, big, E.RunConfig(S), E.Workspace("cuda")).cpu().numpy().reshape(B, N)
+    z = E.forward(flat, big, E.RunConfig(S, math=math), E.Workspace("cuda")).cpu().numpy().reshape(B, N)
     pick = np.random.default_rng(0).choice(B, 24, replace=False)
     Rs, Rr = O.relation_matrices(raw[pick], None)
     tp = O.to_torch(params)
@@ -111,8 +114,11 @@ def test_full_size_towers_are_independent():
                           torch.tensor(Rr, dtype=torch.float64), torch.zeros(24, N, 100, dtype=torch.float64), S).numpy()
     assert np.all(np.abs(z[pick] - ref) <= 1e-5 + 1e-5 * np.abs(ref))
     small = TowerBatch.fully_connected(obj[pick], device="cuda")
-    zs = E.forward(flat, small, E.RunConfig(S), E.Workspace("cuda")).cpu().numpy().reshape(24, N)
-    assert np.array_equal(zs, z[pick])
+    zs = E.forward(flat, small, E.RunConfig(S, math=math), E.Workspace("cuda")).cpu().numpy().reshape(24, N)
+    if math == "f32":
+        assert np.array_equal(zs, z[pick])
+    else:
+        assert np.all(np.abs(zs - z[pick]) <= 2e-6 + 2e-6 * np.abs(z[pick])), np.abs(zs - z[pick]).max()
 
 
 def test_gradient_linearity_over_shards():
