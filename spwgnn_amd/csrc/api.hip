@@ -524,11 +524,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.dh2_out = nullptr;  // the W2 gradient recomputes dh2pre (YM_DH2)
         eb.G3 = c.f(w.G3_at(s));
         eb.w2t = c.pk(PK_W2T);
+        eb.x_w2t = r->math == MATH_X6 ? c.x6(X6_W2T) : nullptr;
         eb.dA = c.f(w.dA);
         eb.dU = c.f(w.dU_at(s));
         eb.dV = c.f(w.dV_at(s));
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_BWD));
-        SPW_CHECK(launch_edge_bwd(eb, st));
+        SPW_CHECK(launch_edge_bwd(eb, r->math, st));
         SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
     }
     if (dprop) {

@@ -106,6 +106,7 @@ struct EdgeBwdArgs {
     const float *G3, *w2t;
     float *dA, *dU, *dV;
     float* dh2_out;    // dh2pre rows, chunk-major blocks (kCmBlk), for the W2 gradient
+    const uint4* x_w2t; // x6 image of W2ᵀ (half rows, kh 76) — the LDS B operand (math == MATH_X6)
 };
 
 struct EncEdgeBwdArgs {
@@ -194,7 +195,7 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st);
 hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);
-hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st);
+hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.h)

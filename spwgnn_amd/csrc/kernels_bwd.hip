@@ -465,7 +465,188 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_node_bwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
-hipError_t launch_edge_bwd(const EdgeBwdArgs& a, hipStream_t st) {
+// One propagation step, edge side, backward, in split-bf16 math (x6; wave-tiles of ≤ 16 nodes).
+// As k_edge_fwd_x6: lane (i, h) holds edge i, features 76h + 8kb + e of k-block kb; the A operand
+// is dh2pre = G3[receiver] ⊙ [h2 > 0] built from the G3 loads, W2ᵀ (x6 image) is the LDS B operand.
+// dh1pre = dh1 ⊙ [h1 > 0] goes to dA (plain stores on the first backward step, atomics after)
+// and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
+// 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
+template <bool ACCUM>
+__global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_bwd_x6(EdgeBwdArgs a) {
+    constexpr int PF = 5;
+    __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
+    for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2t[idx];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
+    const int wstep = gridDim.x * kEdgeWavesX6;
+    const uint4* wlp = wl + lane;
+    struct Pre { int d, s; uint32_t w[5]; };
+    auto load_pre = [&](int blk) {
+        Pre p;
+        const int64_t e = (int64_t)blk * 32 + i;
+        p.d = a.edst[e];
+        p.s = a.esrc[e];
+        const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) p.w[t] = m2[32 * t];
+        return p;
+    };
+    auto g_of = [&](int d, int n0) {
+        return reinterpret_cast<const float4*>(a.G3 + cm_index<kKhE>(d >= 0 ? d : n0, 0) + h * 128);
+    };
+    struct KB { float4 g[2]; };
+    auto ld = [&](const float4* G4, int kb, KB& r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
+    };
+    int wt = blockIdx.x * kEdgeWavesX6 + wave;
+    if (wt >= a.n_wtiles) return;
+    int4 info = wtiles[wt];
+    Pre cur = load_pre(info.x);
+    const float4* G4 = g_of(cur.d, info.z);
+    KB ring[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) ld(G4, k, ring[k]);
+    for (; wt < a.n_wtiles; wt += wstep) {
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];
+    const int key = i < 16 ? n0 + i : n0 + i - 16;   // one-hot rows: receivers, then senders
+    f32x16 nacc[5];
+    zero_tiles(nacc);
+    for (int bb = 0; bb < nb; ++bb) {
+        const int blk = fb + bb;
+        const int nblk = bb + 1 < nb ? blk + 1 : ninfo.x;
+        const int nn0 = bb + 1 < nb ? n0 : ninfo.z;
+        const Pre nxt = load_pre(nblk);
+        const int d = cur.d;
+        const bool valid = d >= 0;
+        const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
+        uint32_t m1w[5];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) m1w[t] = m1[32 * t];
+        uint32_t w[5];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) w[t] = valid ? cur.w[t] : 0u;
+        // this lane's 76 feature bits (features 76h + 0..75): a 64-bit low part and a 12-bit tail
+        const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
+                                    : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
+        const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
+        const float4* NG4 = nullptr;
+        f32x16 acc[5];
+        zero_tiles(acc);
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % PF];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int q = 2 * kb + c;
+                const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
+                xv[4 * c + 0] = (bits & 1u) ? cr.g[c].x : 0.f;
+                xv[4 * c + 1] = (bits & 2u) ? cr.g[c].y : 0.f;
+                xv[4 * c + 2] = (bits & 4u) ? cr.g[c].z : 0.f;
+                xv[4 * c + 3] = (bits & 8u) ? cr.g[c].w : 0.f;
+            }
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            if (kb + PF < 10) {
+                ld(G4, kb + PF, cr);
+            } else {
+                if (kb + PF == 10) NG4 = g_of(nxt.d, nn0);
+                ld(NG4, kb + PF - 10, cr);
+            }
+            bf16x8 ap[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+            for (int T = 0; T < 5; ++T) {
+                const uint4* wp = wlp + (kb * 5 + T) * 3 * 64;
+                bf16x8 bp[3];
+                bp[0] = as_bf16x8(wp[0]);
+                bp[1] = as_bf16x8(wp[64]);
+                bp[2] = as_bf16x8(wp[128]);
+                acc[T] = mfma32_x6(ap, bp, acc[T]);
+            }
+            __builtin_amdgcn_sched_barrier(0);   // no motion across k-blocks (register pressure)
+        }
+        // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const uint32_t mw1 = m1w[t];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = ((mw1 >> rho(r, h)) & 1u) ? acc[t][r] : 0.f;
+        }
+        float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
+        // one-hot [node row][edge]: element e of half h ↔ edge rho(8s + e, h)
+        const int s_ = cur.s;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            uint32_t oh[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                uint32_t wv = 0u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int e = 2 * m + q;
+                    const int d0 = __builtin_amdgcn_readlane(d, rho(8 * s + e, 0));
+                    const int d1 = __builtin_amdgcn_readlane(d, rho(8 * s + e, 1));
+                    const int s0 = __builtin_amdgcn_readlane(s_, rho(8 * s + e, 0));
+                    const int s1 = __builtin_amdgcn_readlane(s_, rho(8 * s + e, 1));
+                    const int node = i < 16 ? (h ? d1 : d0) : (h ? s1 : s0);
+                    wv |= (node == key ? 0x3F80u : 0u) << (16 * q);
+                }
+                oh[m] = wv;
+            }
+            const bf16x8 ao = as_bf16x8(make_uint4(oh[0], oh[1], oh[2], oh[3]));
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+                uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) split2(acc[t][8 * s + 2 * m], acc[t][8 * s + 2 * m + 1], hw[m], mw[m], lw[m]);
+                nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), nacc[t], 0, 0, 0);
+                nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), nacc[t], 0, 0, 0);
+                nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3])), nacc[t], 0, 0, 0);
+                // dA rows of this k-block's 8 registers, issued beside the MFMAs
+#pragma unroll
+                for (int r = 8 * s; r < 8 * s + 8; ++r) {
+                    float* p = dArow + rho(r, h) * kLdE + 32 * t;
+                    if (ACCUM) unsafeAtomicAdd(p, acc[t][r]);
+                    else *p = acc[t][r];
+                }
+            }
+        }
+        cur = nxt;
+        G4 = NG4;
+    }
+    // nacc[t] reg r = row rho(r,h): rows 0..15 receiver nodes, 16..31 sender nodes
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = rho(r, h);
+        const int node = row & 15;
+        if (node < nn) {
+            float* o = row < 16 ? a.dV : a.dU;   // chunk-major node rows
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+                if (32 * t + i < 2 * kKhE) o[cm_index<kKhE>(n0 + node, 32 * t + i)] = nacc[t][r];
+        }
+    }
+    info = ninfo;
+    }
+}
+
+hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
+    if (math == MATH_X6 && a.nw_max <= 16) {
+        const dim3 g(edge_grid(a.n_wtiles, kEdgeWavesX6)), b(64 * kEdgeWavesX6);
+        if (a.dA_accumulate)
+            hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
+        else
+            hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
+        return hipGetLastError();
+    }
     if (a.nw_max <= 16) {
         if (a.dA_accumulate)
             hipLaunchKernelGGL((k_edge_bwd<true, true>), dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
