@@ -311,7 +311,7 @@ __device__ __forceinline__ void bias_act_rho(f32x16 (&X)[NT], const float* __res
 }
 
 constexpr int kX6Ring = 3;
-constexpr int kEdgeWavesX6 = 4;   // edge kernels in x6 math: one wave per SIMD   // weight-fragment steps in flight (tgemm_x6)
+// (the x6 edge kernels pick their wave counts per variant: kernels_fwd.hip / kernels_bwd.hip)
 
 // ---- transposed orientation in split-bf16 math (x6), NC column tiles of 32 rows per wave:
 // out[c][T] += Wᵀ·B[c] over NKB k-blocks of 16. getb(c, kb, v) supplies the 8 fp32 B values of

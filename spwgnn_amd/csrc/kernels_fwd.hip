@@ -7,6 +7,7 @@
 //                    segment sum (Networks.py:174-178, with rmp layer 3 moved behind the sum)
 //   k_node_fwd       per step: rmp layer 3 on the summed messages, tanh, omp, state update,
 //                    readout, next-step U/V (Networks.py:178-186)
+#include <type_traits>
 #include "kernels.h"
 
 namespace spw {
@@ -636,9 +637,82 @@ struct NodeSumX6 {
     }
 };
 
-constexpr int kX6Pf = 5;   // A/U/V k-blocks in flight (edge_fwd x6); divides the 10 k-blocks
+// The same sum for wave-tiles of ≤ 16 nodes on 16x16x32 bf16 MFMAs: one v_permlane16_swap per
+// register pair turns the 32-feature C tiles into two 16-feature B operands of 32 edges each
+// (lane group g of a swapped register = edges of (s = g&1, h = g>>1)), so a block costs 30 MFMAs of
+// 16 cycles into 40 accumulator registers.
+struct NodeSum16X6 {
+    f32x4 acc[10];   // sub-tile u: features 16u + (lane & 15), nodes 4(lane >> 4) + r
+    int key;
+    __device__ __forceinline__ void init(int n0, int lane) {
+        key = n0 + (lane & 15);
+#pragma unroll
+        for (int u = 0; u < 10; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __device__ __forceinline__ void add(const f32x16 (&h2)[5], int d, int lane) {
+        const int g = lane >> 4;
+        // one-hot A: lane (node i, group g), element e ↔ edge 16(g&1) + 8(e>>2) + 4(g>>1) + (e&3)
+        uint32_t oh[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            uint32_t w = 0u;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int e = 2 * m + q, base = 8 * (e >> 2) + (e & 3);
+                const int d0 = __builtin_amdgcn_readlane(d, base), d1 = __builtin_amdgcn_readlane(d, base + 16);
+                const int d2 = __builtin_amdgcn_readlane(d, base + 4), d3 = __builtin_amdgcn_readlane(d, base + 20);
+                const int dn = g == 0 ? d0 : g == 1 ? d1 : g == 2 ? d2 : d3;
+                w |= (dn == key ? 0x3F80u : 0u) << (16 * q);
+            }
+            oh[m] = w;
+        }
+        const bf16x8 ao = as_bf16x8(make_uint4(oh[0], oh[1], oh[2], oh[3]));
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            uint32_t P[2][3][4];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    split2(h2[t][8 * s + 2 * m], h2[t][8 * s + 2 * m + 1], P[s][0][m], P[s][1][m], P[s][2][m]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(P[0][p][m], P[1][p][m], false, false);
+                    P[0][p][m] = r[0];   // sub-tile 2t
+                    P[1][p][m] = r[1];   // sub-tile 2t + 1
+                }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int p = 2; p >= 0; --p)
+                    acc[2 * t + u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        ao, as_bf16x8(make_uint4(P[u][p][0], P[u][p][1], P[u][p][2], P[u][p][3])), acc[2 * t + u], 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int node = 4 * (lane >> 4) + r;
+            if (node < nn) {
+#pragma unroll
+                for (int u = 0; u < 10; ++u) {
+                    const int f = 16 * u + (lane & 15);
+                    if (f < 2 * kKhE) H2s[cm_index<kKhE>(n0 + node, f)] = acc[u][r];
+                }
+            }
+        }
+    }
+};
 
-__global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_fwd_x6(EdgeFwdArgs a) {
+
+// Wave-tiles of ≤ 16 nodes: 8 waves (2 per SIMD, 256 registers: the 16-node sum and a one-k-block
+// ring); up to 32 nodes: 4 waves (1 per SIMD) with a 5-k-block ring.
+template <bool NW16>
+__global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
+void k_edge_fwd_x6(EdgeFwdArgs a) {
+    constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? 1 : 5;
     static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
     __shared__ uint4 wl[50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
     for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
@@ -646,7 +720,7 @@ __global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_fwd_x6(EdgeFwdArg
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
-    const int wstep = gridDim.x * kEdgeWavesX6;
+    const int wstep = gridDim.x * kWaves;
     const uint4* wlp = wl + lane;
     auto load_sd = [&](int blk) { return make_int2(a.esrc[(int64_t)blk * 32 + i], a.edst[(int64_t)blk * 32 + i]); };
     // a block's h1 operand sources: A rows and the gathered U[s], V[r] rows (chunk q at +256q / +64q)
@@ -668,7 +742,7 @@ __global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_fwd_x6(EdgeFwdArg
             r.v[c] = sr.V[64 * q];
         }
     };
-    int wt = blockIdx.x * kEdgeWavesX6 + wave;
+    int wt = blockIdx.x * kWaves + wave;
     if (wt >= a.n_wtiles) return;
     int4 info = wtiles[wt];
     // the first block's sources and its first kX6Pf k-blocks; later blocks' arrive during the
@@ -681,7 +755,7 @@ __global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_fwd_x6(EdgeFwdArg
     for (; wt < a.n_wtiles; wt += wstep) {
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];
-    NodeSumX6 nsum;
+    typename std::conditional<NW16, NodeSum16X6, NodeSumX6>::type nsum;
     nsum.init(n0, lane);
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
@@ -775,7 +849,7 @@ __global__ __launch_bounds__(64 * kEdgeWavesX6, 1) void k_edge_fwd_x6(EdgeFwdArg
             m2row[64 + lane] = mw2[1];
             if (lane < 32) m2row[128 + lane] = mw2[2];
         }
-        nsum.add(acc, d, h);
+        nsum.add(acc, d, NW16 ? lane : h);
         cur_sd = nsd;
         cur = nxt;
     }
@@ -828,7 +902,10 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
     if (math == MATH_X6) {
-        hipLaunchKernelGGL(k_edge_fwd_x6, dim3(edge_grid(a.n_wtiles, kEdgeWavesX6)), dim3(64 * kEdgeWavesX6), 0, st, a);
+        if (a.nw_max <= 16)
+            hipLaunchKernelGGL(k_edge_fwd_x6<true>, dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL(k_edge_fwd_x6<false>, dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (a.nw_max <= 16)
