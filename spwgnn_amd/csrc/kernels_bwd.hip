@@ -472,15 +472,15 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
 // and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
 // 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
 template <bool ACCUM>
-__global__ __launch_bounds__(64 * 4, 1) void k_edge_bwd_x6(EdgeBwdArgs a) {
-    constexpr int PF = 5;
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
+    constexpr int PF = 1, kWaves = 8;
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
     for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2t[idx];
     __syncthreads();
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
-    const int wstep = gridDim.x * 4;
+    const int wstep = gridDim.x * kWaves;
     const uint4* wlp = wl + lane;
     struct Pre { int d, s; uint32_t w[5]; };
     auto load_pre = [&](int blk) {
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(64 * 4, 1) void k_edge_bwd_x6(EdgeBwdArgs a) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
     };
-    int wt = blockIdx.x * 4 + wave;
+    int wt = blockIdx.x * kWaves + wave;
     if (wt >= a.n_wtiles) return;
     int4 info = wtiles[wt];
     Pre cur = load_pre(info.x);
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(64 * 4, 1) void k_edge_bwd_x6(EdgeBwdArgs a) {
 
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
     if (math == MATH_X6 && a.nw_max <= 16) {
-        const dim3 g(edge_grid(a.n_wtiles, 4)), b(256);   // one wave per SIMD (512 registers)
+        const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
         if (a.dA_accumulate)
             hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
         else
