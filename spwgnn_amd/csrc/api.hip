@@ -1,6 +1,7 @@
 // C-ABI entry points of libspwgnn_hip.so: workspace layout and launch sequences.
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include "kernels.h"
 #include "../../include/spwgnn.h"
 static_assert(SPWGNN_MATH_F32 == spw::MATH_F32 && SPWGNN_MATH_X6 == spw::MATH_X6, "math ids");
@@ -74,12 +75,10 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     w.ps.total = poff;
     w.pk = take(poff);
     {   // x6 images (uint4 = 4 floats each)
-        const int nt_nkb[X6_COUNT][2] = {{5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10}, {5, 10},
-                                         {5, 10}, {5, 10}};
         int64_t o = 0;
         for (int id = 0; id < X6_COUNT; ++id) {
             w.x6off[id] = o;
-            o += x6_chain_uint4(nt_nkb[id][0], nt_nkb[id][1]);
+            o += x6_chain_uint4(kX6Specs[id].nt_out, kX6Specs[id].nkb);
         }
         w.x6 = take(o * 4);
     }
@@ -214,6 +213,18 @@ static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
     return SPWGNN_OK;
 }
 
+// Per-kernel x6 selection for A/B diagnosis: SPWGNN_X6_KERNELS (bit mask of kX6*, default all)
+// narrows math == MATH_X6 to some kernels; the others run in f32 math.
+enum : int { kX6EncEdge = 1, kX6EdgeFwd = 2, kX6NodeFwd = 4, kX6NodeBwd = 8, kX6EdgeBwd = 16, kX6EncEdgeBwd = 32,
+             kX6Wgrad = 64 };
+static int kmath(const spwgnn_run* r, int bit) {
+    static const int mask = [] {
+        const char* e = getenv("SPWGNN_X6_KERNELS");
+        return e ? (int)strtol(e, nullptr, 0) : -1;
+    }();
+    return (r->math == MATH_X6 && (mask & bit)) ? MATH_X6 : MATH_F32;
+}
+
 struct Prof {
     const spwgnn_run* r;
     hipStream_t st;
@@ -244,36 +255,27 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     pa.pk = c.f(w.pk);
     build_packs(w, pa);
     SPW_CHECK(launch_prep_weights(pa, st));
-    if (r->math == MATH_X6) {
-        PrepX6Args xa{};
-        xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
-        auto img = [&](int id, int pid, int nt_out, int nkb, int kh) {
-            X6Desc& d = xa.d[id];
-            d.src = c.pk(pid);
-            d.cols = pack_cols(pid);
-            d.k4 = pa.desc[pid].k4;
-            d.nt_out = nt_out;
-            d.nkb = nkb;
-            d.kh = kh;
-            d.dst = w.x6off[id];
-        };
-        img(X6_RM1, PK_RM1, 5, 10, 0);
-        img(X6_RM2, PK_RM2, 5, 10, 0);
-        img(X6_RM3, PK_RM3, 5, 10, 0);
-        img(X6_W1A, PK_W1A, 5, 10, 0);
-        img(X6_W1AT, PK_W1AT, 5, 10, kKhE);
-        img(X6_RM3T, PK_RM3T, 5, 10, 0);
-        img(X6_RM2T, PK_RM2T, 5, 10, 0);
-        img(X6_RM1T, PK_RM1T, 5, 10, 0);
-        img(X6_W2, PK_W2, 5, 10, kKhE);     // edge-side B operands (LDS images)
-        img(X6_W2T, PK_W2T, 5, 10, kKhE);
-        SPW_CHECK(launch_prep_x6(xa, st));
-    }
     // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
     // (k4-blocked: element (150, c) sits at ((150/4)·128 + c)·4 + 150%4, a 16-byte stride)
     SPW_CHECK(hipMemcpy2DAsync(c.f(w.pk + w.ps.off[PK_W3A] + ((150 / 4) * kLdN) * 4 + 150 % 4), 4 * sizeof(float),
                                params + param_table().t[T_RMP2B].offset, sizeof(float), sizeof(float), 100,
                                hipMemcpyDeviceToDevice, st));
+    if (r->math == MATH_X6) {   // after the W3A bias row: the images are split from the packs
+        PrepX6Args xa{};
+        xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
+        for (int id = 0; id < X6_COUNT; ++id) {
+            const X6Spec& sp = kX6Specs[id];
+            X6Desc& d = xa.d[id];
+            d.src = c.pk(sp.pack);
+            d.cols = pack_cols(sp.pack);
+            d.k4 = pa.desc[sp.pack].k4;
+            d.nt_out = sp.nt_out;
+            d.nkb = sp.nkb;
+            d.kh = sp.kh;
+            d.dst = w.x6off[id];
+        }
+        SPW_CHECK(launch_prep_x6(xa, st));
+    }
     const bool drop = r->training && r->dropout > 0.f;
     const uint32_t thresh = (uint32_t)std::min(4294967295.0, std::floor((double)r->dropout * 4294967296.0));
     const float scale = drop ? 1.0f / (1.0f - r->dropout) : 1.0f;
@@ -337,7 +339,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     {
         Prof p0{r, st};
         SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
-        SPW_CHECK(launch_enc_edge(ee, r->math, st));
+        SPW_CHECK(launch_enc_edge(ee, kmath(r, kX6EncEdge), st));
         SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
     }
 
@@ -363,7 +365,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
-        SPW_CHECK(launch_edge_fwd(ef, r->math, st));
+        SPW_CHECK(launch_edge_fwd(ef, kmath(r, kX6EdgeFwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_EDGE_FWD));
 
         NodeFwdArgs nf{};
@@ -386,8 +388,17 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         nf.w1c = c.pk(PK_W1C);
         nf.bo1 = c.pk(PB_O1);
         nf.bo2p = c.pk(PB_O2P);
+        if (r->math == MATH_X6) {
+            nf.x_w3a = c.x6(X6_W3A);
+            nf.x_wo1c = c.x6(X6_WO1C);
+            nf.x_wo1a = c.x6(X6_WO1A);
+            nf.x_wo1p = c.x6(X6_WO1P);
+            nf.x_wo2 = c.x6(X6_WO2);
+            nf.x_w1b = c.x6(X6_W1B);
+            nf.x_w1c = c.x6(X6_W1C);
+        }
         SPW_CHECK(prof.before(SPWGNN_K_NODE_FWD));
-        SPW_CHECK(launch_node_fwd(nf, st));
+        SPW_CHECK(launch_node_fwd(nf, kmath(r, kX6NodeFwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_FWD));
     }
     return SPWGNN_OK;
@@ -506,8 +517,17 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         nb.wo1at = c.pk(PK_WO1AT);
         nb.wo1pt = c.pk(PK_WO1PT);
         nb.w3t = c.pk(PK_W3T);
+        if (r->math == MATH_X6) {
+            nb.x_w1bt = c.x6(X6_W1BT);
+            nb.x_w1ct = c.x6(X6_W1CT);
+            nb.x_wo2t = c.x6(X6_WO2T);
+            nb.x_wo1ct = c.x6(X6_WO1CT);
+            nb.x_wo1at = c.x6(X6_WO1AT);
+            nb.x_wo1pt = c.x6(X6_WO1PT);
+            nb.x_w3t = c.x6(X6_W3T);
+        }
         SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
-        SPW_CHECK(launch_node_bwd(nb, st));
+        SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
 
         EdgeBwdArgs eb{};
@@ -529,7 +549,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.dU = c.f(w.dU_at(s));
         eb.dV = c.f(w.dV_at(s));
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_BWD));
-        SPW_CHECK(launch_edge_bwd(eb, r->math, st));
+        SPW_CHECK(launch_edge_bwd(eb, kmath(r, kX6EdgeBwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
     }
     if (dprop) {
@@ -543,7 +563,11 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         nb.dprop = dprop;
         nb.w1bt = c.pk(PK_W1BT);
         nb.w1ct = c.pk(PK_W1CT);
-        SPW_CHECK(launch_node_bwd(nb, st));
+        if (r->math == MATH_X6) {
+            nb.x_w1bt = c.x6(X6_W1BT);
+            nb.x_w1ct = c.x6(X6_W1CT);
+        }
+        SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
     }
     EncEdgeBwdArgs eeb{};
     eeb.n_eblocks = b->n_eblocks;
@@ -565,7 +589,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     eeb.dz1 = c.f(w.dz1);
     eeb.scale = scale;
     SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
-    SPW_CHECK(launch_enc_edge_bwd(eeb, r->math, st));
+    SPW_CHECK(launch_enc_edge_bwd(eeb, kmath(r, kX6EncEdgeBwd), st));
     SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
 
     EncNodeBwdArgs enb{};
@@ -592,21 +616,21 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
-    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e; }
+    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
         // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
         g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st, &prof))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {
@@ -618,49 +642,49 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)
         WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
         g.rows = nN; g.y_stride = 0;
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, r->math, st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
     }
     return SPWGNN_OK;
 }

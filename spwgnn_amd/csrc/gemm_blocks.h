@@ -380,4 +380,26 @@ __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 
         out, img, lane);
 }
 
+// Half-row operand of tgemm_x6: lane half h of column tile c holds features KH·h .. KH·h + KH-1
+// of its row (chunk-major: chunk q of a 32-row block at + 256q), loaded whole up front.
+template <int KH, int NC>
+struct HalfRows {
+    static constexpr int Q = KH / 4;
+    float4 raw[NC][Q];
+    __device__ __forceinline__ void load(const float* const (&blk)[NC], int lane) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const float* p = blk[c] + ((lane >> 5) * 32 + (lane & 31)) * 4;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) raw[c][q] = *reinterpret_cast<const float4*>(p + 256 * q);
+        }
+    }
+    __device__ __forceinline__ void operator()(int c, int kb, float (&v)[8]) const {
+        const float4 x = raw[c][2 * kb];
+        const float4 y = 2 * kb + 1 < Q ? raw[c][2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    }
+};
+
 }  // namespace spw

@@ -25,7 +25,27 @@ struct PrepArgs {
 // element e of lane (i, h) = W[k(kb, e, h)][32T + i] with
 //   kh == 0 (chain: B is a C layout)          k = 16kb + 8(e>>2) + 4h + (e&3)
 //   kh > 0  (half rows: lane half h holds features kh·h ..)  k = kh·h + 8kb + e, zero if 8kb + e ≥ kh
-enum X6Id : int { X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A, X6_W1AT, X6_RM3T, X6_RM2T, X6_RM1T, X6_W2, X6_W2T, X6_COUNT };
+enum X6Id : int {
+    X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A,          // relation encoder (chains)
+    X6_W1AT, X6_RM3T, X6_RM2T, X6_RM1T,           // its backward
+    X6_W2, X6_W2T,                                // edge side (LDS B operands)
+    X6_W3A, X6_WO1C, X6_WO1A, X6_WO1P, X6_WO2, X6_W1B, X6_W1C,   // node side
+    X6_W1BT, X6_W1CT, X6_WO2T, X6_WO1PT, X6_WO1CT, X6_WO1AT, X6_W3T,   // its backward
+    X6_COUNT
+};
+// (image, fp32 pack, output tiles, k-blocks, kh) — the images every x6 run builds
+struct X6Spec { int id, pack, nt_out, nkb, kh; };
+constexpr X6Spec kX6Specs[X6_COUNT] = {
+    {X6_RM1, PK_RM1, 5, 10, 0},    {X6_RM2, PK_RM2, 5, 10, 0},    {X6_RM3, PK_RM3, 5, 10, 0},
+    {X6_W1A, PK_W1A, 5, 10, 0},    {X6_W1AT, PK_W1AT, 5, 10, kKhE}, {X6_RM3T, PK_RM3T, 5, 10, 0},
+    {X6_RM2T, PK_RM2T, 5, 10, 0},  {X6_RM1T, PK_RM1T, 5, 10, 0},  {X6_W2, PK_W2, 5, 10, kKhE},
+    {X6_W2T, PK_W2T, 5, 10, kKhE}, {X6_W3A, PK_W3A, 4, 10, kKhE}, {X6_WO1C, PK_WO1C, 4, 7, kKhN},
+    {X6_WO1A, PK_WO1A, 4, 7, 0},   {X6_WO1P, PK_WO1P, 4, 7, kKhN}, {X6_WO2, PK_WO2, 4, 7, 0},
+    {X6_W1B, PK_W1B, 5, 7, 0},     {X6_W1C, PK_W1C, 5, 7, 0},
+    {X6_W1BT, PK_W1BT, 4, 10, kKhE}, {X6_W1CT, PK_W1CT, 4, 10, kKhE}, {X6_WO2T, PK_WO2T, 4, 7, 0},
+    {X6_WO1PT, PK_WO1PT, 4, 7, 0}, {X6_WO1CT, PK_WO1CT, 4, 7, 0}, {X6_WO1AT, PK_WO1AT, 4, 7, 0},
+    {X6_W3T, PK_W3T, 5, 7, 0},
+};
 struct X6Desc {
     const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
     int32_t cols, k4;
@@ -83,6 +103,7 @@ struct NodeFwdArgs {
     const float *H2s, *P, *co;
     float *a_out, *o1_out, *Pn, *logits, *U, *V;
     const float *w3a, *wo1c, *wo1a, *wo1p, *wo2, *w1b, *w1c, *bo1, *bo2p;
+    const uint4 *x_w3a, *x_wo1c, *x_wo1a, *x_wo1p, *x_wo2, *x_w1b, *x_w1c;   // x6 images
 };
 
 struct NodeBwdArgs {
@@ -95,6 +116,7 @@ struct NodeBwdArgs {
     float *dx, *do1, *g, *G3, *dPout, *dco, *dprop;
     int dco_accumulate;
     const float *w1bt, *w1ct, *wo2t, *wo1ct, *wo1at, *wo1pt, *w3t;
+    const uint4 *x_w1bt, *x_w1ct, *x_wo2t, *x_wo1ct, *x_wo1at, *x_wo1pt, *x_w3t;   // x6 images
 };
 
 struct EdgeBwdArgs {
@@ -193,8 +215,8 @@ hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st);
 hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st);
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st);
-hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st);
-hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st);
+hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st);
+hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);

@@ -116,6 +116,146 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     store_cm<5>(a.G3 + bE, H, lane, valid);
 }
 
+// Node side of one backward step in split-bf16 math: the k_node_bwd chain on tgemm_x6, two 32-node
+// column tiles per wave (one wave per SIMD).
+template <int NC>
+__global__ __launch_bounds__(256, 1) void k_node_bwd_x6(NodeBwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
+    if (nb0 * 32 >= a.n_nodes) return;
+    const int nblocks = (a.n_nodes + 31) / 32;
+    int nbc[NC];
+    bool has[NC], valid[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        has[c] = nb0 + c < nblocks;
+        nbc[c] = min(nb0 + c, nblocks - 1);
+        valid[c] = has[c] && (nb0 + c) * 32 + j < a.n_nodes;
+    }
+    auto bN = [&](int c) { return (int64_t)nbc[c] * kCmBlkN; };
+    auto bE = [&](int c) { return (int64_t)nbc[c] * kCmBlk; };
+    auto zero2 = [&](f32x16 (&Z)[NC][4]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) zero_tiles(Z[c]);
+    };
+    f32x16 D[NC][4], G[NC][4];
+    if (a.first) {
+        zero2(D);
+    } else {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) load_cm<4>(a.dPin + bN(c), D[c], lane);
+        const float* blk[NC];
+        {
+            HalfRows<kKhE, NC> hr;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) blk[c] = a.dU + bE(c);
+            hr.load(blk, lane);
+            tgemm_x6<4, 10, NC>(hr, D, a.x_w1bt, lane);
+        }
+        {
+            HalfRows<kKhE, NC> hr;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) blk[c] = a.dV + bE(c);
+            hr.load(blk, lane);
+            tgemm_x6<4, 10, NC>(hr, D, a.x_w1ct, lane);
+        }
+    }
+    if (a.tail) {  // dP0 = d/d 'propagation' (ld 100)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (!valid[c]) continue;
+            const int64_t n = (int64_t)(nb0 + c) * 32 + j;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int f0 = 32 * t + 8 * q + 4 * h;
+                    if (f0 < kFN)
+                        *reinterpret_cast<float4*>(a.dprop + n * kFN + f0) =
+                            make_float4(D[c][t][4 * q], D[c][t][4 * q + 1], D[c][t][4 * q + 2], D[c][t][4 * q + 3]);
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        f32x16 Pn[4];
+        load_cm<4>(a.Pn + bN(c), Pn, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                const float p = Pn[t][r];
+                D[c][t][r] = f < kFN ? D[c][t][r] * (1.f - p * p) : 0.f;  // tanh' (Networks.py:181)
+            }
+        // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
+        if (has[c]) store_cm<4>(a.dPout + bN(c), D[c], lane, valid[c]);
+        if (a.first && h == 1) D[c][3][0] = valid[c] ? a.dlogits[(nb0 + c) * 32 + j] : 0.f;  // x' row 100 = logit
+        if (has[c]) store_cm<4>(a.dx + bN(c), D[c], lane, valid[c]);
+    }
+    zero2(G);
+    tchain_x6<4, 7, 4, NC>(D, G, a.x_wo2t, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        f32x16 O1[4];
+        load_cm<4>(a.o1 + bN(c), O1, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) G[c][t][r] = O1[t][r] > 0.f ? G[c][t][r] : 0.f;
+        if (has[c]) store_cm<4>(a.do1 + bN(c), G[c], lane, valid[c]);
+    }
+    // P part of omp's input → dP_s
+    zero2(D);
+    tchain_x6<4, 7, 4, NC>(G, D, a.x_wo1pt, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        f32x16 T[4];
+        load_cm<4>(a.dPout + bN(c), T, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) D[c][t] += T[t];
+        if (has[c]) store_cm<4>(a.dPout + bN(c), D[c], lane, valid[c]);
+    }
+    // c_o part → dc_o (accumulated over steps in step order S-1..0)
+    zero2(D);
+    tchain_x6<4, 7, 4, NC>(G, D, a.x_wo1ct, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (a.dco_accumulate) {
+            f32x16 T[4];
+            load_cm<4>(a.dco + bN(c), T, lane);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) D[c][t] = T[t] + D[c][t];
+        }
+        if (has[c]) store_cm<4>(a.dco + bN(c), D[c], lane, valid[c]);
+    }
+    // effect part → g = da ⊙ (1 - a²) → G3 = g·W3ᵀ
+    zero2(D);
+    tchain_x6<4, 7, 4, NC>(G, D, a.x_wo1at, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        f32x16 Aa[4];
+        load_cm<4>(a.a + bN(c), Aa, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = Aa[t][r];
+                D[c][t][r] = D[c][t][r] * (1.f - v * v);
+            }
+        if (has[c]) store_cm<4>(a.g + bN(c), D[c], lane, valid[c]);
+    }
+    f32x16 H[NC][5];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) zero_tiles(H[c]);
+    tchain_x6<5, 7, 4, NC>(D, H, a.x_w3t, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        if (has[c]) store_cm<5>(a.G3 + bE(c), H[c], lane, valid[c]);
+}
+
+
 // ------------------------------------------------------------------------------------------------
 template <int WORD_BASE>
 __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint32_t csrw, int t, bool tv, int lane) {
@@ -460,7 +600,13 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_node_bwd(const NodeBwdArgs& a, hipStream_t st) {
+hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
+    if (math == MATH_X6) {
+        constexpr int NC = 2;
+        const int w2 = ((a.n_nodes + 31) / 32 + NC - 1) / NC;
+        hipLaunchKernelGGL((k_node_bwd_x6<NC>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     const int waves = (a.n_nodes + 31) / 32;
     hipLaunchKernelGGL(k_node_bwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();

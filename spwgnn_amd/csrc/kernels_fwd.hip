@@ -575,6 +575,108 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Node side of one step in split-bf16 math: the k_node_fwd chain on tgemm_x6, two 32-node column
+// tiles per wave (one wave per SIMD).
+template <int NC>
+__global__ __launch_bounds__(256, 1) void k_node_fwd_x6(NodeFwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
+    if (nb0 * 32 >= a.n_nodes) return;
+    const int nblocks = (a.n_nodes + 31) / 32;
+    int nbc[NC];
+    bool has[NC], valid[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        has[c] = nb0 + c < nblocks;
+        nbc[c] = min(nb0 + c, nblocks - 1);
+        valid[c] = has[c] && (nb0 + c) * 32 + j < a.n_nodes;
+    }
+    auto bN = [&](int c) { return (int64_t)nbc[c] * kCmBlkN; };
+    auto bE = [&](int c) { return (int64_t)nbc[c] * kCmBlk; };
+    auto zero2 = [&](f32x16 (&Z)[NC][4]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) zero_tiles(Z[c]);
+    };
+    f32x16 E[NC][4], O[NC][4];
+    zero2(E);
+    {
+        HalfRows<kKhE, NC> hr;
+        const float* blk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) blk[c] = a.H2s + bE(c);
+        hr.load(blk, lane);
+        tgemm_x6<4, 10, NC>(hr, E, a.x_w3a, lane);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                E[c][t][r] = f < kFN ? tanhf(E[c][t][r]) : 0.f;
+            }
+        if (a.a_out && has[c]) store_cm<4>(a.a_out + bN(c), E[c], lane, valid[c]);
+    }
+    zero2(O);
+    {
+        HalfRows<kKhN, NC> hr;
+        const float* blk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) blk[c] = a.co + bN(c);
+        hr.load(blk, lane);
+        tgemm_x6<4, 7, NC>(hr, O, a.x_wo1c, lane);
+    }
+    tchain_x6<4, 7, 4, NC>(E, O, a.x_wo1a, lane);
+    {
+        HalfRows<kKhN, NC> hr;
+        const float* blk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) blk[c] = a.P + bN(c);
+        hr.load(blk, lane);
+        tgemm_x6<4, 7, NC>(hr, O, a.x_wo1p, lane);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        bias_act_rho<4, true>(O[c], a.bo1, h);
+        if (a.o1_out && has[c]) store_cm<4>(a.o1_out + bN(c), O[c], lane, valid[c]);
+    }
+    // X reuses E's registers: x' = o1·Wo2' + b, then P' = tanh(x' + P) into E
+    f32x16 (&X)[NC][4] = E;
+    zero2(X);
+    tchain_x6<4, 7, 4, NC>(O, X, a.x_wo2, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        bias_act_rho<4, false>(X[c], a.bo2p, h);
+        if (a.logits && h == 1 && valid[c]) a.logits[(nb0 + c) * 32 + j] = X[c][3][0];  // x' row 100 = rho(0,1) + 96
+        f32x16 P[4];
+        load_cm<4>(a.P + bN(c), P, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                X[c][t][r] = f < kFN ? tanhf(X[c][t][r] + P[t][r]) : 0.f;   // X := P'
+            }
+        if (has[c]) store_cm<4>(a.Pn + bN(c), X[c], lane, valid[c]);
+    }
+    if (a.U) {
+        f32x16 U[NC][5];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) zero_tiles(U[c]);
+        tchain_x6<5, 7, 4, NC>(X, U, a.x_w1b, lane);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (has[c]) store_cm<5>(a.U + bE(c), U[c], lane, valid[c]);
+            zero_tiles(U[c]);
+        }
+        tchain_x6<5, 7, 4, NC>(X, U, a.x_w1c, lane);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            if (has[c]) store_cm<5>(a.V + bE(c), U[c], lane, valid[c]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // One propagation step, edge side, in split-bf16 math (x6). Natural orientation as k_edge_fwd:
 // lane (i, h) of a block holds edge i, features 76h + 8kb + e of k-block kb (two 4-feature chunks
@@ -914,8 +1016,14 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
         hipLaunchKernelGGL(k_edge_fwd<false>, dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
     return hipGetLastError();
 }
-hipError_t launch_node_fwd(const NodeFwdArgs& a, hipStream_t st) {
+hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
+    if (math == MATH_X6) {
+        constexpr int NC = 2;
+        const int w2 = (waves + NC - 1) / NC;
+        hipLaunchKernelGGL((k_node_fwd_x6<NC>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_node_fwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
