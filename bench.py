@@ -28,7 +28,10 @@ from spwgnn_amd.trainer import Trainer  # noqa: E402
 
 METRIC = "towers/sec fwd+bwd, 6-block batch=65k, 1/2/4/8 MI355X; achieved HBM GB/s"
 PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: fp32 MFMA (= vector) peak
+PEAK_BF16_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA peak
 PEAK_HBM_GBS = 8000.0
+# x6 math runs each fp32 product as 6 bf16 MFMA products: its fp32-equivalent matrix peak
+PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
 
 # algorithmic FLOPs per launch of each timed kernel, as f(real edges, nodes, S)
 KERNELS = {
@@ -117,15 +120,19 @@ def cpu_baseline(n_objects: int, S: int, seconds: float, threads=None):
 
 # device kernel whose PMC summary (profiles/pmc_summary.json, tools/pmcsum.py) holds the HBM
 # bytes of a bench kernel
-PMC_NAMES = {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true, true>", "enc_edge": "k_enc_edge<true>",
-             "enc_edge_bwd": "k_enc_edge_bwd"}
+PMC_NAMES = {
+    "f32": {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true, true>", "enc_edge": "k_enc_edge<true>",
+            "enc_edge_bwd": "k_enc_edge_bwd", "wgrad_w2": "k_wgrad_t<4, 2, 160, 160>"},
+    "x6": {"edge_fwd": "k_edge_fwd_x6<true>", "edge_bwd": "k_edge_bwd_x6<true>", "enc_edge": "k_enc_edge_x6<true, 2>",
+           "enc_edge_bwd": "k_enc_edge_bwd_x6<2>", "wgrad_w2": "k_wgrad_x6<4, 2, 160, 160, 1>"},
+}
 
 
-def load_pmc(kernel: str):
+def load_pmc(kernel: str, math: str = "x6"):
     """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) from the committed PMC
     summary, or None when absent."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    name = PMC_NAMES.get(kernel)
+    name = PMC_NAMES[math].get(kernel)
     if name is None or not os.path.exists(path):
         return None
     try:
@@ -173,6 +180,7 @@ def main():
     ap.add_argument("--roofline-kernel", default="edge_bwd", choices=sorted(KERNELS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-f32-leg", action="store_true", help="skip the f32-math reference measurement")
     ap.add_argument("--math", default="x6", choices=["x6", "f32"],
                     help="matrix-product arithmetic (spwgnn.h SPWGNN_MATH_*)")
     ap.add_argument("--infer", action="store_true",
@@ -238,6 +246,26 @@ def main():
     achieved = kflops / (avg_ms * 1e-3) / 1e12
     value = world * B * args.steps / el
     total_flops = step_flops(Ne, Nn, S)
+    # roofline of the timed kernel: its algorithmic fp32 FLOPs against the matrix peak of the math
+    # it runs in (x6: bf16 peak / 6), and its PMC HBM bytes against 8 TB/s; the bound is the
+    # larger fraction
+    mpeak = PEAK_X6_TFLOPS if args.math == "x6" else PEAK_FP32_TFLOPS
+    traffic = load_pmc(args.roofline_kernel, args.math)
+    m_frac = achieved / mpeak
+    h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
+    h_frac = h_gbs / PEAK_HBM_GBS if h_gbs else None
+    if h_frac is not None and h_frac > m_frac:
+        roof = {"bound": "hbm", "achieved": round(h_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(h_frac, 4)}
+    else:
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(mpeak, 1), "unit": "TFLOP/s",
+                "frac": round(m_frac, 4)}
+    roof.update({"kernel": args.roofline_kernel, "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
+                 "launches": nl, "flop_per_launch": kflops, "mfma_tflops": round(achieved, 2),
+                 "mfma_peak": round(mpeak, 1), "mfma_frac": round(m_frac, 4),
+                 "hbm_gbs": round(h_gbs, 1) if h_gbs else None, "hbm_frac": round(h_frac, 4) if h_frac else None,
+                 "peak_note": ("x6: fp32 products as 6 bf16 MFMA products, peak = 2.5 PF bf16 / 6"
+                               if args.math == "x6" else "f32 MFMA peak")})
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -249,7 +277,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "f32",
+        "math": ("x6: each fp32 matrix product as 6 bf16 MFMA products of 3-way split operands, fp32 "
+                 "accumulation (DESIGN.md §3c)" if args.math == "x6" else "f32 MFMA"),
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
         "config": {"workload": f"train step fwd+BCE+bwd+{'allreduce+' if world > 1 else ''}Adam, "
                                f"{N}-block towers fully connected (E={N*(N-1)}), {B} towers/GPU, "
@@ -258,12 +288,22 @@ def main():
                    "parallelism": f"dp{world}"},
         "step_tflops": round(total_flops * world * args.steps / el / 1e12, 2),
         "loss": round(loss, 5),
-        "roofline": {"kernel": args.roofline_kernel, "bound": "mfma", "achieved": round(achieved, 2),
-                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                     "avg_launch_ms": round(avg_ms, 4), "launches": nl, "flop_per_launch": kflops,
-                     "traffic": load_pmc(args.roofline_kernel)},
+        "roofline": roof,
         "cpu_baseline": None,
     }
+    if world == 1 and args.math == "x6" and not args.no_f32_leg:
+        # the same step in f32 MFMA math, for reference (the other SPWGNN_MATH_* mode)
+        tr32 = Trainer(params.clone(), mp_steps=S, dropout=args.dropout, seed=7, math="f32")
+        for _ in range(2):
+            tr32.step(batch, target)
+        torch.cuda.synchronize()
+        k32 = max(3, args.steps // 2)
+        t1 = time.perf_counter()
+        for _ in range(k32):
+            tr32.step(batch, target)
+        torch.cuda.synchronize()
+        e32 = time.perf_counter() - t1
+        out["f32_math"] = {"value": round(B * k32 / e32, 1), "ms_per_step": round(e32 / k32 * 1e3, 3), "steps": k32}
     out["hbm"] = step_hbm(out["ms_per_step"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_pair(N, S, args.cpu_seconds)

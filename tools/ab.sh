@@ -8,7 +8,7 @@ for v in A B; do
 done
 cd /tmp && export TMPDIR=/tmp
 for v in A B; do
-  SPWGNN_LIB=$R/tools/ab/lib$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ab_${T}_prof$v -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/ab_${T}_prof$v.log 2>&1
+  SPWGNN_LIB=$R/tools/ab/lib$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ab_${T}_prof$v -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-f32-leg > $R/gpurun_out/ab_${T}_prof$v.log 2>&1
 done
 cd $R
 for v in A B; do echo "== $v"; python3 tools/profsum.py gpurun_out/ab_${T}_prof$v | head -14; done

@@ -1,7 +1,7 @@
 set -e
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline"; TAG=${1:-x}
+B="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-leg"; TAG=${1:-x}
 timeout -k 10 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $R/gpurun_out/pmc${TAG}A -o run --output-format csv -- python3 $B > $R/gpurun_out/pmc${TAG}A.log 2>&1
 timeout -k 10 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $R/gpurun_out/pmc${TAG}B -o run --output-format csv -- python3 $B > $R/gpurun_out/pmc${TAG}B.log 2>&1
 timeout -k 10 240 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES -d $R/gpurun_out/pmc${TAG}C -o run --output-format csv -- python3 $B > $R/gpurun_out/pmc${TAG}C.log 2>&1
