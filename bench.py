@@ -279,7 +279,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "math": ("x6: each fp32 matrix product as 6 bf16 MFMA products of 3-way split operands, fp32 "
-                 "accumulation (DESIGN.md §3c)" if args.math == "x6" else "f32 MFMA"),
+                 "accumulation (DESIGN.md §3b)" if args.math == "x6" else "f32 MFMA"),
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
         "config": {"workload": f"train step fwd+BCE+bwd+{'allreduce+' if world > 1 else ''}Adam, "
                                f"{N}-block towers fully connected (E={N*(N-1)}), {B} towers/GPU, "

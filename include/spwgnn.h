@@ -114,7 +114,7 @@ typedef struct spwgnn_run {
     void** prof_events;
 } spwgnn_run;
 
-/* Matrix-product arithmetic. Both give fp32-class results (DESIGN.md §3c):
+/* Matrix-product arithmetic. Both give fp32-class results (DESIGN.md §3b):
  *   F32  v_mfma_f32_*_f32: one fp32 fma chain per output (the f32 MFMA rate, 157 TF)
  *   X6   each fp32 operand split into three bf16 parts, six bf16 MFMA products per fp32 product,
  *        fp32 accumulation (6/16 of the f32 MFMA cost; error O(2^-24) per product)            */

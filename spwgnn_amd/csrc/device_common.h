@@ -30,7 +30,7 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 __device__ __forceinline__ constexpr int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // ---------------------------------------------------------------------------------------------
-// Split-bf16 products ("x6" math, DESIGN.md §3c). gfx950's bf16 MFMA runs 16× the f32 MFMA rate;
+// Split-bf16 products ("x6" math, DESIGN.md §3b). gfx950's bf16 MFMA runs 16× the f32 MFMA rate;
 // an fp32 operand x is split (round-to-nearest at each stage) into x = h + m + l + O(2^-25·|x|)
 // with h, m, l bf16, and x·y ≈ hh + hm + mh + mm + hl + lh (the dropped ml, lm, ll terms are
 // O(2^-26)): six bf16 products with exact fp32 accumulation = fp32-class results at 6/16 of the

@@ -99,7 +99,7 @@ def test_full_size_towers_are_independent(math):
     """B = 65,536 towers (the bench config): every tower's logits equal the oracle on that tower
     alone (sampled), and match a run of the same tower in a small batch — bit-identical in f32
     math; in x6 math the receiver sums add a node's messages in 16-edge k-blocks whose grouping
-    follows the tower's position, so the two runs agree to rounding (DESIGN.md §3c)."""
+    follows the tower's position, so the two runs agree to rounding (DESIGN.md §3b)."""
     B, N, S = 65536, 6, 5
     params = O.random_params(6)
     raw = D.synthetic_towers(B, N, seed=17)
