@@ -429,15 +429,19 @@ template <int W>
 struct X6Img {
     static constexpr int ROWB = W * 2, PART = 32 * ROWB;
     __device__ static __forceinline__ int sigma(int r) { return (ROWB % 256 == 0) ? (r & 7) : ((r >> 2) & 1); }
+    // within a unit the four 8-byte granules are XOR-permuted by row & 3: the 32 rows one wave's
+    // staging store touches then spread over all 32 store banks (2-way, the minimum for b64)
+    // instead of 4 of them; a row's unit still holds the same 8 dwords, so the transposed reads
+    // stay conflict-free
     __device__ static __forceinline__ int woff(int rr, int c4) {
-        return rr * ROWB + 32 * ((c4 >> 2) ^ sigma(rr)) + 8 * (c4 & 3);
+        return rr * ROWB + 32 * ((c4 >> 2) ^ sigma(rr)) + 8 * ((c4 & 3) ^ (rr & 3));
     }
     // lane's read offset for 16-column tile t: group g = lane>>4 reads rows 4g..4g+3 (elements 0-3)
     // and 16+4g..16+4g+3 (elements 4-7, at + 16·ROWB) — the k order of the 16x16x32 operand, the
     // same for both operands of a product
     __device__ static __forceinline__ int roff(int lane, int t) {
         const int li = lane & 15, row = 4 * (lane >> 4) + (li >> 2);
-        return row * ROWB + 32 * (t ^ sigma(row)) + 8 * (li & 3);
+        return row * ROWB + 32 * (t ^ sigma(row)) + 8 * ((li & 3) ^ (row & 3));
     }
     __device__ static __forceinline__ void put(char* S, int rr, int c4, float4 v) {
         uint32_t h0, m0, l0, h1, m1, l1;
