@@ -51,6 +51,11 @@ struct Ws {
 };
 
 static constexpr int kMaxChunks = 1024;
+static constexpr int kW2gWgs = 256;   // W2 gradient: one workgroup per CU (MI355X: 256 CUs)
+static bool getenv_flag(const char* name) {
+    const char* e = getenv(name);
+    return e && *e && *e != '0';
+}
 static constexpr int kReduceGroups = 32;
 
 static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
@@ -459,8 +464,20 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.RN = w.RN;
         a.S = (int)(g.rows / w.RE);
     }
+    // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
+    const bool ws = g.recompute && math == MATH_X6 && !getenv_flag("SPWGNN_W2G_OLD");
+    int64_t bpw = 0;
+    if (ws) {
+        const int64_t nblk = w.RE / 32;
+        const int64_t wgs = std::min<int64_t>(nblk, kW2gWgs);
+        bpw = (nblk + wgs - 1) / wgs;
+        chunks = (nblk + bpw - 1) / bpw;
+    }
     if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
-    SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
+    if (ws)
+        SPW_CHECK(launch_w2grad_ws(a, (int)chunks, bpw, st));
+    else
+        SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     const ParamTable& pt = param_table();
     ReduceArgs ra{};

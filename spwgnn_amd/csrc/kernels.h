@@ -222,6 +222,7 @@ hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
+hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hipStream_t st);
 hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);

@@ -1,6 +1,7 @@
 // Weight gradients (dW = Σ_rows Xᵀ·Y, deterministic split-row slabs + ordered reduction),
 // Keras BCE loss, Keras Adam, sigmoid readout.
 #include "kernels.h"
+#include <cstdlib>
 
 namespace spw {
 
@@ -514,6 +515,195 @@ __global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
                 out[(int64_t)(16 * (MX * wx + x) + 4 * kq + r) * NYP + 16 * (MY * wy + y) + c16] = acc[x][y][r];
 }
 
+// W2 gradient (x6), warp-specialized: dW2 = Σ_{s,e} [h1 | 1]ᵀ · dh2pre over all (edge, step) rows,
+// h1 = relu(A + U_s[src] + V_s[dst]), dh2pre = G3_s[dst] ⊙ [h2_s > 0], recomputed from chunk-major
+// rows. A 512-thread workgroup per CU walks a contiguous range of edge blocks × steps (stage t =
+// (edge block b0 + t / S, step t % S)). Waves 0-3 (one per SIMD) only read split images from LDS
+// and run the 16x16x32 MFMAs (5×5 tiles each, 2×2 over the 160×160 output); waves 4-7 (the
+// partner wave on each SIMD) gather stage t+2 into registers, build and split stage t+1 into the
+// other LDS buffer, so the matrix pipe runs while the staging VALU work issues in its gaps.
+// One barrier per stage; deterministic (fixed ranges and order).
+constexpr int kW2gThreads = 512;
+constexpr int kW2gImg = 3 * X6Img<160>::PART;   // one operand's split image (30 KB)
+
+struct W2gSet {
+    float4 a[5], u[5], v[5], g[5];
+    uint32_t m[5];
+    int in;
+};
+
+// DBG (diagnosis builds, SPWGNN_W2G_DBG): 1 no MFMAs, 2 gathers from stage 0, 4 no staging
+// arithmetic, 8 matrix waves at s_setprio 1, 32 no gathers
+template <int dbg>
+__global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
+    using IM = X6Img<160>;
+    __shared__ __attribute__((aligned(16))) char buf[2][2 * kW2gImg];   // [stage parity][X | Y]
+    const int tid = threadIdx.x;
+    const int S = a.S;
+    const int64_t nblk = a.RE >> 5;
+    const int64_t b0 = (int64_t)blockIdx.x * blk_per_wg;
+    const int64_t b1 = min(nblk, b0 + blk_per_wg);
+    const int T = b1 > b0 ? (int)(b1 - b0) * S : 0;   // stages of this workgroup (< 2^31)
+    if (tid < 256) {
+        // ---------------- matrix waves ----------------
+        const int lane = tid & 63, c16 = lane & 15, kq = lane >> 4;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int wx = wave >> 1, wy = wave & 1;
+        f32x4 acc[5][5];
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+#pragma unroll
+            for (int y = 0; y < 5; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int ox[5], oy[5];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) ox[x] = IM::roff(lane, 5 * wx + x);
+#pragma unroll
+        for (int y = 0; y < 5; ++y) oy[y] = IM::roff(lane, 5 * wy + y);
+        if constexpr ((dbg & 8) != 0) __builtin_amdgcn_s_setprio(1);
+        __syncthreads();   // stage 0 staged
+        for (int t = 0; t < T; ++t) {
+            if constexpr ((dbg & 1) != 0) { __syncthreads(); continue; }
+            const char* Xs = buf[t & 1];
+            const char* Ys = Xs + kW2gImg;
+            // fragment reads run one (x, y) group ahead of the MFMAs that use them: X0 Y0 | Y1 ·
+            // (0,0) | Y2 · (0,1) | … | X1 · (0,4) | X2 · (1,*) | X3 · (2,*) | X4 · (3,*) | (4,*)
+            bf16x8 yb[5][3], xa[2][3];
+            IM::get(Xs, ox[0], xa[0]);
+            IM::get(Ys, oy[0], yb[0]);
+#pragma unroll
+            for (int y = 0; y < 5; ++y) {
+                if (y < 4) IM::get(Ys, oy[y + 1], yb[y + 1]);
+                else IM::get(Xs, ox[1], xa[1]);
+                __builtin_amdgcn_sched_barrier(0);
+                acc[0][y] = mfma16_x6(xa[0], yb[y], acc[0][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int x = 1; x < 5; ++x) {
+                if (x < 4) IM::get(Xs, ox[x + 1], xa[(x + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int y = 0; y < 5; ++y) acc[x][y] = mfma16_x6(xa[x & 1], yb[y], acc[x][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+        }
+        float* out = a.slab + (int64_t)blockIdx.x * 160 * 160;
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+#pragma unroll
+            for (int y = 0; y < 5; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    out[(int64_t)(16 * (5 * wx + x) + 4 * kq + r) * 160 + 16 * (5 * wy + y) + c16] = acc[x][y][r];
+        return;
+    }
+    // ---------------- staging waves ----------------
+    // thread: edge rr of the 32-edge block, column groups c4 = c0 + 8k (k < 5; c4 ≥ 38 is padding)
+    const int st = tid - 256, rr = st & 31, c0 = st >> 5;
+    const bool k4ok = __builtin_amdgcn_readfirstlane(st >> 6) < 3;   // c0 < 6: staging waves 0-2
+    int off[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) off[k] = (k < 4 || k4ok) ? cm_offk<kKhE>(0, 4 * (c0 + 8 * k)) : 0;
+    const int64_t nstep_n = a.RN * kRowE;
+    auto stage_of = [&](int t, int64_t& b, int& s) {
+        const uint32_t tc = (uint32_t)(t < T ? t : T - 1);
+        const uint32_t q = tc / (uint32_t)S;
+        b = b0 + q;
+        s = (int)(tc - q * (uint32_t)S);
+    };
+    auto load_idx = [&](int t, int2& idx) {
+        int64_t b; int s;
+        stage_of(t, b, s);
+        idx.x = a.esrc[32 * b + rr];
+        idx.y = a.edst[32 * b + rr];
+    };
+    auto fetch = [&](int t, const int2& idx, W2gSet& R) {
+        if constexpr ((dbg & 32) != 0) return;
+        if constexpr ((dbg & 2) != 0) t = 0;
+        int64_t b; int s;
+        stage_of(t, b, s);
+        R.in = idx.x >= 0;
+        const int sn = R.in ? idx.x : 0, dn = R.in ? idx.y : 0;
+        const float* pa = a.A + b * kCmBlk + rr * 4;
+        const int64_t ns = (int64_t)s * nstep_n;
+        const float* pu = a.U + ns + (int64_t)(sn >> 5) * kCmBlk + (sn & 31) * 4;
+        const int64_t dno = ns + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
+        const float* pv = a.V + dno;
+        const float* pg = a.G3 + dno;
+        const uint32_t* pm = a.mask2 + ((int64_t)s * nblk + b) * 160 + rr;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            R.a[k] = *reinterpret_cast<const float4*>(pa + off[k]);
+            R.u[k] = *reinterpret_cast<const float4*>(pu + off[k]);
+            R.v[k] = *reinterpret_cast<const float4*>(pv + off[k]);
+            R.g[k] = *reinterpret_cast<const float4*>(pg + off[k]);
+            R.m[k] = pm[k * 32];
+        }
+    };
+    auto build = [&](const W2gSet& R, char* Xs) {
+        if constexpr ((dbg & 4) != 0) return;
+        char* Ys = Xs + kW2gImg;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k == 4 && !k4ok) break;
+            float4 x = f4relu(f4add3(R.a[k], R.u[k], R.v[k]));
+            if (k == 4 && c0 == 5) x.z = 1.f;   // feature 150: the b2 ones column
+            // dh2pre = G3 ⊙ [h2 > 0]: sign-extended single-bit fields as AND masks
+            const int w = (int)(R.in ? R.m[k] : 0u);
+            const float4 gv = R.g[k];
+            const float4 y = make_float4(
+                __int_as_float(__float_as_int(gv.x) & __builtin_amdgcn_sbfe(w, 4 * c0, 1)),
+                __int_as_float(__float_as_int(gv.y) & __builtin_amdgcn_sbfe(w, 4 * c0 + 1, 1)),
+                __int_as_float(__float_as_int(gv.z) & __builtin_amdgcn_sbfe(w, 4 * c0 + 2, 1)),
+                __int_as_float(__float_as_int(gv.w) & __builtin_amdgcn_sbfe(w, 4 * c0 + 3, 1)));
+            IM::put(Xs, rr, c0 + 8 * k, x);
+            IM::put(Ys, rr, c0 + 8 * k, y);
+        }
+    };
+    if (T == 0) {
+        __syncthreads();
+        return;
+    }
+    if (!k4ok) {   // padding columns 152..159 of both operands in both buffers stay zero
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            IM::put(buf[p], rr, c0 + 32, f4zero());
+            IM::put(buf[p] + kW2gImg, rr, c0 + 32, f4zero());
+        }
+    }
+    W2gSet R0, R1;
+    int2 i0, i1;
+    load_idx(0, i0);
+    load_idx(1, i1);
+    fetch(0, i0, R0);
+    load_idx(2, i0);
+    fetch(1, i1, R1);
+    load_idx(3, i1);
+    build(R0, buf[0]);
+    __syncthreads();   // stage 0 staged
+    // iteration t: gather stage t+2 (set t&1, indices loaded an iteration earlier), load the
+    // indices of stage t+3, build stage t+1 (set (t+1)&1) into buffer (t+1)&1, barrier
+    int t = 0;
+    for (; t + 2 < T; t += 2) {
+        fetch(t + 2, i0, R0);
+        load_idx(t + 4, i0);
+        build(R1, buf[1]);
+        __syncthreads();
+        fetch(t + 3, i1, R1);
+        load_idx(t + 5, i1);
+        build(R0, buf[0]);
+        __syncthreads();
+    }
+    if (t + 1 < T) {   // t even: build stage t+1 from set 1
+        build(R1, buf[1]);
+        __syncthreads();
+        ++t;
+    }
+    __syncthreads();   // the matrix waves' last stage
+}
+
 // stage 1: partial[g][idx] = Σ_{c in group g} slab[c][idx] (contiguous chunk ranges, fixed order)
 __global__ void k_wgrad_reduce1(ReduceArgs a, float* partial, int groups) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -633,6 +823,19 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st
     SPW_WG(XM_H1, YM_DH2, 160, 160)
 #undef SPW_WG
     return hipErrorInvalidValue;
+}
+hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hipStream_t st) {
+    static const int dbg = getenv("SPWGNN_W2G_DBG") ? atoi(getenv("SPWGNN_W2G_DBG")) : 0;
+    const dim3 g(wgs), b(kW2gThreads);
+    switch (dbg) {
+        case 0: hipLaunchKernelGGL(k_w2grad_ws<0>, g, b, 0, st, a, blk_per_wg); break;
+        case 1: hipLaunchKernelGGL(k_w2grad_ws<1>, g, b, 0, st, a, blk_per_wg); break;
+        case 4: hipLaunchKernelGGL(k_w2grad_ws<4>, g, b, 0, st, a, blk_per_wg); break;
+        case 8: hipLaunchKernelGGL(k_w2grad_ws<8>, g, b, 0, st, a, blk_per_wg); break;
+        case 33: hipLaunchKernelGGL(k_w2grad_ws<33>, g, b, 0, st, a, blk_per_wg); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st) {
     const int n = a.kx_pad * a.ny_pad;
