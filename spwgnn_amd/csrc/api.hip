@@ -464,6 +464,29 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.RN = w.RN;
         a.S = (int)(g.rows / w.RE);
     }
+    // stored chunk-major operands in x6 math: the warp-specialized kernel, one workgroup per CU
+    if (math == MATH_X6 && g.xmode == XM_CM && (g.ymode == YM_CM || g.ymode == YM_ROW) &&
+        !getenv_flag("SPWGNN_WG_OLD")) {
+        WgWsArgs wa{};
+        wa.x = g.x;
+        wa.y = g.y;
+        wa.slab = c.f(w.slab);
+        wa.count = g.x_count;
+        wa.S = g.rows / g.x_count;
+        wa.nbs = (g.x_count + 31) / 32;
+        wa.x_sb = g.x_stride / 32;
+        wa.y_sb = g.y_stride / 32;
+        wa.x_ones = g.x_ones;
+        const int64_t nst = wa.nbs * wa.S;
+        int64_t wgs = std::min<int64_t>(nst, kW2gWgs);
+        wa.stages_per_wg = (nst + wgs - 1) / wgs;
+        wgs = (nst + wa.stages_per_wg - 1) / wa.stages_per_wg;
+        chunks = wgs;
+        const bool mask = !(g.kx_pad == 160 && g.ny_pad == 160);   // node arrays: rows ≥ count masked
+        if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
+        SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, st));
+        if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
+    } else {
     // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
     const bool ws = g.recompute && math == MATH_X6 && !getenv_flag("SPWGNN_W2G_OLD");
     int64_t bpw = 0;
@@ -479,6 +502,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     else
         SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
+    }
     const ParamTable& pt = param_table();
     ReduceArgs ra{};
     ra.slab = c.f(w.slab);

@@ -183,6 +183,13 @@ struct WgradArgs {
     int S;                         // steps (XM_H1 / YM_DH2 walk rows as (edge block, step) stages)
     float* slab;           // [chunks][kx_pad][ny_pad]
 };
+struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 32-row blocks
+    const float* x;        // chunk-major
+    const float* y;        // chunk-major, or row-major with stride 160 (yrow)
+    float* slab;           // [wgs][kx_pad][ny_pad]
+    int64_t nbs, S, x_sb, y_sb, count, stages_per_wg;
+    int x_ones, pad0;
+};
 struct ReduceArgs {
     const float* slab;
     int chunks, kx_pad, ny_pad;
@@ -222,6 +229,7 @@ hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
+hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, hipStream_t st);
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hipStream_t st);
 hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);

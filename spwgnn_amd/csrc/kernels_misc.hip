@@ -704,6 +704,193 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
     __syncthreads();   // the matrix waves' last stage
 }
 
+// Stored-operand weight gradients (x6), warp-specialized like k_w2grad_ws: dW[k][n] =
+// Σ_rows X[row][k]·Y[row][n] with X chunk-major and Y chunk-major (YROW = 0) or row-major
+// (YROW = 1, stride 160: the dA rows). Stages are 32-row blocks t = (step s, block nb) of a
+// [S][nbs] grid; X block s·x_sb + nb (x_sb = 0: an operand shared by every step), Y block
+// s·y_sb + nb; rows ≥ count of a step are masked (MASK). Waves 0-3 run the MFMAs on
+// double-buffered split images, waves 4-7 stream the operands three stages ahead and split them.
+constexpr int kWsThreads = 512;
+
+template <int KXP, int NYP, int YROW, bool MASK>
+struct WsStage {
+    static constexpr int KHX = KXP == 160 ? kKhE : kKhN, KHY = NYP == 160 ? kKhE : kKhN;
+    static constexpr int GX = KHX / 2, GY = YROW ? NYP / 4 : KHY / 2;   // float4 groups per row
+    static constexpr int NKX = (GX + 7) / 8, NKY = (GY + 7) / 8;        // groups per staging thread
+    static constexpr int IMX = 3 * X6Img<KXP>::PART, IMY = 3 * X6Img<NYP>::PART;
+    static constexpr int BUF = IMX + IMY;
+};
+struct WsSet4 {
+    float4 x[5], y[5];
+    int nvalid;
+};
+
+template <int KXP, int NYP, int YROW, bool MASK>
+__global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_wgrad_ws(WgWsArgs a) {
+    using W = WsStage<KXP, NYP, YROW, MASK>;
+    using IX = X6Img<KXP>;
+    using IY = X6Img<NYP>;
+    constexpr int MX = KXP / 32, MY = NYP / 32;
+    __shared__ __attribute__((aligned(16))) char buf[2][W::BUF];
+    const int tid = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * a.stages_per_wg;
+    const int64_t nst = a.nbs * a.S;
+    const int T = t0 < nst ? (int)min<int64_t>(a.stages_per_wg, nst - t0) : 0;
+    if (tid < 256) {
+        const int lane = tid & 63, c16 = lane & 15, kq = lane >> 4;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int wx = wave >> 1, wy = wave & 1;
+        f32x4 acc[MX][MY];
+#pragma unroll
+        for (int x = 0; x < MX; ++x)
+#pragma unroll
+            for (int y = 0; y < MY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int ox[MX], oy[MY];
+#pragma unroll
+        for (int x = 0; x < MX; ++x) ox[x] = IX::roff(lane, MX * wx + x);
+#pragma unroll
+        for (int y = 0; y < MY; ++y) oy[y] = IY::roff(lane, MY * wy + y);
+        __syncthreads();
+        for (int t = 0; t < T; ++t) {
+            const char* Xs = buf[t & 1];
+            const char* Ys = Xs + W::IMX;
+            bf16x8 yb[MY][3], xa[2][3];
+            IX::get(Xs, ox[0], xa[0]);
+            IY::get(Ys, oy[0], yb[0]);
+#pragma unroll
+            for (int y = 0; y < MY; ++y) {
+                if (y + 1 < MY) IY::get(Ys, oy[y + 1], yb[y + 1]);
+                else IX::get(Xs, ox[1], xa[1]);
+                __builtin_amdgcn_sched_barrier(0);
+                acc[0][y] = mfma16_x6(xa[0], yb[y], acc[0][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int x = 1; x < MX; ++x) {
+                if (x + 1 < MX) IX::get(Xs, ox[x + 1], xa[(x + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6(xa[x & 1], yb[y], acc[x][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+        }
+        float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
+#pragma unroll
+        for (int x = 0; x < MX; ++x)
+#pragma unroll
+            for (int y = 0; y < MY; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    out[(int64_t)(16 * (MX * wx + x) + 4 * kq + r) * NYP + 16 * (MY * wy + y) + c16] = acc[x][y][r];
+        return;
+    }
+    // ---------------- staging waves ----------------
+    // chunk-major operands: thread = row rr, column groups c0 + 8k; row-major Y: 8 threads per row
+    // (row yr = st >> 3, groups (st & 7) + 8k: 128 contiguous bytes per 8 lanes)
+    const int st = tid - 256, rr = st & 31, c0 = st >> 5;
+    const int yr = YROW ? (st >> 3) & 31 : rr, yc0 = YROW ? (st & 7) : c0;
+    const int swave = __builtin_amdgcn_readfirstlane(st >> 6);
+    int offx[W::NKX], offy[W::NKY];
+#pragma unroll
+    for (int k = 0; k < W::NKX; ++k) {
+        const int c4 = c0 + 8 * k;
+        offx[k] = c4 < W::GX ? cm_offk<W::KHX>(0, 4 * c4) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < W::NKY; ++k) {
+        const int c4 = yc0 + 8 * k;
+        offy[k] = YROW ? 4 * c4 : (c4 < W::GY ? cm_offk<W::KHY>(0, 4 * c4) : 0);
+    }
+    // wave-uniform: does this staging wave own a real group at slot k (c0 = 2·swave + {0, 1})
+    auto xk_ok = [&](int k) { return 2 * swave + 8 * k < W::GX; };
+    auto yk_ok = [&](int k) { return YROW ? true : 2 * swave + 8 * k < W::GY; };
+    const int ones_k = a.x_ones >= 0 && ((a.x_ones >> 2) & 7) == c0 ? (a.x_ones >> 5) : -1;
+    const int ones_c = a.x_ones & 3;
+    auto fetch = [&](int t, WsSet4& R) {
+        const int64_t tg = t0 + (t < T ? t : T - 1);
+        const int64_t s = tg / a.nbs, nb = tg - s * a.nbs;
+        if (MASK) R.nvalid = (int)min<int64_t>(32, a.count - nb * 32);
+        const float* px = a.x + (s * a.x_sb + nb) * (W::KHX * 64) + rr * 4;
+        const float* py = YROW ? a.y + ((s * a.y_sb + nb) * 32 + yr) * 160
+                               : a.y + (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
+#pragma unroll
+        for (int k = 0; k < W::NKX; ++k) R.x[k] = *reinterpret_cast<const float4*>(px + offx[k]);
+#pragma unroll
+        for (int k = 0; k < W::NKY; ++k) R.y[k] = *reinterpret_cast<const float4*>(py + offy[k]);
+    };
+    auto build = [&](const WsSet4& R, char* Xs) {
+        char* Ys = Xs + W::IMX;
+        const bool xin = !MASK || rr < R.nvalid, yin = !MASK || yr < R.nvalid;
+#pragma unroll
+        for (int k = 0; k < W::NKX; ++k) {
+            if (!xk_ok(k)) break;
+            float4 v = R.x[k];
+            if (MASK && !xin) v = f4zero();
+            if (k == ones_k) f4set(v, ones_c, xin ? 1.f : 0.f);
+            IX::put(Xs, rr, c0 + 8 * k, v);
+        }
+#pragma unroll
+        for (int k = 0; k < W::NKY; ++k) {
+            if (!yk_ok(k)) break;
+            float4 v = R.y[k];
+            if (MASK && !yin) v = f4zero();
+            IY::put(Ys, yr, yc0 + 8 * k, v);
+        }
+    };
+    if (T == 0) {
+        __syncthreads();
+        return;
+    }
+    // padding column groups (≥ GX / GY, below the image width) stay zero in both buffers
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int k = 0; k < (KXP / 4 + 7) / 8; ++k) {
+            const int c4 = c0 + 8 * k;
+            if (c4 >= W::GX && c4 < KXP / 4) IX::put(buf[p], rr, c4, f4zero());
+        }
+        if (!YROW) {
+#pragma unroll
+            for (int k = 0; k < (NYP / 4 + 7) / 8; ++k) {
+                const int c4 = c0 + 8 * k;
+                if (c4 >= W::GY && c4 < NYP / 4) IY::put(buf[p] + W::IMX, rr, c4, f4zero());
+            }
+        }
+    }
+    WsSet4 R0, R1, R2;
+    fetch(0, R0);
+    fetch(1, R1);
+    fetch(2, R2);
+    build(R0, buf[0]);
+    __syncthreads();
+    // iteration t: stream stage t+3 into set t%3, build stage t+1 (set (t+1)%3) into buffer (t+1)&1
+    int t = 0;
+    for (; t + 3 <= T - 1; t += 3) {
+        fetch(t + 3, R0);
+        build(R1, buf[(t + 1) & 1]);
+        __syncthreads();
+        fetch(t + 4, R1);
+        build(R2, buf[t & 1]);
+        __syncthreads();
+        fetch(t + 5, R2);
+        build(R0, buf[(t + 1) & 1]);
+        __syncthreads();
+    }
+    if (t < T - 1) {
+        build(R1, buf[(t + 1) & 1]);
+        __syncthreads();
+        ++t;
+    }
+    if (t < T - 1) {
+        build(R2, buf[(t + 1) & 1]);
+        __syncthreads();
+        ++t;
+    }
+    __syncthreads();
+}
+
 // stage 1: partial[g][idx] = Σ_{c in group g} slab[c][idx] (contiguous chunk ranges, fixed order)
 __global__ void k_wgrad_reduce1(ReduceArgs a, float* partial, int groups) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -836,6 +1023,21 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hip
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, hipStream_t st) {
+    const dim3 g(wgs), b(kWsThreads);
+#define SPW_WS(KX, NY, YR, MK)                                                                   \
+    if (kx_pad == KX && ny_pad == NY && yrow == YR && (mask != 0) == MK) {                     \
+        hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK>), g, b, 0, st, a);                      \
+        return hipGetLastError();                                                              \
+    }
+    SPW_WS(160, 160, 0, false)
+    SPW_WS(160, 160, 1, false)
+    SPW_WS(128, 160, 0, true)
+    SPW_WS(160, 128, 0, true)
+    SPW_WS(128, 128, 0, true)
+#undef SPW_WS
+    return hipErrorInvalidValue;
 }
 hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st) {
     const int n = a.kx_pad * a.ny_pad;
