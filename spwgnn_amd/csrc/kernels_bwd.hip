@@ -10,6 +10,7 @@
 //   k_enc_edge_bwd   dc_r = dA·W1aᵀ → rm backward chain (dz4..dz1, pre-activation grads)
 //   k_enc_node_bwd   dc_o → om backward chain
 #include "kernels.h"
+#include <cstdlib>
 
 namespace spw {
 
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // Node side of one backward step in split-bf16 math: the k_node_bwd chain on tgemm_x6, two 32-node
 // column tiles per wave (one wave per SIMD).
 template <int NC>
-__global__ __launch_bounds__(256, 1) void k_node_bwd_x6(NodeBwdArgs a) {
+__global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
     if (nb0 * 32 >= a.n_nodes) return;
@@ -617,7 +618,7 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 // dh1pre = dh1 ⊙ [h1 > 0] goes to dA (plain stores on the first backward step, atomics after)
 // and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
 // 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
-template <bool ACCUM>
+template <bool ACCUM, int DBG = 0>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
     constexpr int PF = 1, kWaves = 8;
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
@@ -760,7 +761,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
                 for (int r = 8 * s; r < 8 * s + 8; ++r) {
                     float* p = dArow + rho(r, h) * kLdE + 32 * t;
-                    if (ACCUM) unsafeAtomicAdd(p, acc[t][r]);
+                    if constexpr (DBG == 1) {
+                    } else if (ACCUM) unsafeAtomicAdd(p, acc[t][r]);
                     else *p = acc[t][r];
                 }
             }
@@ -787,7 +789,13 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
     if (math == MATH_X6 && a.nw_max <= 16) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
-        if (a.dA_accumulate)
+        static const int dbg = getenv("SPWGNN_EBWD_DBG") ? atoi(getenv("SPWGNN_EBWD_DBG")) : 0;
+        if (dbg == 1) {
+            if (a.dA_accumulate)
+                hipLaunchKernelGGL((k_edge_bwd_x6<true, 1>), g, b, 0, st, a);
+            else
+                hipLaunchKernelGGL((k_edge_bwd_x6<false, 1>), g, b, 0, st, a);
+        } else if (a.dA_accumulate)
             hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
         else
             hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
