@@ -50,13 +50,13 @@ struct Ws {
     int64_t DH2_at(int s) const { return DH2 + (int64_t)s * NB * kCmBlk; }
 };
 
-static constexpr int kMaxChunks = 1024;
+static constexpr int kMaxChunks = 256;   // slabs per weight gradient (the ws kernels: one per CU)
+static constexpr int kWgSlots = kMaxReduce; // weight gradients per backward, reduced by one batched launch
 static constexpr int kW2gWgs = 256;   // W2 gradient: one workgroup per CU (MI355X: 256 CUs)
 static bool getenv_flag(const char* name) {
     const char* e = getenv(name);
     return e && *e && *e != '0';
 }
-static constexpr int kReduceGroups = 32;
 
 static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     Ws w;
@@ -121,7 +121,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.dz3 = take(eCM);
         w.dz2 = take(eCM);
         w.dz1 = take(eCM);
-        w.slab_floats = (int64_t)(kMaxChunks + kReduceGroups) * 160 * 160;
+        w.slab_floats = (int64_t)kWgSlots * kMaxChunks * 160 * 160;
         w.slab = take(w.slab_floats);
     } else {
         w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = w.zmask = -1;
@@ -424,10 +424,14 @@ struct WgSpec {
     bool recompute = false;   // XM_H1 / YM_DH2 context below
 };
 
+// Each weight gradient writes its per-chunk slabs into its own slot; the ordered chunk sums of all
+// of them run as one batched launch at the end of the backward (launch_wgrad_reduce_all).
 static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, int math, hipStream_t st,
-                         const Prof* prof = nullptr) {
+                         ReduceBatch& rb, const Prof* prof = nullptr) {
     const Ws& w = c.w;
     if (g.rows <= 0) return SPWGNN_OK;
+    if (rb.n >= kWgSlots) return SPWGNN_E_ARG;
+    float* const slab = c.f(w.slab) + (int64_t)rb.n * kMaxChunks * 160 * 160;
     int64_t chunks = (g.rows + 32 * 16 - 1) / (32 * 16);
     chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, kMaxChunks));
     int64_t rpc = up((g.rows + chunks - 1) / chunks, 32);
@@ -453,7 +457,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     a.pos = b->pos;
     a.esrc = b->edge_src;
     a.edst = b->edge_dst;
-    a.slab = c.f(w.slab);
+    a.slab = slab;
     if (g.recompute) {
         a.A = c.f(w.A);
         a.U = c.f(w.U);
@@ -470,7 +474,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         WgWsArgs wa{};
         wa.x = g.x;
         wa.y = g.y;
-        wa.slab = c.f(w.slab);
+        wa.slab = slab;
         wa.count = g.x_count;
         wa.S = g.rows / g.x_count;
         wa.nbs = (g.x_count + 31) / 32;
@@ -504,8 +508,9 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     }
     const ParamTable& pt = param_table();
-    ReduceArgs ra{};
-    ra.slab = c.f(w.slab);
+    ReduceArgs& ra = rb.r[rb.n++];
+    ra = ReduceArgs{};
+    ra.slab = slab;
     ra.chunks = (int)chunks;
     ra.kx_pad = g.kx_pad;
     ra.ny_pad = g.ny_pad;
@@ -517,7 +522,6 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     ra.bias_off = g.tb >= 0 ? pt.t[g.tb].offset : -1;
     ra.bias_row = g.bias_row;
     ra.perm = g.perm;
-    SPW_CHECK(launch_wgrad_reduce(ra, c.f(w.slab) + (int64_t)kMaxChunks * 160 * 160, kReduceGroups, st));
     return SPWGNN_OK;
 }
 
@@ -653,25 +657,26 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.tk = tk; g.tb = tb; g.k_rows = kFE; g.k_row0 = 0; g.bias_row = kFE;
     };
     int32_t e;
+    ReduceBatch rb{};
     {   // rm.0: X = [d | 1]
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
-    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e; }
+    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
         // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
         g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, &prof))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {
@@ -683,50 +688,51 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)
         WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
         g.rows = nN; g.y_stride = 0;
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
+    SPW_CHECK(launch_wgrad_reduce_all(rb, st));
     return SPWGNN_OK;
 }
 

@@ -201,6 +201,11 @@ struct ReduceArgs {
     int perm;              // 1: omp.1 column permutation (slab col f' → tensor col wo2_perm(f'))
 };
 
+constexpr int kMaxReduce = 16;
+struct ReduceBatch {       // the weight gradients of one backward, reduced in one launch (blockIdx.y)
+    ReduceArgs r[kMaxReduce];
+    int n;
+};
 struct BceArgs {
     const float *logits, *targets;
     int64_t n;
@@ -231,7 +236,7 @@ enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, hipStream_t st);
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hipStream_t st);
-hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st);
+hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);

@@ -891,30 +891,31 @@ void k_wgrad_ws(WgWsArgs a) {
     __syncthreads();
 }
 
-// stage 1: partial[g][idx] = Σ_{c in group g} slab[c][idx] (contiguous chunk ranges, fixed order)
-__global__ void k_wgrad_reduce1(ReduceArgs a, float* partial, int groups) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int n = a.kx_pad * a.ny_pad;
-    if (idx >= n) return;
-    const int g = blockIdx.y;
-    const int per = (a.chunks + groups - 1) / groups;
-    const int c0 = g * per, c1 = min(a.chunks, c0 + per);
-    float s = 0.f;
-    for (int c = c0; c < c1; ++c) s += a.slab[(int64_t)c * n + idx];
-    partial[(int64_t)g * n + idx] = s;
-}
-
-__global__ void k_wgrad_reduce(ReduceArgs a) {
+// dW = Σ_c slab[c] in chunk order (deterministic), scattered into the Keras tensors (kernel rows,
+// bias row, omp.1 column permutation); blockIdx.y selects the weight gradient of the batch.
+__global__ void k_wgrad_reduce_all(ReduceBatch rb) {
+    const ReduceArgs& a = rb.r[blockIdx.y];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.kx_pad * a.ny_pad) return;
     const int k = idx / a.ny_pad, n = idx - k * a.ny_pad;
-    const int64_t stride = (int64_t)a.kx_pad * a.ny_pad;
-    float s = 0.f;
-    for (int c = 0; c < a.chunks; ++c) s += a.slab[c * stride + idx];
-    int col = a.perm ? wo2_perm(n) : n;
+    const int col = a.perm ? wo2_perm(n) : n;
     if (col < 0 || col >= a.kernel_cols) return;
-    if (a.kernel_off >= 0 && k < a.kernel_rows) a.out[a.kernel_off + (int64_t)(a.kernel_row0 + k) * a.kernel_cols + col] = s;
-    if (a.bias_off >= 0 && k == a.bias_row) a.out[a.bias_off + col] = s;
+    const bool kern = a.kernel_off >= 0 && k < a.kernel_rows, bias = a.bias_off >= 0 && k == a.bias_row;
+    if (!kern && !bias) return;
+    const int64_t stride = (int64_t)a.kx_pad * a.ny_pad;
+    const float* p = a.slab + idx;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // four interleaved partial sums, fixed order
+    int c = 0;
+    for (; c + 4 <= a.chunks; c += 4) {
+        s0 += p[(c + 0) * stride];
+        s1 += p[(c + 1) * stride];
+        s2 += p[(c + 2) * stride];
+        s3 += p[(c + 3) * stride];
+    }
+    for (; c < a.chunks; ++c) s0 += p[c * stride];
+    const float s = (s0 + s1) + (s2 + s3);
+    if (kern) a.out[a.kernel_off + (int64_t)(a.kernel_row0 + k) * a.kernel_cols + col] = s;
+    if (bias) a.out[a.bias_off + col] = s;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1039,17 +1040,9 @@ hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, i
 #undef SPW_WS
     return hipErrorInvalidValue;
 }
-hipError_t launch_wgrad_reduce(const ReduceArgs& a, float* partial, int groups, hipStream_t st) {
-    const int n = a.kx_pad * a.ny_pad;
-    if (groups > 1 && a.chunks > groups) {
-        hipLaunchKernelGGL(k_wgrad_reduce1, dim3((n + 255) / 256, groups), dim3(256), 0, st, a, partial, groups);
-        ReduceArgs b = a;
-        b.slab = partial;
-        b.chunks = groups;
-        hipLaunchKernelGGL(k_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, st, b);
-    } else {
-        hipLaunchKernelGGL(k_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, st, a);
-    }
+hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {
+    if (rb.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_wgrad_reduce_all, dim3((160 * 160 + 255) / 256, rb.n), dim3(256), 0, st, rb);
     return hipGetLastError();
 }
 hipError_t launch_bce(const BceArgs& a, hipStream_t st) {
