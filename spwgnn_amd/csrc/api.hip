@@ -297,6 +297,11 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.b_om1 = c.pk(PB_OM1);
     en.w1b = c.pk(PK_W1B);
     en.w1c = c.pk(PK_W1C);
+    if (r->math == MATH_X6) {
+        en.x_om1 = c.x6(X6_OM1);
+        en.x_w1b = c.x6(X6_W1B);
+        en.x_w1c = c.x6(X6_W1C);
+    }
     en.zo1 = c.f(w.zo1);
     en.co = c.f(w.co);
     en.P0 = c.f(w.P_at(0));
@@ -306,7 +311,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.thresh = thresh;
     en.scale = scale;
     en.seed = r->seed;
-    SPW_CHECK(launch_enc_node(en, st));
+    SPW_CHECK(launch_enc_node(en, r->math, st));
 
     EncEdgeArgs ee{};
     ee.n_eblocks = b->n_eblocks;

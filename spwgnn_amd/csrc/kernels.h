@@ -31,6 +31,7 @@ enum X6Id : int {
     X6_W2, X6_W2T,                                // edge side (LDS B operands)
     X6_W3A, X6_WO1C, X6_WO1A, X6_WO1P, X6_WO2, X6_W1B, X6_W1C,   // node side
     X6_W1BT, X6_W1CT, X6_WO2T, X6_WO1PT, X6_WO1CT, X6_WO1AT, X6_W3T,   // its backward
+    X6_OM1,                                       // object encoder
     X6_COUNT
 };
 // (image, fp32 pack, output tiles, k-blocks, kh) — the images every x6 run builds
@@ -44,7 +45,7 @@ constexpr X6Spec kX6Specs[X6_COUNT] = {
     {X6_W1B, PK_W1B, 5, 7, 0},     {X6_W1C, PK_W1C, 5, 7, 0},
     {X6_W1BT, PK_W1BT, 4, 10, kKhE}, {X6_W1CT, PK_W1CT, 4, 10, kKhE}, {X6_WO2T, PK_WO2T, 4, 7, 0},
     {X6_WO1PT, PK_WO1PT, 4, 7, 0}, {X6_WO1CT, PK_WO1CT, 4, 7, 0}, {X6_WO1AT, PK_WO1AT, 4, 7, 0},
-    {X6_W3T, PK_W3T, 5, 7, 0},
+    {X6_W3T, PK_W3T, 5, 7, 0},     {X6_OM1, PK_OM1, 4, 7, 0},
 };
 struct X6Desc {
     const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
@@ -66,6 +67,7 @@ struct EncNodeArgs {
     const int32_t* node_tower;
     const int32_t* node_local;
     const float *w_om0, *b_om0, *w_om1, *b_om1, *w1b, *w1c;
+    const uint4 *x_om1, *x_w1b, *x_w1c;   // x6 images (x6 math)
     float *zo1, *co, *P0, *U0, *V0;
     int dropout_on;
     uint32_t thresh;
@@ -223,7 +225,7 @@ struct AdamArgs {
 
 // Host launchers (defined next to their kernels; each returns hipGetLastError()).
 hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st);
-hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st);
+hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st);
 hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st);
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st);

@@ -126,6 +126,65 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     store_cm<5>(a.V0 + bE, U, lane, valid);
 }
 
+// The om encoder in split-bf16 math: the k_enc_node chain on tchain_x6 (one 32-node column tile per
+// wave, two waves per SIMD).
+__global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int n = nb * 32 + j;
+    if (nb * 32 >= a.n_nodes) return;
+    const bool valid = n < a.n_nodes;
+    const int nc = valid ? n : a.n_nodes - 1;
+    const float4 p = reinterpret_cast<const float4*>(a.pos)[nc];
+    const float o0 = p.y, o1 = p.z;  // Networks.py:155-161: (y, width)
+    f32x16 Z[1][4], C[1][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * t;
+            Z[0][t][r] = relu(dense2(o0, o1, a.w_om0[f], a.w_om0[128 + f], a.b_om0[f]));
+        }
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;   // chunk-major node blocks
+    if (a.zo1) store_cm<4>(a.zo1 + bN, Z[0], lane, valid);
+    zero_tiles(C[0]);
+    tchain_x6<4, 7, 4, 1>(Z, C, a.x_om1, lane);
+    bias_act_rho<4, true>(C[0], a.b_om1, h);  // relu(om(.)) — Networks.py:166
+    if (a.dropout_on) {                       // Networks.py:168
+        const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                C[0][t][r] = drop_keep(key, (uint32_t)f, a.thresh) ? C[0][t][r] * a.scale : 0.f;
+            }
+    }
+    store_cm<4>(a.co + bN, C[0], lane, valid);
+    // P0: the 'propagation' input (Networks.py:119,169), ld 100 → workspace ld 128 (Z's registers)
+    f32x16 (&P)[1][4] = Z;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.prop && f0 < kFN && valid) v = *reinterpret_cast<const float4*>(a.prop + (int64_t)n * kFN + f0);
+            P[0][t][4 * q] = v.x;
+            P[0][t][4 * q + 1] = v.y;
+            P[0][t][4 * q + 2] = v.z;
+            P[0][t][4 * q + 3] = v.w;
+        }
+    store_cm<4>(a.P0 + bN, P[0], lane, valid);
+    f32x16 U[1][5];
+    zero_tiles(U[0]);
+    tchain_x6<5, 7, 4, 1>(P, U, a.x_w1b, lane);
+    store_cm<5>(a.U0 + bE, U[0], lane, valid);
+    zero_tiles(U[0]);
+    tchain_x6<5, 7, 4, 1>(P, U, a.x_w1c, lane);
+    store_cm<5>(a.V0 + bE, U[0], lane, valid);
+}
+
 // ------------------------------------------------------------------------------------------------
 // rm encoder (transposed orientation, one 32-edge block per wave): d = pos[r]-pos[s] (2 feats)
 // → 150 → 150 → 150 → 150 (+relu, dropout) = c_r; A = c_r·W1a + b1 (step-invariant first-layer
@@ -976,8 +1035,12 @@ hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_prep_weights, dim3(32, PK_COUNT), dim3(256), 0, st, a);
     return hipGetLastError();
 }
-hipError_t launch_enc_node(const EncNodeArgs& a, hipStream_t st) {
+hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
+    if (math == MATH_X6) {
+        hipLaunchKernelGGL(k_enc_node_x6, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_enc_node, dim3((waves + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
