@@ -118,6 +118,14 @@ __device__ __forceinline__ uint32_t writelane_imm(uint32_t val, int ln, uint32_t
     return r;
 }
 
+// The same without the wait state, for batches: every SGPR it reads must have been written several
+// instructions earlier (a group of ballots, a sched_barrier, then the group's writelanes).
+__device__ __forceinline__ uint32_t writelane_imm_batched(uint32_t val, int ln, uint32_t old) {
+    uint32_t r;
+    asm volatile("v_writelane_b32 %0, %1, %2" : "=v"(r) : "s"(val), "i"(ln), "0"(old));
+    return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Dropout key (our own counter-based RNG; Keras' TF draws cannot be reproduced — DESIGN.md §6).
 // keep(seed, kind, tower, a, b, feature) = mix(...) >= rate·2^32.  Restated bit-exactly in

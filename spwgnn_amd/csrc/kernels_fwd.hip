@@ -9,6 +9,7 @@
 //                    readout, next-step U/V (Networks.py:178-186)
 #include <type_traits>
 #include "kernels.h"
+#include <cstdlib>
 
 namespace spw {
 
@@ -870,7 +871,7 @@ struct NodeSum16X6 {
 
 // Wave-tiles of ≤ 16 nodes: 8 waves (2 per SIMD, 256 registers: the 16-node sum and a one-k-block
 // ring); up to 32 nodes: 4 waves (1 per SIMD) with a 5-k-block ring.
-template <bool NW16>
+template <bool NW16, int DBG = 0>
 __global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? 1 : 5;
@@ -888,7 +889,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     struct Src { const float* A; const float4 *U, *V; };
     auto src_of = [&](int blk, int2 sd, int n0) {
         const int sc = sd.x >= 0 ? sd.x : n0, dc = sd.x >= 0 ? sd.y : n0;
-        return Src{a.A + (int64_t)blk * kCmBlk + h * 128 + i * 4,
+        return Src{a.A + (int64_t)(DBG == 1 ? (blk & 7) : blk) * kCmBlk + h * 128 + i * 4,
                    reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128),
                    reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128)};
     };
@@ -956,7 +957,13 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
             ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
             ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
-            if (mrow) {   // h1 > 0 bits of the block's real chunks
+            if (mrow) {   // h1 > 0 bits of the block's real chunks (ballots first, then the writelanes)
+                uint64_t bal[2][4];
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) bal[c][f] = __ballot(xv[4 * c + f] > 0.f);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const int q = 2 * kb + c;
@@ -964,9 +971,8 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                         uint32_t stg = 0u;
 #pragma unroll
                         for (int f = 0; f < 4; ++f) {
-                            const uint64_t bal = __ballot(xv[4 * c + f] > 0.f);
-                            stg = writelane_imm((uint32_t)bal, f, stg);
-                            stg = writelane_imm((uint32_t)(bal >> 32), 4 + f, stg);
+                            stg = writelane_imm_batched((uint32_t)bal[c][f], f, stg);
+                            stg = writelane_imm_batched((uint32_t)(bal[c][f] >> 32), 4 + f, stg);
                         }
                         if (lane < 8) mrow[m1off + 4 * q] = stg;
                     }
@@ -1000,11 +1006,18 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
 #pragma unroll
             for (int t = 0; t < 5; ++t)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const uint64_t bal = __ballot(acc[t][r] > 0.f);
-                    const int w0 = t * 32 + rho(r, 0), w1 = t * 32 + rho(r, 1);
-                    mw2[w0 >> 6] = writelane_imm((uint32_t)bal, w0 & 63, mw2[w0 >> 6]);
-                    mw2[w1 >> 6] = writelane_imm((uint32_t)(bal >> 32), w1 & 63, mw2[w1 >> 6]);
+                for (int r0 = 0; r0 < 16; r0 += 8) {   // 8 ballots, then their 16 writelanes
+                    uint64_t bal[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) bal[r] = __ballot(acc[t][r0 + r] > 0.f);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const int w0 = t * 32 + rho(r0 + r, 0), w1 = t * 32 + rho(r0 + r, 1);
+                        mw2[w0 >> 6] = writelane_imm_batched((uint32_t)bal[r], w0 & 63, mw2[w0 >> 6]);
+                        mw2[w1 >> 6] = writelane_imm_batched((uint32_t)(bal[r] >> 32), w1 & 63, mw2[w1 >> 6]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             m2row[lane] = mw2[0];
             m2row[64 + lane] = mw2[1];
@@ -1067,7 +1080,10 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
     if (math == MATH_X6) {
-        if (a.nw_max <= 16)
+        static const int dbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;
+        if (a.nw_max <= 16 && dbg == 1)   // diagnosis: A rows from 8 cached blocks
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 1>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+        else if (a.nw_max <= 16)
             hipLaunchKernelGGL(k_edge_fwd_x6<true>, dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL(k_edge_fwd_x6<false>, dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);
