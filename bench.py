@@ -123,8 +123,8 @@ def cpu_baseline(n_objects: int, S: int, seconds: float, threads=None):
 PMC_NAMES = {
     "f32": {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true, true>", "enc_edge": "k_enc_edge<true>",
             "enc_edge_bwd": "k_enc_edge_bwd", "wgrad_w2": "k_wgrad_t<4, 2, 160, 160>"},
-    "x6": {"edge_fwd": "k_edge_fwd_x6<true>", "edge_bwd": "k_edge_bwd_x6<true>", "enc_edge": "k_enc_edge_x6<true, 2>",
-           "enc_edge_bwd": "k_enc_edge_bwd_x6<2>", "wgrad_w2": "k_wgrad_x6<4, 2, 160, 160, 1>"},
+    "x6": {"edge_fwd": "k_edge_fwd_x6<true, 0>", "edge_bwd": "k_edge_bwd_x6<true, 0>",
+           "enc_edge": "k_enc_edge_x6<true, 2>", "enc_edge_bwd": "k_enc_edge_bwd_x6<2>", "wgrad_w2": "k_w2grad_ws<0>"},
 }
 
 

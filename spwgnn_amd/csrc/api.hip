@@ -24,7 +24,7 @@ struct Ws {
     int64_t dA, dz4, dz3, dz2, dz1;                  // edge (bwd)
     int64_t H1, DH2;                                 // per step: h1 (fwd) and dh2pre (bwd) rows for the W2 gradient
     int64_t slab, bce;
-    int64_t slab_floats;
+    int64_t slab_floats, slot_floats;   // weight-gradient slabs: kWgSlots slots of slot_floats
     PackSlots ps;
     int64_t x6;                                      // split-bf16 weight images (uint4 units below)
     int64_t x6off[X6_COUNT];
@@ -121,13 +121,18 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.dz3 = take(eCM);
         w.dz2 = take(eCM);
         w.dz1 = take(eCM);
-        w.slab_floats = (int64_t)kWgSlots * kMaxChunks * 160 * 160;
+        // a slot holds ≥ 256 160×160 slabs (one per CU for the ws kernels) and up to 1024 for the
+        // row-chunked kernels of large batches (chunks of ≥ 512 rows)
+        const int64_t rows = std::max(w.RE, w.RN) * S;
+        const int64_t slot_chunks = std::min<int64_t>(1024, std::max<int64_t>(kMaxChunks, (rows + 511) / 512));
+        w.slot_floats = slot_chunks * 160 * 160;
+        w.slab_floats = (int64_t)kWgSlots * w.slot_floats;
         w.slab = take(w.slab_floats);
     } else {
         w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = w.zmask = -1;
         w.dx = w.do1 = w.g = w.G3 = w.dU = w.dV = w.dP = w.dco = w.dzo2 = w.dzo1 = -1;
         w.dA = w.dz4 = w.dz3 = w.dz2 = w.dz1 = w.slab = w.H1 = w.DH2 = -1;
-        w.slab_floats = 0;
+        w.slab_floats = w.slot_floats = 0;
     }
     w.total = cur * 4;
     return w;
@@ -436,9 +441,11 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     const Ws& w = c.w;
     if (g.rows <= 0) return SPWGNN_OK;
     if (rb.n >= kWgSlots) return SPWGNN_E_ARG;
-    float* const slab = c.f(w.slab) + (int64_t)rb.n * kMaxChunks * 160 * 160;
+    float* const slab = c.f(w.slab) + (int64_t)rb.n * w.slot_floats;
+    // the row-chunked kernels: up to 1024 chunks of ≥ 512 rows, as many as the slot holds
+    const int64_t slot_chunks = w.slot_floats / ((int64_t)g.kx_pad * g.ny_pad);
     int64_t chunks = (g.rows + 32 * 16 - 1) / (32 * 16);
-    chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, kMaxChunks));
+    chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, std::min<int64_t>(1024, slot_chunks)));
     int64_t rpc = up((g.rows + chunks - 1) / chunks, 32);
     chunks = (g.rows + rpc - 1) / rpc;
     WgradArgs a{};
