@@ -132,7 +132,7 @@ def load_pmc(kernel: str, math: str = "x6"):
     """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) from the committed PMC
     summary, or None when absent."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    name = PMC_NAMES[math].get(kernel)
+    name = PMC_NAMES.get(math, {}).get(kernel)
     if name is None or not os.path.exists(path):
         return None
     try:
@@ -181,7 +181,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the f32-math reference measurement")
-    ap.add_argument("--math", default="x6", choices=["x6", "f32"],
+    ap.add_argument("--math", default="x6", choices=["x6", "f32", "bf16"],
                     help="matrix-product arithmetic (spwgnn.h SPWGNN_MATH_*)")
     ap.add_argument("--infer", action="store_true",
                     help="BASELINE config 5: forward-only inference replayed from a hipGraph "
@@ -249,7 +249,7 @@ def main():
     # roofline of the timed kernel: its algorithmic fp32 FLOPs against the matrix peak of the math
     # it runs in (x6: bf16 peak / 6), and its PMC HBM bytes against 8 TB/s; the bound is the
     # larger fraction
-    mpeak = PEAK_X6_TFLOPS if args.math == "x6" else PEAK_FP32_TFLOPS
+    mpeak = {"x6": PEAK_X6_TFLOPS, "f32": PEAK_FP32_TFLOPS, "bf16": PEAK_BF16_TFLOPS}[args.math]
     traffic = load_pmc(args.roofline_kernel, args.math)
     m_frac = achieved / mpeak
     h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
@@ -264,8 +264,8 @@ def main():
                  "launches": nl, "flop_per_launch": kflops, "mfma_tflops": round(achieved, 2),
                  "mfma_peak": round(mpeak, 1), "mfma_frac": round(m_frac, 4),
                  "hbm_gbs": round(h_gbs, 1) if h_gbs else None, "hbm_frac": round(h_frac, 4) if h_frac else None,
-                 "peak_note": ("x6: fp32 products as 6 bf16 MFMA products, peak = 2.5 PF bf16 / 6"
-                               if args.math == "x6" else "f32 MFMA peak")})
+                 "peak_note": {"x6": "x6: fp32 products as 6 bf16 MFMA products, peak = 2.5 PF bf16 / 6",
+                               "f32": "f32 MFMA peak", "bf16": "bf16 MFMA dense peak"}[args.math]})
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -277,9 +277,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "math": ("x6: each fp32 matrix product as 6 bf16 MFMA products of 3-way split operands, fp32 "
-                 "accumulation (DESIGN.md §3b)" if args.math == "x6" else "f32 MFMA"),
+        "dtype": "bf16" if args.math == "bf16" else "f32",
+        "math": {"x6": "x6: each fp32 matrix product as 6 bf16 MFMA products of 3-way split operands, fp32 "
+                       "accumulation (DESIGN.md §3b)", "f32": "f32 MFMA",
+                 "bf16": "bf16: operands rounded to bf16, one bf16 MFMA product, fp32 accumulation"}[args.math],
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
         "config": {"workload": f"train step fwd+BCE+bwd+{'allreduce+' if world > 1 else ''}Adam, "
                                f"{N}-block towers fully connected (E={N*(N-1)}), {B} towers/GPU, "
@@ -292,18 +293,22 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and args.math == "x6" and not args.no_f32_leg:
-        # the same step in f32 MFMA math, for reference (the other SPWGNN_MATH_* mode)
-        tr32 = Trainer(params.clone(), mp_steps=S, dropout=args.dropout, seed=7, math="f32")
-        for _ in range(2):
-            tr32.step(batch, target)
-        torch.cuda.synchronize()
-        k32 = max(3, args.steps // 2)
-        t1 = time.perf_counter()
-        for _ in range(k32):
-            tr32.step(batch, target)
-        torch.cuda.synchronize()
-        e32 = time.perf_counter() - t1
-        out["f32_math"] = {"value": round(B * k32 / e32, 1), "ms_per_step": round(e32 / k32 * 1e3, 3), "steps": k32}
+        # the same step in the other SPWGNN_MATH_* modes, for reference: f32 MFMA (fp32-class like
+        # x6) and bf16 (operands rounded to bf16, one product — BASELINE configs 3-4's arithmetic)
+        for m in ("f32", "bf16"):
+            trm = Trainer(params.clone(), mp_steps=S, dropout=args.dropout, seed=7, math=m)
+            for _ in range(2):
+                trm.step(batch, target)
+            torch.cuda.synchronize()
+            km = max(3, args.steps // 2)
+            t1 = time.perf_counter()
+            for _ in range(km):
+                trm.step(batch, target)
+            torch.cuda.synchronize()
+            em = time.perf_counter() - t1
+            out[f"{m}_math"] = {"value": round(B * km / em, 1), "ms_per_step": round(em / km * 1e3, 3), "steps": km}
+            del trm
+            torch.cuda.empty_cache()
     out["hbm"] = step_hbm(out["ms_per_step"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_pair(N, S, args.cpu_seconds)

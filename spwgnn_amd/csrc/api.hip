@@ -4,7 +4,8 @@
 #include <cstdlib>
 #include "kernels.h"
 #include "../../include/spwgnn.h"
-static_assert(SPWGNN_MATH_F32 == spw::MATH_F32 && SPWGNN_MATH_X6 == spw::MATH_X6, "math ids");
+static_assert(SPWGNN_MATH_F32 == spw::MATH_F32 && SPWGNN_MATH_X6 == spw::MATH_X6 && SPWGNN_MATH_BF16 == spw::MATH_BF16,
+              "math ids");
 
 namespace spw {
 
@@ -218,13 +219,13 @@ static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
     if (r->mp_steps < 1 || r->mp_steps > 64) return SPWGNN_E_SHAPE;
     if (!b->pos || !b->wtile || !b->edge_src || !b->edge_dst || !b->blk_csr) return SPWGNN_E_ARG;
     if (r->dropout < 0.f || r->dropout >= 1.f) return SPWGNN_E_ARG;
-    if (r->math != SPWGNN_MATH_F32 && r->math != SPWGNN_MATH_X6) return SPWGNN_E_ARG;
+    if (r->math != SPWGNN_MATH_F32 && r->math != SPWGNN_MATH_X6 && r->math != SPWGNN_MATH_BF16) return SPWGNN_E_ARG;
     if (r->training && r->dropout > 0.f && (!b->node_tower || !b->node_local)) return SPWGNN_E_ARG;
     return SPWGNN_OK;
 }
 
 // Per-kernel x6 selection for A/B diagnosis: SPWGNN_X6_KERNELS (bit mask of kX6*, default all)
-// narrows math == MATH_X6 to some kernels; the others run in f32 math.
+// narrows math == MATH_X6 (or MATH_BF16) to some kernels; the others run in f32 math.
 enum : int { kX6EncEdge = 1, kX6EdgeFwd = 2, kX6NodeFwd = 4, kX6NodeBwd = 8, kX6EdgeBwd = 16, kX6EncEdgeBwd = 32,
              kX6Wgrad = 64 };
 static int kmath(const spwgnn_run* r, int bit) {
@@ -232,7 +233,7 @@ static int kmath(const spwgnn_run* r, int bit) {
         const char* e = getenv("SPWGNN_X6_KERNELS");
         return e ? (int)strtol(e, nullptr, 0) : -1;
     }();
-    return (r->math == MATH_X6 && (mask & bit)) ? MATH_X6 : MATH_F32;
+    return (r->math != MATH_F32 && (mask & bit)) ? r->math : MATH_F32;
 }
 
 struct Prof {
@@ -270,7 +271,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     SPW_CHECK(hipMemcpy2DAsync(c.f(w.pk + w.ps.off[PK_W3A] + ((150 / 4) * kLdN) * 4 + 150 % 4), 4 * sizeof(float),
                                params + param_table().t[T_RMP2B].offset, sizeof(float), sizeof(float), 100,
                                hipMemcpyDeviceToDevice, st));
-    if (r->math == MATH_X6) {   // after the W3A bias row: the images are split from the packs
+    if (r->math != MATH_F32) {   // after the W3A bias row: the images are split from the packs
         PrepX6Args xa{};
         xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
         for (int id = 0; id < X6_COUNT; ++id) {
@@ -302,7 +303,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.b_om1 = c.pk(PB_OM1);
     en.w1b = c.pk(PK_W1B);
     en.w1c = c.pk(PK_W1C);
-    if (r->math == MATH_X6) {
+    if (r->math != MATH_F32) {
         en.x_om1 = c.x6(X6_OM1);
         en.x_w1b = c.x6(X6_W1B);
         en.x_w1c = c.x6(X6_W1C);
@@ -335,7 +336,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.b_rm3 = c.pk(PB_RM3);
     ee.w_w1a = c.pk(PK_W1A);
     ee.b_w1a = c.pk(PB_W1A);
-    if (r->math == MATH_X6) {
+    if (r->math != MATH_F32) {
         ee.x_rm1 = c.x6(X6_RM1);
         ee.x_rm2 = c.x6(X6_RM2);
         ee.x_rm3 = c.x6(X6_RM3);
@@ -374,7 +375,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.V = c.f(w.V_at(s));
         ef.w2 = c.pk(PK_W2);
         ef.b2 = c.pk(PB_W2);
-        ef.x_w2 = r->math == MATH_X6 ? c.x6(X6_W2) : nullptr;
+        ef.x_w2 = r->math != MATH_F32 ? c.x6(X6_W2) : nullptr;
         ef.H2s = c.f(w.H2s_at(s));
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
@@ -403,7 +404,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         nf.w1c = c.pk(PK_W1C);
         nf.bo1 = c.pk(PB_O1);
         nf.bo2p = c.pk(PB_O2P);
-        if (r->math == MATH_X6) {
+        if (r->math != MATH_F32) {
             nf.x_w3a = c.x6(X6_W3A);
             nf.x_wo1c = c.x6(X6_WO1C);
             nf.x_wo1a = c.x6(X6_WO1A);
@@ -481,7 +482,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.S = (int)(g.rows / w.RE);
     }
     // stored chunk-major operands in x6 math: the warp-specialized kernel, one workgroup per CU
-    if (math == MATH_X6 && g.xmode == XM_CM && (g.ymode == YM_CM || g.ymode == YM_ROW) &&
+    if (math != MATH_F32 && g.xmode == XM_CM && (g.ymode == YM_CM || g.ymode == YM_ROW) &&
         !getenv_flag("SPWGNN_WG_OLD")) {
         WgWsArgs wa{};
         wa.x = g.x;
@@ -500,11 +501,11 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         chunks = wgs;
         const bool mask = !(g.kx_pad == 160 && g.ny_pad == 160);   // node arrays: rows ≥ count masked
         if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
-        SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, st));
+        SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, math, st));
         if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     } else {
     // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
-    const bool ws = g.recompute && math == MATH_X6 && !getenv_flag("SPWGNN_W2G_OLD");
+    const bool ws = g.recompute && math != MATH_F32 && (math == MATH_BF16 || !getenv_flag("SPWGNN_W2G_OLD"));
     int64_t bpw = 0;
     if (ws) {
         const int64_t nblk = w.RE / 32;
@@ -514,7 +515,9 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     }
     if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
     if (ws)
-        SPW_CHECK(launch_w2grad_ws(a, (int)chunks, bpw, st));
+        SPW_CHECK(launch_w2grad_ws(a, (int)chunks, bpw, math, st));
+    else if (math == MATH_BF16)
+        SPW_CHECK(launch_wgrad_bf16(a, (int)chunks, st));
     else
         SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
@@ -574,7 +577,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         nb.wo1at = c.pk(PK_WO1AT);
         nb.wo1pt = c.pk(PK_WO1PT);
         nb.w3t = c.pk(PK_W3T);
-        if (r->math == MATH_X6) {
+        if (r->math != MATH_F32) {
             nb.x_w1bt = c.x6(X6_W1BT);
             nb.x_w1ct = c.x6(X6_W1CT);
             nb.x_wo2t = c.x6(X6_WO2T);
@@ -601,7 +604,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.dh2_out = nullptr;  // the W2 gradient recomputes dh2pre (YM_DH2)
         eb.G3 = c.f(w.G3_at(s));
         eb.w2t = c.pk(PK_W2T);
-        eb.x_w2t = r->math == MATH_X6 ? c.x6(X6_W2T) : nullptr;
+        eb.x_w2t = r->math != MATH_F32 ? c.x6(X6_W2T) : nullptr;
         eb.dA = c.f(w.dA);
         eb.dU = c.f(w.dU_at(s));
         eb.dV = c.f(w.dV_at(s));
@@ -620,7 +623,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         nb.dprop = dprop;
         nb.w1bt = c.pk(PK_W1BT);
         nb.w1ct = c.pk(PK_W1CT);
-        if (r->math == MATH_X6) {
+        if (r->math != MATH_F32) {
             nb.x_w1bt = c.x6(X6_W1BT);
             nb.x_w1ct = c.x6(X6_W1CT);
         }
@@ -634,7 +637,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     eeb.rm3t = c.pk(PK_RM3T);
     eeb.rm2t = c.pk(PK_RM2T);
     eeb.rm1t = c.pk(PK_RM1T);
-    if (r->math == MATH_X6) {
+    if (r->math != MATH_F32) {
         eeb.x_w1at = c.x6(X6_W1AT);
         eeb.x_rm3t = c.x6(X6_RM3T);
         eeb.x_rm2t = c.x6(X6_RM2T);

@@ -58,8 +58,11 @@ __device__ __forceinline__ bf16x8 as_bf16x8(i16x4 lo, i16x4 hi) {
     return __builtin_bit_cast(bf16x8, v);
 }
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
-// acc += a·b over the six split products (a[p], b[p]: parts h, m, l); small terms first
+// acc += a·b over the six split products (a[p], b[p]: parts h, m, l); small terms first.
+// NP = 1 is the bf16 math (SPWGNN_MATH_BF16): the h parts alone, one product.
+template <int NP = 3>
 __device__ __forceinline__ f32x4 mfma16_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+    if constexpr (NP == 1) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
@@ -67,7 +70,9 @@ __device__ __forceinline__ f32x4 mfma16_x6(const bf16x8 (&a)[3], const bf16x8 (&
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
 }
+template <int NP = 3>
 __device__ __forceinline__ f32x16 mfma32_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+    if constexpr (NP == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);

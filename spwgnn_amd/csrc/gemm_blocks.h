@@ -319,7 +319,7 @@ constexpr int kX6Ring = 3;
 // (k_prep_x6) holds, per step u = kb·NT_OUT + T, the three matching A-operand parts of lane (i, h),
 // 16 bytes each: [u][part][lane] uint4. Steps stream through a D-deep ring of static slots (fully
 // unrolled; the loads of step u + D issue before step u's MFMAs).
-template <int NT_OUT, int NKB, int NC, int D = kX6Ring, class GetB>
+template <int NT_OUT, int NKB, int NC, int D = kX6Ring, int PARTS = 3, class GetB>
 __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
                                          int lane) {
     constexpr int NS = NKB * NT_OUT, NP = 4 * NC;   // pair-splits per k-block
@@ -362,17 +362,17 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6(a, bq[c], out[c][T]);
+        for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6<PARTS>(a, bq[c], out[c][T]);
     }
 }
 // Chain layer: B = the C layout of the previous layer; k-block kb of tile t = kb>>1 is registers
 // 8(kb&1) .. +7 of in[c][t] (element e of lane half h = feature 16kb + 8(e>>2) + 4h + (e&3): image
 // kind X6_CHAIN).
-template <int NT_OUT, int NKB, int NT_IN, int NC, int D = kX6Ring>
+template <int NT_OUT, int NKB, int NT_IN, int NC, int D = kX6Ring, int PARTS = 3>
 __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
                                           const uint4* __restrict__ img, int lane) {
     static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");
-    tgemm_x6<NT_OUT, NKB, NC, D>(
+    tgemm_x6<NT_OUT, NKB, NC, D, PARTS>(
         [&](int c, int kb, float (&v)[8]) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = in[c][kb >> 1][8 * (kb & 1) + e];

@@ -234,10 +234,12 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
-enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1 };   // = SPWGNN_MATH_* (spwgnn.h)
+enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1, MATH_BF16 = 2 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
-hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, hipStream_t st);
-hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hipStream_t st);
+hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
+                           hipStream_t st);
+hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st);
+hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st);
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 // Node side of one backward step in split-bf16 math: the k_node_bwd chain on tgemm_x6, two 32-node
 // column tiles per wave (one wave per SIMD).
-template <int NC>
+template <int NC, int NP = 3>
 __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -151,14 +151,14 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
 #pragma unroll
             for (int c = 0; c < NC; ++c) blk[c] = a.dU + bE(c);
             hr.load(blk, lane);
-            tgemm_x6<4, 10, NC>(hr, D, a.x_w1bt, lane);
+            tgemm_x6<4, 10, NC, kX6Ring, NP>(hr, D, a.x_w1bt, lane);
         }
         {
             HalfRows<kKhE, NC> hr;
 #pragma unroll
             for (int c = 0; c < NC; ++c) blk[c] = a.dV + bE(c);
             hr.load(blk, lane);
-            tgemm_x6<4, 10, NC>(hr, D, a.x_w1ct, lane);
+            tgemm_x6<4, 10, NC, kX6Ring, NP>(hr, D, a.x_w1ct, lane);
         }
     }
     if (a.tail) {  // dP0 = d/d 'propagation' (ld 100)
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
         if (has[c]) store_cm<4>(a.dx + bN(c), D[c], lane, valid[c]);
     }
     zero2(G);
-    tchain_x6<4, 7, 4, NC>(D, G, a.x_wo2t, lane);
+    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(D, G, a.x_wo2t, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 O1[4];
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // P part of omp's input → dP_s
     zero2(D);
-    tchain_x6<4, 7, 4, NC>(G, D, a.x_wo1pt, lane);
+    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1pt, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 T[4];
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // c_o part → dc_o (accumulated over steps in step order S-1..0)
     zero2(D);
-    tchain_x6<4, 7, 4, NC>(G, D, a.x_wo1ct, lane);
+    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1ct, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if (a.dco_accumulate) {
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // effect part → g = da ⊙ (1 - a²) → G3 = g·W3ᵀ
     zero2(D);
-    tchain_x6<4, 7, 4, NC>(G, D, a.x_wo1at, lane);
+    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1at, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 Aa[4];
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     f32x16 H[NC][5];
 #pragma unroll
     for (int c = 0; c < NC; ++c) zero_tiles(H[c]);
-    tchain_x6<5, 7, 4, NC>(D, H, a.x_w3t, lane);
+    tchain_x6<5, 7, 4, NC, kX6Ring, NP>(D, H, a.x_w3t, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
         if (has[c]) store_cm<5>(a.G3 + bE(c), H[c], lane, valid[c]);
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // The same backward chain in split-bf16 math: two 32-edge column tiles per wave (kernels_fwd.hip
 // k_enc_edge_x6). dA rows (row-major) are loaded whole up front as half rows (lane half h: features
 // 76h .. 76h+75, image kind kh = 76), into the registers the second layer's output uses later.
-template <int NC>
+template <int NC, int NP = 3>
 __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
             for (int q = 0; q < kKhE / 4; ++q) raw[c][q] = row[q];
             zero_tiles(D[c]);
         }
-        tgemm_x6<5, (kKhE + 7) / 8, NC, 6>(
+        tgemm_x6<5, (kKhE + 7) / 8, NC, 6, NP>(
             [&](int c, int kb, float (&v)[8]) {
                 const float4 x = raw[c][2 * kb];
                 const float4 y = 2 * kb + 1 < kKhE / 4 ? raw[c][2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -561,15 +561,15 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
     bits(3, D, a.scale);   // relu + dropout of c_r
     save(a.dz4, D);
     zero2(E);
-    tchain_x6<5, 10, 5, NC, 6>(D, E, a.x_rm3t, lane);
+    tchain_x6<5, 10, 5, NC, 6, NP>(D, E, a.x_rm3t, lane);
     bits(2, E, 1.f);
     save(a.dz3, E);
     zero2(D);
-    tchain_x6<5, 10, 5, NC, 6>(E, D, a.x_rm2t, lane);
+    tchain_x6<5, 10, 5, NC, 6, NP>(E, D, a.x_rm2t, lane);
     bits(1, D, 1.f);
     save(a.dz2, D);
     zero2(E);
-    tchain_x6<5, 10, 5, NC, 6>(D, E, a.x_rm1t, lane);
+    tchain_x6<5, 10, 5, NC, 6, NP>(D, E, a.x_rm1t, lane);
     bits(0, E, 1.f);
     save(a.dz1, E);
     (void)h;
@@ -602,6 +602,12 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
+    if (math == MATH_BF16) {
+        constexpr int NC = 2;
+        const int w2 = ((a.n_nodes + 31) / 32 + NC - 1) / NC;
+        hipLaunchKernelGGL((k_node_bwd_x6<NC, 1>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (math == MATH_X6) {
         constexpr int NC = 2;
         const int w2 = ((a.n_nodes + 31) / 32 + NC - 1) / NC;
@@ -618,7 +624,7 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 // dh1pre = dh1 ⊙ [h1 > 0] goes to dA (plain stores on the first backward step, atomics after)
 // and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
 // 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
-template <bool ACCUM, int DBG = 0>
+template <bool ACCUM, int DBG = 0, int NP = 3>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
     constexpr int PF = 1, kWaves = 8;
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 bp[0] = as_bf16x8(wp[0]);
                 bp[1] = as_bf16x8(wp[64]);
                 bp[2] = as_bf16x8(wp[128]);
-                acc[T] = mfma32_x6(ap, bp, acc[T]);
+                acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
             }
             __builtin_amdgcn_sched_barrier(0);   // no motion across k-blocks (register pressure)
         }
@@ -754,8 +760,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) split2(acc[t][8 * s + 2 * m], acc[t][8 * s + 2 * m + 1], hw[m], mw[m], lw[m]);
-                nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), nacc[t], 0, 0, 0);
-                nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), nacc[t], 0, 0, 0);
+                if constexpr (NP == 3) {
+                    nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), nacc[t], 0, 0, 0);
+                    nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), nacc[t], 0, 0, 0);
+                }
                 nacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3])), nacc[t], 0, 0, 0);
                 // dA rows of this k-block's 8 registers, issued beside the MFMAs
 #pragma unroll
@@ -787,6 +795,12 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
+    if (math == MATH_BF16 && a.nw_max <= 16) {
+        const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);
+        if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true, 0, 1>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_edge_bwd_x6<false, 0, 1>), g, b, 0, st, a);
+        return hipGetLastError();
+    }
     if (math == MATH_X6 && a.nw_max <= 16) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
         static const int dbg = getenv("SPWGNN_EBWD_DBG") ? atoi(getenv("SPWGNN_EBWD_DBG")) : 0;
@@ -816,6 +830,11 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st) {
+    if (math == MATH_BF16) {
+        constexpr int NC = 2;
+        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1>), dim3((a.n_eblocks + 4 * NC - 1) / (4 * NC)), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (math == MATH_X6) {
         constexpr int NC = 2;
         hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC>), dim3((a.n_eblocks + 4 * NC - 1) / (4 * NC)), dim3(256), 0, st, a);

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 // The om encoder in split-bf16 math: the k_enc_node chain on tchain_x6 (one 32-node column tile per
 // wave, two waves per SIMD).
+template <int NP>
 __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;   // chunk-major node blocks
     if (a.zo1) store_cm<4>(a.zo1 + bN, Z[0], lane, valid);
     zero_tiles(C[0]);
-    tchain_x6<4, 7, 4, 1>(Z, C, a.x_om1, lane);
+    tchain_x6<4, 7, 4, 1, kX6Ring, NP>(Z, C, a.x_om1, lane);
     bias_act_rho<4, true>(C[0], a.b_om1, h);  // relu(om(.)) — Networks.py:166
     if (a.dropout_on) {                       // Networks.py:168
         const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
@@ -179,10 +180,10 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     store_cm<4>(a.P0 + bN, P[0], lane, valid);
     f32x16 U[1][5];
     zero_tiles(U[0]);
-    tchain_x6<5, 7, 4, 1>(P, U, a.x_w1b, lane);
+    tchain_x6<5, 7, 4, 1, kX6Ring, NP>(P, U, a.x_w1b, lane);
     store_cm<5>(a.U0 + bE, U[0], lane, valid);
     zero_tiles(U[0]);
-    tchain_x6<5, 7, 4, 1>(P, U, a.x_w1c, lane);
+    tchain_x6<5, 7, 4, 1, kX6Ring, NP>(P, U, a.x_w1c, lane);
     store_cm<5>(a.V0 + bE, U[0], lane, valid);
 }
 
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // The rm encoder in split-bf16 math: two 32-edge blocks per wave (column tiles c), so each 16-byte
 // weight fragment feeds two MFMAs (the x6 images stream from L2 at half the per-MFMA rate);
 // 1 wave per SIMD (in + out activations: 320 registers).
-template <bool TRAIN, int NC>
+template <bool TRAIN, int NC, int NP = 3>
 __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -308,17 +309,17 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     };
     if (TRAIN) save(a.z1, a.zmask, X);
     zero2(Y);
-    tchain_x6<5, 10, 5, NC>(X, Y, a.x_rm1, lane);
+    tchain_x6<5, 10, 5, NC, kX6Ring, NP>(X, Y, a.x_rm1, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, true>(Y[c], a.b_rm1, h);
     if (TRAIN) save(a.z2, a.zmask + 3 * 64, Y);
     zero2(X);
-    tchain_x6<5, 10, 5, NC>(Y, X, a.x_rm2, lane);
+    tchain_x6<5, 10, 5, NC, kX6Ring, NP>(Y, X, a.x_rm2, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, true>(X[c], a.b_rm2, h);
     if (TRAIN) save(a.z3, a.zmask + 6 * 64, X);
     zero2(Y);
-    tchain_x6<5, 10, 5, NC>(X, Y, a.x_rm3, lane);
+    tchain_x6<5, 10, 5, NC, kX6Ring, NP>(X, Y, a.x_rm3, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         bias_act_rho<5, true>(Y[c], a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:165
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     }
     if (TRAIN) save(a.cr, a.zmask + 9 * 64, Y);
     zero2(X);
-    tchain_x6<5, 10, 5, NC>(Y, X, a.x_w1a, lane);
+    tchain_x6<5, 10, 5, NC, kX6Ring, NP>(Y, X, a.x_w1a, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, false>(X[c], a.b_w1a, h);
     save(a.A, nullptr, X);   // chunk-major; k_edge_fwd masks padding edges
@@ -637,7 +638,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // ------------------------------------------------------------------------------------------------
 // Node side of one step in split-bf16 math: the k_node_fwd chain on tgemm_x6, two 32-node column
 // tiles per wave (one wave per SIMD).
-template <int NC>
+template <int NC, int NP = 3>
 __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
         for (int c = 0; c < NC; ++c) blk[c] = a.H2s + bE(c);
         hr.load(blk, lane);
-        tgemm_x6<4, 10, NC>(hr, E, a.x_w3a, lane);
+        tgemm_x6<4, 10, NC, kX6Ring, NP>(hr, E, a.x_w3a, lane);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -685,16 +686,16 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
         for (int c = 0; c < NC; ++c) blk[c] = a.co + bN(c);
         hr.load(blk, lane);
-        tgemm_x6<4, 7, NC>(hr, O, a.x_wo1c, lane);
+        tgemm_x6<4, 7, NC, kX6Ring, NP>(hr, O, a.x_wo1c, lane);
     }
-    tchain_x6<4, 7, 4, NC>(E, O, a.x_wo1a, lane);
+    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(E, O, a.x_wo1a, lane);
     {
         HalfRows<kKhN, NC> hr;
         const float* blk[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) blk[c] = a.P + bN(c);
         hr.load(blk, lane);
-        tgemm_x6<4, 7, NC>(hr, O, a.x_wo1p, lane);
+        tgemm_x6<4, 7, NC, kX6Ring, NP>(hr, O, a.x_wo1p, lane);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -704,7 +705,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
     // X reuses E's registers: x' = o1·Wo2' + b, then P' = tanh(x' + P) into E
     f32x16 (&X)[NC][4] = E;
     zero2(X);
-    tchain_x6<4, 7, 4, NC>(O, X, a.x_wo2, lane);
+    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(O, X, a.x_wo2, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         bias_act_rho<4, false>(X[c], a.bo2p, h);
@@ -724,13 +725,13 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
         f32x16 U[NC][5];
 #pragma unroll
         for (int c = 0; c < NC; ++c) zero_tiles(U[c]);
-        tchain_x6<5, 7, 4, NC>(X, U, a.x_w1b, lane);
+        tchain_x6<5, 7, 4, NC, kX6Ring, NP>(X, U, a.x_w1b, lane);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             if (has[c]) store_cm<5>(a.U + bE(c), U[c], lane, valid[c]);
             zero_tiles(U[c]);
         }
-        tchain_x6<5, 7, 4, NC>(X, U, a.x_w1c, lane);
+        tchain_x6<5, 7, 4, NC, kX6Ring, NP>(X, U, a.x_w1c, lane);
 #pragma unroll
         for (int c = 0; c < NC; ++c)
             if (has[c]) store_cm<5>(a.V + bE(c), U[c], lane, valid[c]);
@@ -744,6 +745,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 // operand straight from the loads; W2 (x6 image, 150 KB) is the LDS B operand. The receiver sum
 // runs as one-hot [node][edge] (exact in bf16) × h2 parts: 3 MFMAs per 16 edges per feature tile.
 // 4 waves (one per SIMD: 512 registers) per CU, A/U/V prefetched kX6Pf k-blocks ahead.
+template <int NP>
 struct NodeSumX6 {
     f32x16 acc[5];
     int key;
@@ -776,8 +778,10 @@ struct NodeSumX6 {
                 uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) split2(h2[t][8 * s + 2 * m], h2[t][8 * s + 2 * m + 1], hw[m], mw[m], lw[m]);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), acc[t], 0, 0, 0);
+                if constexpr (NP == 3) {
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), acc[t], 0, 0, 0);
+                }
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3])), acc[t], 0, 0, 0);
             }
         }
@@ -803,6 +807,7 @@ struct NodeSumX6 {
 // register pair turns the 32-feature C tiles into two 16-feature B operands of 32 edges each
 // (lane group g of a swapped register = edges of (s = g&1, h = g>>1)), so a block costs 30 MFMAs of
 // 16 cycles into 40 accumulator registers.
+template <int NP>
 struct NodeSum16X6 {
     f32x4 acc[10];   // sub-tile u: features 16u + (lane & 15), nodes 4(lane >> 4) + r
     int key;
@@ -848,7 +853,7 @@ struct NodeSum16X6 {
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int p = 2; p >= 0; --p)
+                for (int p = NP - 1; p >= 0; --p)
                     acc[2 * t + u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                         ao, as_bf16x8(make_uint4(P[u][p][0], P[u][p][1], P[u][p][2], P[u][p][3])), acc[2 * t + u], 0, 0, 0);
         }
@@ -871,7 +876,7 @@ struct NodeSum16X6 {
 
 // Wave-tiles of ≤ 16 nodes: 8 waves (2 per SIMD, 256 registers: the 16-node sum and a one-k-block
 // ring); up to 32 nodes: 4 waves (1 per SIMD) with a 5-k-block ring.
-template <bool NW16, int DBG = 0>
+template <bool NW16, int DBG = 0, int NP = 3>
 __global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? 1 : 5;
@@ -917,7 +922,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     for (; wt < a.n_wtiles; wt += wstep) {
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];
-    typename std::conditional<NW16, NodeSum16X6, NodeSumX6>::type nsum;
+    typename std::conditional<NW16, NodeSum16X6<NP>, NodeSumX6<NP>>::type nsum;
     nsum.init(n0, lane);
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
@@ -985,7 +990,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                 bp[0] = as_bf16x8(wp[0]);
                 bp[1] = as_bf16x8(wp[64]);
                 bp[2] = as_bf16x8(wp[128]);
-                acc[T] = mfma32_x6(ap, bp, acc[T]);
+                acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
             }
         }
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
@@ -1051,7 +1056,11 @@ hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st) {
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
     if (math == MATH_X6) {
-        hipLaunchKernelGGL(k_enc_node_x6, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_enc_node_x6<3>, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
+    if (math == MATH_BF16) {
+        hipLaunchKernelGGL(k_enc_node_x6<1>, dim3((waves + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_enc_node, dim3((waves + 3) / 4), dim3(256), 0, st, a);
@@ -1062,13 +1071,17 @@ hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
-    if (math == MATH_X6) {   // NC blocks per wave, 4 waves per workgroup
+    if (math == MATH_X6 || math == MATH_BF16) {   // NC blocks per wave, 4 waves per workgroup
         constexpr int NC = 2;
         const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
-        if (a.z1)
+        if (math == MATH_BF16) {
+            if (a.z1) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1>), g, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((k_enc_edge_x6<false, NC, 1>), g, dim3(256), 0, st, a);
+        } else if (a.z1) {
             hipLaunchKernelGGL((k_enc_edge_x6<true, NC>), g, dim3(256), 0, st, a);
-        else
+        } else {
             hipLaunchKernelGGL((k_enc_edge_x6<false, NC>), g, dim3(256), 0, st, a);
+        }
         return hipGetLastError();
     }
     if (a.z1)
@@ -1079,6 +1092,13 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 }
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
+    if (math == MATH_BF16) {
+        if (a.nw_max <= 16)
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL((k_edge_fwd_x6<false, 0, 1>), dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (math == MATH_X6) {
         static const int dbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;
         if (a.nw_max <= 16 && dbg == 1)   // diagnosis: A rows from 8 cached blocks
@@ -1103,6 +1123,10 @@ hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st) {
         constexpr int NC = 1;
         const int w2 = (waves + NC - 1) / NC;
         hipLaunchKernelGGL((k_node_fwd_x6<NC>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
+    if (math == MATH_BF16) {
+        hipLaunchKernelGGL((k_node_fwd_x6<1, 1>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_node_fwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);

@@ -444,18 +444,23 @@ struct X6Img {
         const int li = lane & 15, row = 4 * (lane >> 4) + (li >> 2);
         return row * ROWB + 32 * (t ^ sigma(row)) + 8 * ((li & 3) ^ (row & 3));
     }
+    // NP = 1 (bf16 math): the h part only
+    template <int NP = 3>
     __device__ static __forceinline__ void put(char* S, int rr, int c4, float4 v) {
         uint32_t h0, m0, l0, h1, m1, l1;
         split2(v.x, v.y, h0, m0, l0);
         split2(v.z, v.w, h1, m1, l1);
         char* p = S + woff(rr, c4);
         *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(p + PART) = make_uint2(m0, m1);
-        *reinterpret_cast<uint2*>(p + 2 * PART) = make_uint2(l0, l1);
+        if constexpr (NP == 3) {
+            *reinterpret_cast<uint2*>(p + PART) = make_uint2(m0, m1);
+            *reinterpret_cast<uint2*>(p + 2 * PART) = make_uint2(l0, l1);
+        }
     }
+    template <int NP = 3>
     __device__ static __forceinline__ void get(const char* S, int off, bf16x8 (&f)[3]) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
             f[p] = as_bf16x8(lds_tr16(S + p * PART + off), lds_tr16(S + p * PART + off + 16 * ROWB));
     }
 };
@@ -463,7 +468,7 @@ struct X6Img {
 // The same gradient in split-bf16 math (x6): operands are split once when staged (every element
 // feeds MX or MY tiles), 16x16x32 bf16 MFMAs, one k-step per 32-row block: 6·MX·MY MFMAs of 16
 // cycles per wave per block instead of 8·MX·MY f32 MFMAs of 32.
-template <int XM, int YM, int KXP, int NYP, int OCC>
+template <int XM, int YM, int KXP, int NYP, int OCC, int NP = 3>
 __global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
     constexpr int MX = KXP / 32, MY = NYP / 32;
     using IX = X6Img<KXP>;
@@ -490,19 +495,19 @@ __global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
     st.fetch(a, r_begin, tid);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
         __syncthreads();
-        st.emit_x(a, tid, [&](int rr, int c4, float4 v) { IX::put(Xs, rr, c4, v); });
-        st.emit_y(tid, [&](int rr, int c4, float4 v) { IY::put(Ys, rr, c4, v); });
+        st.emit_x(a, tid, [&](int rr, int c4, float4 v) { IX::template put<NP>(Xs, rr, c4, v); });
+        st.emit_y(tid, [&](int rr, int c4, float4 v) { IY::template put<NP>(Ys, rr, c4, v); });
         __syncthreads();
         if (r0 + 32 < r_end) st.fetch(a, r0 + 32, tid);
         bf16x8 yb[MY][3];
 #pragma unroll
-        for (int y = 0; y < MY; ++y) IY::get(Ys, oy[y], yb[y]);
+        for (int y = 0; y < MY; ++y) IY::template get<NP>(Ys, oy[y], yb[y]);
 #pragma unroll
         for (int x = 0; x < MX; ++x) {
             bf16x8 xa[3];
-            IX::get(Xs, ox[x], xa);
+            IX::template get<NP>(Xs, ox[x], xa);
 #pragma unroll
-            for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6(xa, yb[y], acc[x][y]);
+            for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6<NP>(xa, yb[y], acc[x][y]);
         }
     }
     float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
@@ -534,7 +539,7 @@ struct W2gSet {
 
 // DBG (diagnosis builds, SPWGNN_W2G_DBG): 1 no MFMAs, 2 gathers from stage 0, 4 no staging
 // arithmetic, 8 matrix waves at s_setprio 1, 32 no gathers
-template <int dbg>
+template <int dbg, int NP = 3>
 __global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
     using IM = X6Img<160>;
@@ -569,22 +574,22 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
             // fragment reads run one (x, y) group ahead of the MFMAs that use them: X0 Y0 | Y1 ·
             // (0,0) | Y2 · (0,1) | … | X1 · (0,4) | X2 · (1,*) | X3 · (2,*) | X4 · (3,*) | (4,*)
             bf16x8 yb[5][3], xa[2][3];
-            IM::get(Xs, ox[0], xa[0]);
-            IM::get(Ys, oy[0], yb[0]);
+            IM::template get<NP>(Xs, ox[0], xa[0]);
+            IM::template get<NP>(Ys, oy[0], yb[0]);
 #pragma unroll
             for (int y = 0; y < 5; ++y) {
-                if (y < 4) IM::get(Ys, oy[y + 1], yb[y + 1]);
-                else IM::get(Xs, ox[1], xa[1]);
+                if (y < 4) IM::template get<NP>(Ys, oy[y + 1], yb[y + 1]);
+                else IM::template get<NP>(Xs, ox[1], xa[1]);
                 __builtin_amdgcn_sched_barrier(0);
-                acc[0][y] = mfma16_x6(xa[0], yb[y], acc[0][y]);
+                acc[0][y] = mfma16_x6<NP>(xa[0], yb[y], acc[0][y]);
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int x = 1; x < 5; ++x) {
-                if (x < 4) IM::get(Xs, ox[x + 1], xa[(x + 1) & 1]);
+                if (x < 4) IM::template get<NP>(Xs, ox[x + 1], xa[(x + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int y = 0; y < 5; ++y) acc[x][y] = mfma16_x6(xa[x & 1], yb[y], acc[x][y]);
+                for (int y = 0; y < 5; ++y) acc[x][y] = mfma16_x6<NP>(xa[x & 1], yb[y], acc[x][y]);
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
@@ -658,8 +663,8 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
                 __int_as_float(__float_as_int(gv.y) & __builtin_amdgcn_sbfe(w, 4 * c0 + 1, 1)),
                 __int_as_float(__float_as_int(gv.z) & __builtin_amdgcn_sbfe(w, 4 * c0 + 2, 1)),
                 __int_as_float(__float_as_int(gv.w) & __builtin_amdgcn_sbfe(w, 4 * c0 + 3, 1)));
-            IM::put(Xs, rr, c0 + 8 * k, x);
-            IM::put(Ys, rr, c0 + 8 * k, y);
+            IM::template put<NP>(Xs, rr, c0 + 8 * k, x);
+            IM::template put<NP>(Ys, rr, c0 + 8 * k, y);
         }
     };
     if (T == 0) {
@@ -669,8 +674,8 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
     if (!k4ok) {   // padding columns 152..159 of both operands in both buffers stay zero
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            IM::put(buf[p], rr, c0 + 32, f4zero());
-            IM::put(buf[p] + kW2gImg, rr, c0 + 32, f4zero());
+            IM::template put<NP>(buf[p], rr, c0 + 32, f4zero());
+            IM::template put<NP>(buf[p] + kW2gImg, rr, c0 + 32, f4zero());
         }
     }
     W2gSet R0, R1;
@@ -725,7 +730,7 @@ struct WsSet4 {
     int nvalid;
 };
 
-template <int KXP, int NYP, int YROW, bool MASK>
+template <int KXP, int NYP, int YROW, bool MASK, int NP = 3>
 __global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_wgrad_ws(WgWsArgs a) {
     using W = WsStage<KXP, NYP, YROW, MASK>;
@@ -756,22 +761,22 @@ void k_wgrad_ws(WgWsArgs a) {
             const char* Xs = buf[t & 1];
             const char* Ys = Xs + W::IMX;
             bf16x8 yb[MY][3], xa[2][3];
-            IX::get(Xs, ox[0], xa[0]);
-            IY::get(Ys, oy[0], yb[0]);
+            IX::template get<NP>(Xs, ox[0], xa[0]);
+            IY::template get<NP>(Ys, oy[0], yb[0]);
 #pragma unroll
             for (int y = 0; y < MY; ++y) {
-                if (y + 1 < MY) IY::get(Ys, oy[y + 1], yb[y + 1]);
-                else IX::get(Xs, ox[1], xa[1]);
+                if (y + 1 < MY) IY::template get<NP>(Ys, oy[y + 1], yb[y + 1]);
+                else IX::template get<NP>(Xs, ox[1], xa[1]);
                 __builtin_amdgcn_sched_barrier(0);
-                acc[0][y] = mfma16_x6(xa[0], yb[y], acc[0][y]);
+                acc[0][y] = mfma16_x6<NP>(xa[0], yb[y], acc[0][y]);
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int x = 1; x < MX; ++x) {
-                if (x + 1 < MX) IX::get(Xs, ox[x + 1], xa[(x + 1) & 1]);
+                if (x + 1 < MX) IX::template get<NP>(Xs, ox[x + 1], xa[(x + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6(xa[x & 1], yb[y], acc[x][y]);
+                for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6<NP>(xa[x & 1], yb[y], acc[x][y]);
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
@@ -829,14 +834,14 @@ void k_wgrad_ws(WgWsArgs a) {
             float4 v = R.x[k];
             if (MASK && !xin) v = f4zero();
             if (k == ones_k) f4set(v, ones_c, xin ? 1.f : 0.f);
-            IX::put(Xs, rr, c0 + 8 * k, v);
+            IX::template put<NP>(Xs, rr, c0 + 8 * k, v);
         }
 #pragma unroll
         for (int k = 0; k < W::NKY; ++k) {
             if (!yk_ok(k)) break;
             float4 v = R.y[k];
             if (MASK && !yin) v = f4zero();
-            IY::put(Ys, yr, yc0 + 8 * k, v);
+            IY::template put<NP>(Ys, yr, yc0 + 8 * k, v);
         }
     };
     if (T == 0) {
@@ -849,13 +854,13 @@ void k_wgrad_ws(WgWsArgs a) {
 #pragma unroll
         for (int k = 0; k < (KXP / 4 + 7) / 8; ++k) {
             const int c4 = c0 + 8 * k;
-            if (c4 >= W::GX && c4 < KXP / 4) IX::put(buf[p], rr, c4, f4zero());
+            if (c4 >= W::GX && c4 < KXP / 4) IX::template put<NP>(buf[p], rr, c4, f4zero());
         }
         if (!YROW) {
 #pragma unroll
             for (int k = 0; k < (NYP / 4 + 7) / 8; ++k) {
                 const int c4 = c0 + 8 * k;
-                if (c4 >= W::GY && c4 < NYP / 4) IY::put(buf[p] + W::IMX, rr, c4, f4zero());
+                if (c4 >= W::GY && c4 < NYP / 4) IY::template put<NP>(buf[p] + W::IMX, rr, c4, f4zero());
             }
         }
     }
@@ -1012,9 +1017,24 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st
 #undef SPW_WG
     return hipErrorInvalidValue;
 }
-hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hipStream_t st) {
+// bf16 math: the two small position-operand gradients (the stored-operand ones run on k_wgrad_ws)
+hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st) {
+    const dim3 g(chunks), b(kWgThreads);
+    if (a.xmode == XM_EDGE_D && a.ymode == YM_CM && a.kx_pad == 32 && a.ny_pad == 160)
+        hipLaunchKernelGGL((k_wgrad_x6<XM_EDGE_D, YM_CM, 32, 160, 2, 1>), g, b, 0, st, a);
+    else if (a.xmode == XM_NODE_O && a.ymode == YM_CM && a.kx_pad == 32 && a.ny_pad == 128)
+        hipLaunchKernelGGL((k_wgrad_x6<XM_NODE_O, YM_CM, 32, 128, 2, 1>), g, b, 0, st, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st) {
     static const int dbg = getenv("SPWGNN_W2G_DBG") ? atoi(getenv("SPWGNN_W2G_DBG")) : 0;
     const dim3 g(wgs), b(kW2gThreads);
+    if (math == MATH_BF16) {
+        hipLaunchKernelGGL((k_w2grad_ws<0, 1>), g, b, 0, st, a, blk_per_wg);
+        return hipGetLastError();
+    }
     switch (dbg) {
         case 0: hipLaunchKernelGGL(k_w2grad_ws<0>, g, b, 0, st, a, blk_per_wg); break;
         case 1: hipLaunchKernelGGL(k_w2grad_ws<1>, g, b, 0, st, a, blk_per_wg); break;
@@ -1025,11 +1045,15 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, hip
     }
     return hipGetLastError();
 }
-hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, hipStream_t st) {
+hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
+                           hipStream_t st) {
     const dim3 g(wgs), b(kWsThreads);
 #define SPW_WS(KX, NY, YR, MK)                                                                   \
     if (kx_pad == KX && ny_pad == NY && yrow == YR && (mask != 0) == MK) {                     \
-        hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK>), g, b, 0, st, a);                      \
+        if (math == MATH_BF16)                                                                 \
+            hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK, 1>), g, b, 0, st, a);               \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK>), g, b, 0, st, a);                  \
         return hipGetLastError();                                                              \
     }
     SPW_WS(160, 160, 0, false)

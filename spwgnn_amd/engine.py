@@ -27,7 +27,7 @@ def _require_gpu(t: torch.Tensor, what: str):
         raise _lib.SpwgnnError(f"{what} must be a HIP device tensor (got {t.device}); the HIP path has no CPU fallback")
 
 
-MATH_MODES = {"f32": _lib.MATH_F32, "x6": _lib.MATH_X6}
+MATH_MODES = {"f32": _lib.MATH_F32, "x6": _lib.MATH_X6, "bf16": _lib.MATH_BF16}
 
 
 @dataclass
