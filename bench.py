@@ -123,8 +123,9 @@ def cpu_baseline(n_objects: int, S: int, seconds: float, threads=None):
 PMC_NAMES = {
     "f32": {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true, true>", "enc_edge": "k_enc_edge<true>",
             "enc_edge_bwd": "k_enc_edge_bwd", "wgrad_w2": "k_wgrad_t<4, 2, 160, 160>"},
-    "x6": {"edge_fwd": "k_edge_fwd_x6<true, 0>", "edge_bwd": "k_edge_bwd_x6<true, 0>",
-           "enc_edge": "k_enc_edge_x6<true, 2>", "enc_edge_bwd": "k_enc_edge_bwd_x6<2>", "wgrad_w2": "k_w2grad_ws<0>"},
+    "x6": {"edge_fwd": "k_edge_fwd_x6<true, 0, 3>", "edge_bwd": "k_edge_bwd_x6<true, 0, 3>",
+           "enc_edge": "k_enc_edge_x6<true, 2, 3>", "enc_edge_bwd": "k_enc_edge_bwd_x6<2, 3>",
+           "wgrad_w2": "k_w2grad_ws<0, 3>"},
 }
 
 

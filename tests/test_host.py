@@ -175,3 +175,18 @@ def test_removal_candidates_order():
     assert c.shape == (5, 4, 3)
     for i in range(5):
         assert np.array_equal(c[i], np.delete(boxes, i, axis=0))   # JengaBuilder.py:244-249 order
+
+
+def test_bench_pmc_names_match_committed_summary():
+    """bench.py's roofline `traffic` looks kernels up by their rocprofv3 names in the committed
+    PMC summary; a template change that renames a kernel must be caught here, not as a null."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    with open(os.path.join(root, "profiles", "pmc_summary.json")) as f:
+        summary = json.load(f)
+    for kernel, name in bench.PMC_NAMES["x6"].items():
+        assert name in summary, (kernel, name)
+        assert bench.load_pmc(kernel, "x6") is not None, kernel

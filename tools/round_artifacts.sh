@@ -3,7 +3,7 @@
 set -e
 R=$GRAFT_REPO_ROOT; T=${1:-r01}
 cd $R
-timeout -k 10 600 python3 -m pytest tests -m gpu -x -q > gpurun_out/${T}_pytest_gpu.log 2>&1
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest_gpu.log 2>&1
 tail -1 gpurun_out/${T}_pytest_gpu.log
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-leg"
