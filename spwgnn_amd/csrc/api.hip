@@ -20,6 +20,7 @@ struct Ws {
     int64_t pk;
     int64_t zo1, co, P, a, o1, U, V, H2s;           // node
     int64_t A, z1, z2, z3, cr;                       // edge
+    int64_t ed;                                      // per-edge (dx, dy) float2 (training)
     int64_t mask1, mask2, zmask;                     // u32
     int64_t dx, do1, g, G3, dU, dV, dP, dco, dzo2, dzo1;   // node (bwd)
     int64_t dA, dz4, dz3, dz2, dz1;                  // edge (bwd)
@@ -101,6 +102,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.a = take(nN * S);
         w.o1 = take(nN * S);
         w.z1 = take(eCM);
+        w.ed = take(w.RE * 2);
         w.z2 = take(eCM);
         w.z3 = take(eCM);
         w.cr = take(eCM);
@@ -130,6 +132,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.slab_floats = (int64_t)kWgSlots * w.slot_floats;
         w.slab = take(w.slab_floats);
     } else {
+        w.ed = -1;
         w.zo1 = w.a = w.o1 = w.z1 = w.z2 = w.z3 = w.cr = w.mask1 = w.mask2 = w.zmask = -1;
         w.dx = w.do1 = w.g = w.G3 = w.dU = w.dV = w.dP = w.dco = w.dzo2 = w.dzo1 = -1;
         w.dA = w.dz4 = w.dz3 = w.dz2 = w.dz1 = w.slab = w.H1 = w.DH2 = -1;
@@ -236,6 +239,13 @@ static int kmath(const spwgnn_run* r, int bit) {
     return (r->math != MATH_F32 && (mask & bit)) ? r->math : MATH_F32;
 }
 
+// The rm.1 / om.1 weight gradients rebuild their operands z1 = relu(rm.0(d)) and zo1 = relu(om.0(y, w))
+// on the staging waves of k_wgrad_ws from the per-edge d (8 bytes) and the node positions, so the
+// encoders store d instead of the 608-byte z1 rows and no zo1 rows.
+static bool z1_rebuilt(const spwgnn_run* r) {
+    return r->training && kmath(r, kX6Wgrad) != MATH_F32 && !getenv_flag("SPWGNN_WG_OLD");
+}
+
 struct Prof {
     const spwgnn_run* r;
     hipStream_t st;
@@ -308,7 +318,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         en.x_w1b = c.x6(X6_W1B);
         en.x_w1c = c.x6(X6_W1C);
     }
-    en.zo1 = c.f(w.zo1);
+    en.zo1 = z1_rebuilt(r) ? nullptr : c.f(w.zo1);
     en.co = c.f(w.co);
     en.P0 = c.f(w.P_at(0));
     en.U0 = c.f(w.U_at(0));
@@ -342,7 +352,8 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ee.x_rm3 = c.x6(X6_RM3);
         ee.x_w1a = c.x6(X6_W1A);
     }
-    ee.z1 = c.f(w.z1);
+    ee.z1 = z1_rebuilt(r) ? nullptr : c.f(w.z1);
+    ee.ed = z1_rebuilt(r) ? reinterpret_cast<float2*>(c.f(w.ed)) : nullptr;
     ee.z2 = c.f(w.z2);
     ee.z3 = c.f(w.z3);
     ee.cr = c.f(w.cr);
@@ -433,6 +444,9 @@ struct WgSpec {
     // reduce target
     int tk = -1, tb = -1, k_rows = 0, k_row0 = 0, bias_row = -1, perm = 0;
     bool recompute = false;   // XM_H1 / YM_DH2 context below
+    const float2* xd = nullptr;          // z1 rebuilt from d (k_wgrad_ws XD 1)
+    const float4* xp = nullptr;          // zo1 rebuilt from the node positions (XD 2)
+    const float *w0 = nullptr, *b0 = nullptr;
 };
 
 // Each weight gradient writes its per-chunk slabs into its own slot; the ordered chunk sums of all
@@ -494,6 +508,10 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         wa.x_sb = g.x_stride / 32;
         wa.y_sb = g.y_stride / 32;
         wa.x_ones = g.x_ones;
+        wa.xd = g.xd;
+        wa.xp = g.xp;
+        wa.w0 = g.w0;
+        wa.b0 = g.b0;
         const int64_t nst = wa.nbs * wa.S;
         int64_t wgs = std::min<int64_t>(nst, kW2gWgs);
         wa.stages_per_wg = (nst + wgs - 1) / wgs;
@@ -656,7 +674,10 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     enb.n_nodes = b->n_nodes;
     enb.dco = c.f(w.dco);
     enb.co = c.f(w.co);
-    enb.zo1 = c.f(w.zo1);
+    enb.zo1 = z1_rebuilt(r) ? nullptr : c.f(w.zo1);
+    enb.pos = b->pos;
+    enb.w_om0 = c.pk(PK_OM0);
+    enb.b_om0 = c.pk(PB_OM0);
     enb.om1t = c.pk(PK_OM1T);
     enb.dzo2 = c.f(w.dzo2);
     enb.dzo1 = c.f(w.dzo1);
@@ -681,7 +702,15 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
-    { WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    {
+        WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g);
+        if (z1_rebuilt(r)) {
+            g.xd = reinterpret_cast<const float2*>(c.f(w.ed));
+            g.w0 = c.pk(PK_RM0);
+            g.b0 = c.pk(PB_RM0);
+        }
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+    }
     { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
     { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
     { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
@@ -744,6 +773,11 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
         g.rows = nN; g.y_stride = 0;
+        if (z1_rebuilt(r)) {
+            g.xp = reinterpret_cast<const float4*>(b->pos);
+            g.w0 = c.pk(PK_OM0);
+            g.b0 = c.pk(PB_OM0);
+        }
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }

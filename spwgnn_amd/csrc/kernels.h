@@ -81,7 +81,8 @@ struct EncEdgeArgs {
     const int32_t *esrc, *edst, *node_tower, *node_local;
     const float *w_rm0, *b_rm0, *w_rm1, *b_rm1, *w_rm2, *b_rm2, *w_rm3, *b_rm3, *w_w1a, *b_w1a;
     const uint4 *x_rm1, *x_rm2, *x_rm3, *x_w1a;   // x6 images (math == MATH_X6)
-    float *z1, *z2, *z3, *cr, *A;   // chunk-major blocks
+    float *z1, *z2, *z3, *cr, *A;   // chunk-major blocks (z1 null: the W1 gradient rebuilds it from ed)
+    float2* ed;                     // training: per-edge (dx, dy), rows of the 32-edge blocks
     uint32_t* zmask;                // [blk][4 layers: z1,z2,z3,cr][3 words][64 lanes] — activation > 0 bits
     int dropout_on;
     uint32_t thresh;
@@ -146,6 +147,8 @@ struct EncEdgeBwdArgs {
 struct EncNodeBwdArgs {
     int n_nodes;
     const float *dco, *co, *zo1, *om1t;
+    const float* pos;                 // zo1 null: its relu mask is rebuilt from (y, w) and om.0
+    const float *w_om0, *b_om0;
     float *dzo2, *dzo1;
     float scale;
 };
@@ -188,6 +191,9 @@ struct WgradArgs {
 struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 32-row blocks
     const float* x;        // chunk-major
     const float* y;        // chunk-major, or row-major with stride 160 (yrow)
+    const float2* xd;      // XD 1: per-edge (dx, dy); X = [relu(rm.0(dx, dy)) | 1] (= z1) is rebuilt
+    const float4* xp;      // XD 2: node positions; X = [relu(om.0(y, w)) | 1] (= zo1) is rebuilt
+    const float *w0, *b0;  // XD: the first-layer pack [2][KXP] and its bias [KXP]
     float* slab;           // [wgs][kx_pad][ny_pad]
     int64_t nbs, S, x_sb, y_sb, count, stages_per_wg;
     int x_ones, pad0;

@@ -592,7 +592,18 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     store_cm<4>(a.dzo2 + bN, D, lane, valid);
     zero_tiles(E);
     tchain_acc<4, 4, 4, kLdN>(D, E, a.om1t, lane);
-    load_cm<4>(a.zo1 + bN, Z, lane);
+    if (a.zo1) {
+        load_cm<4>(a.zo1 + bN, Z, lane);
+    } else {   // the forward's own first-layer arithmetic (k_enc_node), not a stored row
+        const float4 p = reinterpret_cast<const float4*>(a.pos)[valid ? n : a.n_nodes - 1];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                Z[t][r] = relu(dense2(p.y, p.z, a.w_om0[f], a.w_om0[128 + f], a.b_om0[f]));
+            }
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll

@@ -221,7 +221,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     // saved activations (padding-edge rows unmasked: finite, and met only by zero gradients)
     const int64_t cmo = (int64_t)blk * kCmBlk;
     if (zb) {
-        store_cm<5>(a.z1 + cmo, X, lane, true);
+        if (a.ed && h == 0) a.ed[e] = make_float2(dx, dy);
+        if (a.z1) store_cm<5>(a.z1 + cmo, X, lane, true);
         store_pos_bits<5>(mb, X, lane);
     }
     zero_tiles(Y);
@@ -285,6 +286,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
             dx = pd.x - ps.x;  // Networks.py:148-152 (receiver − sender), (x, y)
             dy = pd.y - ps.y;
         }
+        if (TRAIN && a.ed && h == 0 && blk < a.n_eblocks) a.ed[e] = make_float2(dx, dy);
 #pragma unroll
         for (int t = 0; t < 5; ++t)
 #pragma unroll
@@ -1071,20 +1073,21 @@ hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
+    const bool train = a.z1 || a.ed;   // z1 null with ed set: training, z1 rebuilt by the W1 gradient
     if (math == MATH_X6 || math == MATH_BF16) {   // NC blocks per wave, 4 waves per workgroup
         constexpr int NC = 2;
         const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
         if (math == MATH_BF16) {
-            if (a.z1) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1>), g, dim3(256), 0, st, a);
+            if (train) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1>), g, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((k_enc_edge_x6<false, NC, 1>), g, dim3(256), 0, st, a);
-        } else if (a.z1) {
+        } else if (train) {
             hipLaunchKernelGGL((k_enc_edge_x6<true, NC>), g, dim3(256), 0, st, a);
         } else {
             hipLaunchKernelGGL((k_enc_edge_x6<false, NC>), g, dim3(256), 0, st, a);
         }
         return hipGetLastError();
     }
-    if (a.z1)
+    if (train)
         hipLaunchKernelGGL(k_enc_edge<true>, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(k_enc_edge<false>, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);

@@ -727,10 +727,14 @@ struct WsStage {
 };
 struct WsSet4 {
     float4 x[5], y[5];
+    float2 d;
     int nvalid;
 };
 
-template <int KXP, int NYP, int YROW, bool MASK, int NP = 3>
+// XD: X = [z1 | 1] rebuilt from the per-edge (dx, dy) (XD 1), or [zo1 | 1] from the node's (y, w)
+// (XD 2), with the encoders' own first-layer arithmetic (dense2 + relu on the same pack):
+// bit-identical to the activations the encoders no longer store.
+template <int KXP, int NYP, int YROW, bool MASK, int NP = 3, int XD = 0>
 __global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_wgrad_ws(WgWsArgs a) {
     using W = WsStage<KXP, NYP, YROW, MASK>;
@@ -813,6 +817,17 @@ void k_wgrad_ws(WgWsArgs a) {
     auto yk_ok = [&](int k) { return YROW ? true : 2 * swave + 8 * k < W::GY; };
     const int ones_k = a.x_ones >= 0 && ((a.x_ones >> 2) & 7) == c0 ? (a.x_ones >> 5) : -1;
     const int ones_c = a.x_ones & 3;
+    float4 w0r[XD ? W::NKX : 1], w1r[XD ? W::NKX : 1], b0r[XD ? W::NKX : 1];
+    if (XD) {
+#pragma unroll
+        for (int k = 0; k < W::NKX; ++k) {
+            const int f = 4 * (c0 + 8 * k);
+            const bool ok = c0 + 8 * k < W::GX;
+            w0r[k] = ok ? *reinterpret_cast<const float4*>(a.w0 + f) : f4zero();
+            w1r[k] = ok ? *reinterpret_cast<const float4*>(a.w0 + KXP + f) : f4zero();
+            b0r[k] = ok ? *reinterpret_cast<const float4*>(a.b0 + f) : f4zero();
+        }
+    }
     auto fetch = [&](int t, WsSet4& R) {
         const int64_t tg = t0 + (t < T ? t : T - 1);
         const int64_t s = tg / a.nbs, nb = tg - s * a.nbs;
@@ -820,8 +835,15 @@ void k_wgrad_ws(WgWsArgs a) {
         const float* px = a.x + (s * a.x_sb + nb) * (W::KHX * 64) + rr * 4;
         const float* py = YROW ? a.y + ((s * a.y_sb + nb) * 32 + yr) * 160
                                : a.y + (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
+        if (XD == 1) {
+            R.d = a.xd[(s * a.x_sb + nb) * 32 + rr];
+        } else if (XD == 2) {
+            const float4 p = a.xp[min<int64_t>((s * a.x_sb + nb) * 32 + rr, a.count - 1)];
+            R.d = make_float2(p.y, p.z);   // Networks.py:155-161: (y, width)
+        } else {
 #pragma unroll
-        for (int k = 0; k < W::NKX; ++k) R.x[k] = *reinterpret_cast<const float4*>(px + offx[k]);
+            for (int k = 0; k < W::NKX; ++k) R.x[k] = *reinterpret_cast<const float4*>(px + offx[k]);
+        }
 #pragma unroll
         for (int k = 0; k < W::NKY; ++k) R.y[k] = *reinterpret_cast<const float4*>(py + offy[k]);
     };
@@ -831,7 +853,15 @@ void k_wgrad_ws(WgWsArgs a) {
 #pragma unroll
         for (int k = 0; k < W::NKX; ++k) {
             if (!xk_ok(k)) break;
-            float4 v = R.x[k];
+            float4 v;
+            if (XD) {
+                v.x = relu(dense2(R.d.x, R.d.y, w0r[k].x, w1r[k].x, b0r[k].x));
+                v.y = relu(dense2(R.d.x, R.d.y, w0r[k].y, w1r[k].y, b0r[k].y));
+                v.z = relu(dense2(R.d.x, R.d.y, w0r[k].z, w1r[k].z, b0r[k].z));
+                v.w = relu(dense2(R.d.x, R.d.y, w0r[k].w, w1r[k].w, b0r[k].w));
+            } else {
+                v = R.x[k];
+            }
             if (MASK && !xin) v = f4zero();
             if (k == ones_k) f4set(v, ones_c, xin ? 1.f : 0.f);
             IX::template put<NP>(Xs, rr, c0 + 8 * k, v);
@@ -1048,6 +1078,22 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
                            hipStream_t st) {
     const dim3 g(wgs), b(kWsThreads);
+    if (a.xd) {   // the rm.1 gradient with X = [z1 | 1] rebuilt from (dx, dy)
+        if (kx_pad != 160 || ny_pad != 160 || yrow || mask) return hipErrorInvalidValue;
+        if (math == MATH_BF16)
+            hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1>), g, b, 0, st, a);
+        else
+            hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 3, 1>), g, b, 0, st, a);
+        return hipGetLastError();
+    }
+    if (a.xp) {   // the om.1 gradient with X = [zo1 | 1] rebuilt from the node positions
+        if (kx_pad != 128 || ny_pad != 128 || yrow || !mask) return hipErrorInvalidValue;
+        if (math == MATH_BF16)
+            hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 1, 2>), g, b, 0, st, a);
+        else
+            hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 3, 2>), g, b, 0, st, a);
+        return hipGetLastError();
+    }
 #define SPW_WS(KX, NY, YR, MK)                                                                   \
     if (kx_pad == KX && ny_pad == NY && yrow == YR && (mask != 0) == MK) {                     \
         if (math == MATH_BF16)                                                                 \
