@@ -66,7 +66,8 @@ int32_t spwgnn_dense_to_edges(const float* Rs, const float* Rr, int32_t B, int32
 /* Work plan for the edge kernels: towers are packed into wave-tiles of whole towers with at
  * most nw_max nodes; each wave-tile's edges are cut into 32-edge blocks (last one padded with
  * -1). blk_csr holds, per block, the block's edge slots sorted by local receiver and by local
- * sender (deterministic segment sums). Two phases: sizes, then fill. Host memory. */
+ * sender (deterministic segment sums). Two phases: sizes, then fill. Host memory. src/dst may
+ * be NULL when no tower has an edge (single-box towers, or no relation under the threshold). */
 typedef struct spwgnn_plan_sizes {
     int32_t n_wtiles;
     int32_t n_eblocks;

@@ -84,6 +84,8 @@ class TowerBatch:
         dst = np.ascontiguousarray(dst, dtype=np.int32)
         T = len(tower_nodes)
         Nn = int(tower_nodes.sum())
+        if T == 0:
+            raise ValueError("empty batch: at least one tower is needed")
         if pos.shape[0] != Nn:
             raise ValueError(f"pos has {pos.shape[0]} rows, towers hold {Nn} nodes")
         if int(tower_edges.sum()) != len(src) or len(src) != len(dst):
@@ -164,6 +166,8 @@ class TowerBatch:
                raw_positions_list=None) -> "TowerBatch":
         """Towers of different sizes: list of (N_b, 3) objects; relations fully connected, or
         thresholded on ``raw_positions_list`` (pixels) like main.py:71-81."""
+        if len(objects_list) == 0:
+            raise ValueError("empty batch: at least one tower is needed")
         tower_nodes = np.array([len(o) for o in objects_list], np.int32)
         srcs, dsts, tes = [], [], []
         off = 0

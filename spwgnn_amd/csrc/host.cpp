@@ -168,7 +168,7 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
                          const int32_t* src, const int32_t* dst, int32_t nw_max,
                          const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src,
                          int32_t* edge_dst, int32_t* edge_id, uint8_t* blk_csr) {
-    if (!sizes || !wtile || !edge_src || !edge_dst || !blk_csr || !src || !dst) return SPWGNN_E_ARG;
+    if (!sizes || !wtile || !edge_src || !edge_dst || !blk_csr) return SPWGNN_E_ARG;
     std::vector<int32_t> first;
     int32_t nb = 0, used = 0;
     int32_t st = plan_pack(n_towers, tower_nodes, tower_edges, nw_max, &first, &nb, &used);
@@ -181,6 +181,7 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
         node_off[t + 1] = node_off[t] + tower_nodes[t];
         edge_off[t + 1] = edge_off[t] + tower_edges[t];
     }
+    if (edge_off[n_towers] > 0 && (!src || !dst)) return SPWGNN_E_ARG;   // no list needed without edges
     int32_t blk = 0;
     for (int32_t w = 0; w < ntiles; ++w) {
         const int32_t t0 = first[w], t1 = first[w + 1];

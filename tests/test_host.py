@@ -190,3 +190,15 @@ def test_bench_pmc_names_match_committed_summary():
     for kernel, name in bench.PMC_NAMES["x6"].items():
         assert name in summary, (kernel, name)
         assert bench.load_pmc(kernel, "x6") is not None, kernel
+
+
+def test_plan_without_any_edge_and_empty_batch():
+    """Single-box towers: no edge list at all (NULL src/dst through the C-ABI), one padding block
+    per wave-tile; an empty batch is rejected before the library is called."""
+    from spwgnn_amd import TowerBatch, data as D
+    objs = [(D.synthetic_towers(1, 1, seed=i)[0] / 170).astype(np.float32) for i in range(5)]
+    b = TowerBatch.ragged(objs, device="cpu")
+    assert b.n_edges == 0 and b.n_eblocks == b.n_wtiles >= 1
+    assert np.all(b.edge_src.numpy() == -1) and np.all(b.edge_dst.numpy() == -1)
+    with pytest.raises(ValueError):
+        TowerBatch.ragged([], device="cpu")
