@@ -18,6 +18,7 @@ struct Ws {
     int64_t RN, RE, NB;
     // floats offsets (bytes / 4) — every array starts on 256 bytes
     int64_t pk;
+    int64_t cw;                                      // node: c_o·Wo1c (x6/bf16 node forward)
     int64_t zo1, co, P, a, o1, U, V, H2s;           // node
     int64_t A, z1, z2, z3, cr;                       // edge
     int64_t ed;                                      // per-edge (dx, dy) float2 (training)
@@ -91,6 +92,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
     }
     const int64_t nN = w.RN * kRowN, nE = w.RN * kRowE, eE = w.RE * kLdE;
     w.co = take(nN);
+    w.cw = take(nN);
     w.P = take(nN * w.sP());
     w.U = take(nE * w.sStep());
     w.V = take(nE * w.sStep());
@@ -400,6 +402,8 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         nf.H2s = c.f(w.H2s_at(s));
         nf.P = c.f(w.P_at(s));
         nf.co = c.f(w.co);
+        nf.cw_out = (s == 0) ? c.f(w.cw) : nullptr;
+        nf.cw_in = (s > 0) ? c.f(w.cw) : nullptr;
         nf.a_out = r->training ? c.f(w.a_at(s)) : nullptr;
         nf.o1_out = r->training ? c.f(w.o1_at(s)) : nullptr;
         nf.Pn = c.f(w.P_at(s + 1));

@@ -105,6 +105,10 @@ struct NodeFwdArgs {
     int n_nodes;
     const float *H2s, *P, *co;
     float *a_out, *o1_out, *Pn, *logits, *U, *V;
+    // x6/bf16: c_o·Wo1c is step-invariant — step 0 stores the accumulator after that product
+    // (cw_out), later steps start from it (cw_in) instead of repeating the product
+    const float* cw_in;
+    float* cw_out;
     const float *w3a, *wo1c, *wo1a, *wo1p, *wo2, *w1b, *w1c, *bo1, *bo2p;
     const uint4 *x_w3a, *x_wo1c, *x_wo1a, *x_wo1p, *x_wo2, *x_w1b, *x_w1c;   // x6 images
 };

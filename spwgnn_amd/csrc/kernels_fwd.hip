@@ -681,14 +681,21 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
             }
         if (a.a_out && has[c]) store_cm<4>(a.a_out + bN(c), E[c], lane, valid[c]);
     }
-    zero2(O);
-    {
+    if (a.cw_in) {   // c_o·Wo1c of step 0 (bit-identical to repeating the product)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) load_cm<4>(a.cw_in + bN(c), O[c], lane);
+    } else {
+        zero2(O);
         HalfRows<kKhN, NC> hr;
         const float* blk[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) blk[c] = a.co + bN(c);
         hr.load(blk, lane);
         tgemm_x6<4, 7, NC, kX6Ring, NP>(hr, O, a.x_wo1c, lane);
+        if (a.cw_out)
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (has[c]) store_cm<4>(a.cw_out + bN(c), O[c], lane, true);
     }
     tchain_x6<4, 7, 4, NC, kX6Ring, NP>(E, O, a.x_wo1a, lane);
     {
