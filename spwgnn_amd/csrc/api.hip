@@ -592,6 +592,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         nb.dPout = c.f(w.dP_at(s));
         nb.dco = c.f(w.dco);
         nb.dco_accumulate = !first;
+        nb.dco_sum = kmath(r, kX6NodeBwd) != MATH_F32;
         nb.w1bt = c.pk(PK_W1BT);
         nb.w1ct = c.pk(PK_W1CT);
         nb.wo2t = c.pk(PK_WO2T);
@@ -683,6 +684,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     enb.w_om0 = c.pk(PK_OM0);
     enb.b_om0 = c.pk(PB_OM0);
     enb.om1t = c.pk(PK_OM1T);
+    enb.wo1ct = kmath(r, kX6NodeBwd) != MATH_F32 ? c.pk(PK_WO1CT) : nullptr;
     enb.dzo2 = c.f(w.dzo2);
     enb.dzo1 = c.f(w.dzo1);
     enb.scale = scale;
