@@ -685,6 +685,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     enb.b_om0 = c.pk(PB_OM0);
     enb.om1t = c.pk(PK_OM1T);
     enb.wo1ct = kmath(r, kX6NodeBwd) != MATH_F32 ? c.pk(PK_WO1CT) : nullptr;
+    enb.do1 = c.f(w.do1_at(0));
+    enb.do1_step = w.do1_at(1) - w.do1_at(0);
+    enb.S = S;
     enb.dzo2 = c.f(w.dzo2);
     enb.dzo1 = c.f(w.dzo1);
     enb.scale = scale;

@@ -122,7 +122,7 @@ struct NodeBwdArgs {
     const float* dlogits;
     float *dx, *do1, *g, *G3, *dPout, *dco, *dprop;
     int dco_accumulate;
-    int dco_sum;    // x6: dco accumulates Σ_s do1_s; k_enc_node_bwd applies Wo1cᵀ once (linear)
+    int dco_sum;    // x6: no dco here; k_enc_node_bwd applies Wo1cᵀ once to Σ_s do1_s (linear)
     const float *w1bt, *w1ct, *wo2t, *wo1ct, *wo1at, *wo1pt, *w3t;
     const uint4 *x_w1bt, *x_w1ct, *x_wo2t, *x_wo1ct, *x_wo1at, *x_wo1pt, *x_w3t;   // x6 images
 };
@@ -154,7 +154,10 @@ struct EncNodeBwdArgs {
     const float *dco, *co, *zo1, *om1t;
     const float* pos;                 // zo1 null: its relu mask is rebuilt from (y, w) and om.0
     const float *w_om0, *b_om0;
-    const float* wo1ct;               // non-null: dco holds Σ_s do1_s, dc_o = (Σ do1)·Wo1cᵀ here
+    const float* wo1ct;               // non-null: dc_o = (Σ_s do1_s)·Wo1cᵀ here, from the per-step do1
+    const float* do1;                 //   rows (do1 + s·do1_step, s < S) instead of dco
+    int64_t do1_step;
+    int S;
     float *dzo2, *dzo1;
     float scale;
 };

@@ -220,20 +220,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // c_o part → dc_o (accumulated over steps in step order S-1..0); with dco_sum the product with
     // Wo1cᵀ is linear in do1 and runs once on Σ_s do1_s (k_enc_node_bwd)
-    if (a.dco_sum) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            if (a.dco_accumulate) {
-                f32x16 T[4];
-                load_cm<4>(a.dco + bN(c), T, lane);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) D[c][t] = T[t] + G[c][t];
-                if (has[c]) store_cm<4>(a.dco + bN(c), D[c], lane, valid[c]);
-            } else if (has[c]) {
-                store_cm<4>(a.dco + bN(c), G[c], lane, valid[c]);
-            }
-        }
-    } else {
+    if (!a.dco_sum) {
         zero2(D);
         tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1ct, lane);
 #pragma unroll
@@ -599,8 +586,13 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const bool valid = n < a.n_nodes;
     const int64_t bN = (int64_t)nb * kCmBlkN;   // chunk-major node block
     f32x16 D[4], Z[4], E[4];
-    if (a.wo1ct) {   // dco holds Σ_s do1_s: dc_o = (Σ do1)·Wo1cᵀ (fp32 MFMA)
-        load_cm<4>(a.dco + bN, E, lane);
+    if (a.wo1ct) {   // dc_o = (Σ_s do1_s)·Wo1cᵀ (fp32 MFMA), steps summed in backward order S-1..0
+        load_cm<4>(a.do1 + (int64_t)(a.S - 1) * a.do1_step + bN, E, lane);
+        for (int s = a.S - 2; s >= 0; --s) {
+            load_cm<4>(a.do1 + (int64_t)s * a.do1_step + bN, Z, lane);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) E[t] += Z[t];
+        }
         zero_tiles(D);
         tchain_acc<4, 4, 4, kLdN>(E, D, a.wo1ct, lane);
     } else {
