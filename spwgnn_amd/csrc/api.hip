@@ -756,6 +756,11 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
+        if (kmath(r, kX6NodeBwd) != MATH_F32) {   // c_oᵀ·Σ_s do1_s: Σ do1 stored by k_enc_node_bwd
+            g.y = c.f(w.dco);
+            g.rows = nN;
+            g.y_stride = 0;
+        }
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)

@@ -151,10 +151,12 @@ struct EncEdgeBwdArgs {
 
 struct EncNodeBwdArgs {
     int n_nodes;
-    const float *dco, *co, *zo1, *om1t;
+    float* dco;                       // dc_o in; with wo1ct: Σ_s do1_s out
+    const float *co, *zo1, *om1t;
     const float* pos;                 // zo1 null: its relu mask is rebuilt from (y, w) and om.0
     const float *w_om0, *b_om0;
     const float* wo1ct;               // non-null: dc_o = (Σ_s do1_s)·Wo1cᵀ here, from the per-step do1
+                                      //   rows; Σ_s do1_s is stored into dco (Wo1c gradient)
     const float* do1;                 //   rows (do1 + s·do1_step, s < S) instead of dco
     int64_t do1_step;
     int S;

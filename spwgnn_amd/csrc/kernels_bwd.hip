@@ -593,6 +593,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
             for (int t = 0; t < 4; ++t) E[t] += Z[t];
         }
+        store_cm<4>(a.dco + bN, E, lane, valid);   // Σ_s do1_s: Y of the Wo1c weight gradient
         zero_tiles(D);
         tchain_acc<4, 4, 4, kLdN>(E, D, a.wo1ct, lane);
     } else {
