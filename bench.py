@@ -129,6 +129,9 @@ PMC_NAMES = {
 }
 
 
+PMC_WORKLOAD = (65536, 6, 5)   # (towers per GPU, nodes, MP steps) of profiles/pmc_summary.json
+
+
 def load_pmc(kernel: str, math: str = "x6"):
     """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) from the committed PMC
     summary, or None when absent."""
@@ -192,9 +195,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SPWGNN_DIST_BACKEND=gloo rehearses the N>1 path with every rank on the visible GPU(s)
+    # (gloo all-reduces device tensors through the host); the driver's runs use nccl = RCCL
+    backend = os.environ.get("SPWGNN_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
 
     if args.infer:
@@ -251,7 +262,10 @@ def main():
     # it runs in (x6: bf16 peak / 6), and its PMC HBM bytes against 8 TB/s; the bound is the
     # larger fraction
     mpeak = {"x6": PEAK_X6_TFLOPS, "f32": PEAK_FP32_TFLOPS, "bf16": PEAK_BF16_TFLOPS}[args.math]
-    traffic = load_pmc(args.roofline_kernel, args.math)
+    # the committed PMC summary was collected at the default workload (tools/round_artifacts.sh):
+    # its bytes are only quoted for that shape
+    pmc_shape = (B, N, S) == PMC_WORKLOAD
+    traffic = load_pmc(args.roofline_kernel, args.math) if pmc_shape else None
     m_frac = achieved / mpeak
     h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
     h_frac = h_gbs / PEAK_HBM_GBS if h_gbs else None
@@ -310,7 +324,7 @@ def main():
             out[f"{m}_math"] = {"value": round(B * km / em, 1), "ms_per_step": round(em / km * 1e3, 3), "steps": km}
             del trm
             torch.cuda.empty_cache()
-    out["hbm"] = step_hbm(out["ms_per_step"])
+    out["hbm"] = step_hbm(out["ms_per_step"]) if pmc_shape else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_pair(N, S, args.cpu_seconds)
     if rank == 0:
