@@ -86,6 +86,29 @@ def test_backward_parity_small(T, N, nw, math):
     print("worst relative", worst)
 
 
+@pytest.mark.parametrize("math", ["x6", "f32"])
+@pytest.mark.parametrize("S", [1, 2, 10])
+def test_backward_parity_step_counts(S, math):
+    """Other propagation-step counts than the reference's 5: S = 1 (no step reuses c_o·Wo1c, the
+    Σ_s do1_s of the c_o gradients is one step, the backward writes dA once and never accumulates),
+    S = 2 and S = 10 (config 5's step count)."""
+    params = O.random_params(seed=17)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(5, 7, seed=9, fully_connected=False)
+    prop = np.random.default_rng(S).normal(0, 0.3, size=prop.shape).astype(np.float32)
+    loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, S)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    flat, ws, z = _gpu_forward(params, batch, S, training=True, math=math)
+    out3, dz = E.bce(z, torch.tensor(tgt, device="cuda").reshape(-1), E.BceScratch("cuda"))
+    grads, _ = E.backward(flat, batch, E.RunConfig(S, training=True, math=math), ws, dz)
+    torch.cuda.synchronize()
+    ref = np.asarray(z_ref).reshape(-1)
+    assert np.all(np.abs(z.cpu().numpy().reshape(-1) - ref) <= LOGIT_ATOL + LOGIT_RTOL * np.abs(ref))
+    assert abs(float(out3[0]) - loss_ref) < 1e-5
+    got = P.from_flat(grads)
+    for name, r in g_ref.items():
+        assert np.abs(got[name] - r).max() <= 1e-5 * np.abs(r).max() + 1e-7, name
+
+
 @pytest.mark.parametrize("N,fully", [(6, True), (9, False)])
 def test_bf16_math_forward_backward(N, fully):
     """SPWGNN_MATH_BF16 (BASELINE configs 3–4's arithmetic: operands rounded to bf16, one product,
