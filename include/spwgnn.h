@@ -2,7 +2,7 @@
  * spwgnn.h — C-ABI of libspwgnn_hip.so, the MI355X (gfx950) propagation-network engine.
  *
  * The reference (irmakguzey/SPWGNN) has no FFI: its hot path is a Keras graph built by
- * PropagationNetwork.getModel (src/Networks.py:106-194) over MLP blocks (src/Blocks.py:12-91),
+ * PropagationNetwork.getModel (src/Networks.py:16-104) over MLP blocks (src/Blocks.py:12-91),
  * driven by model.fit (src/main.py:92-98) and model.predict (src/JengaBuilder.py:328-329,
  * src/TowerCreator.py:430-431). Each entry point below replaces one piece of that graph; the
  * cited lines say which. Everything is plain C: raw pointers, sizes, an int status. All device
@@ -34,7 +34,7 @@ extern "C" {
 typedef void* spwgnn_stream_t;      /* a hipStream_t (NULL = default stream) */
 
 /* ---------------------------------------------------------------- parameters ------------ */
-/* The 22 Keras weight tensors of rm, om, rmp, omp (Networks.py:136-140, Blocks.py:20-28/60-68)
+/* The 22 Keras weight tensors of rm, om, rmp, omp (Networks.py:46-50, Blocks.py:20-28/60-68)
  * live in ONE flat fp32 buffer, Keras layout (kernel = [in][out] row-major, bias = [out]),
  * each tensor starting on a 64-float boundary. 209,501 real parameters. */
 typedef struct spwgnn_param_info {
@@ -53,9 +53,9 @@ int32_t spwgnn_param_tensor(int32_t index, spwgnn_param_info* out);
 
 /* ------------------------------------------------------------- host-side input builders -- */
 /* Dense relation matrices → compact edge list. Replaces the one-hot batch_dot gathers of
- * Networks.py:117-123/:174-175 and the segment-sum of :178 at the input boundary: a column k
+ * Networks.py:27-33/:174-175 and the segment-sum of :178 at the input boundary: a column k
  * of (Rs, Rr) that is one-hot in both is edge k (sender, receiver); an all-zero column is an
- * inactive relation (it never reaches an output, Networks.py:178); a column one-hot in Rs only
+ * inactive relation (it never reaches an output, Networks.py:88); a column one-hot in Rs only
  * also never reaches an output and is dropped; anything else → SPWGNN_E_RELATION.
  * Rs, Rr: host fp32 [B][N][E], E = N(N-1). Output edges are tower-major, slot order (the
  * sender-major enumeration of main.py:72-81). src/dst are GLOBAL node ids (b*N + local). */
@@ -91,8 +91,8 @@ typedef struct spwgnn_batch {
     int32_t n_eblocks;
     int32_t nw_max;
     int32_t pad0;
-    const float* pos;           /* [n_nodes][4]: objects (x, y, w)/170 + 0 pad (Networks.py:112)   */
-    const float* prop;          /* [n_nodes][100] 'propagation' input (Networks.py:119); NULL = 0  */
+    const float* pos;           /* [n_nodes][4]: objects (x, y, w)/170 + 0 pad (Networks.py:22)   */
+    const float* prop;          /* [n_nodes][100] 'propagation' input (Networks.py:29); NULL = 0  */
     const int32_t* node_tower;  /* [n_nodes] tower id (dropout key)                                */
     const int32_t* node_local; /* [n_nodes] node index inside its tower (dropout key)             */
     const int32_t* wtile;       /* [n_wtiles][4] first block, #blocks, first node, #nodes         */
@@ -102,9 +102,9 @@ typedef struct spwgnn_batch {
 } spwgnn_batch;
 
 typedef struct spwgnn_run {
-    int32_t mp_steps;   /* propagation steps; the reference hard-codes 5 (Networks.py:173)      */
+    int32_t mp_steps;   /* propagation steps; the reference hard-codes 5 (Networks.py:83)      */
     int32_t training;   /* 1: keep activations for backward + apply dropout                      */
-    float dropout;      /* Dropout rate on the two encodings (Networks.py:167-168); 0 = off      */
+    float dropout;      /* Dropout rate on the two encodings (Networks.py:77-78); 0 = off      */
     int32_t math;       /* SPWGNN_MATH_*: how the fp32 matrix products run on the matrix cores   */
     uint64_t seed;      /* dropout mask key                                                       */
     /* Optional timing hook (bench/profiling): for each launch of kernel `prof_kernel`
@@ -137,34 +137,34 @@ typedef struct spwgnn_run {
 /* Workspace bytes for (n_nodes, n_eblocks, mp_steps, training). */
 int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training);
 
-/* Forward: the whole graph of Networks.py:121-186 → per-node logits z (the model output is
- * sigmoid(z), Networks.py:184). logits: [n_nodes] device fp32. */
+/* Forward: the whole graph of Networks.py:31-96 → per-node logits z (the model output is
+ * sigmoid(z), Networks.py:94). logits: [n_nodes] device fp32. */
 int32_t spwgnn_forward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run,
                        void* workspace, int64_t workspace_bytes, float* logits,
                        spwgnn_stream_t stream);
 
 /* Backward of the last spwgnn_forward on the same workspace (training == 1): dlogits [n_nodes]
  * → grads (flat, same layout as params; overwritten) and, if dprop != NULL, d/d propagation
- * [n_nodes][100]. Replaces TF autodiff of the graph (Networks.py:192 compile → fit). */
+ * [n_nodes][100]. Replaces TF autodiff of the graph (Networks.py:102 compile → fit). */
 int32_t spwgnn_backward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run,
                         void* workspace, int64_t workspace_bytes, const float* dlogits,
                         float* grads, float* dprop, spwgnn_stream_t stream);
 
-/* Keras binary_crossentropy on sigmoid(logits) (Networks.py:192), mean over n:
+/* Keras binary_crossentropy on sigmoid(logits) (Networks.py:102), mean over n:
  * out3 = {loss, sum of correct (binary_accuracy numerator), n}; dlogits = dloss/dlogit.
  * scratch: >= spwgnn_bce_scratch_bytes(n) device bytes. Deterministic. */
 int64_t spwgnn_bce_scratch_bytes(int64_t n);
 int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* out3,
                    float* dlogits, void* scratch, spwgnn_stream_t stream);
 
-/* Keras-2.x Adam (Networks.py:191: lr=5e-4, decay=0): in-place on the flat buffer.
+/* Keras-2.x Adam (Networks.py:101: lr=5e-4, decay=0): in-place on the flat buffer.
  * g' = grad_scale*grad + 2*l2*param; lr_t = lr*sqrt(1-b2^t)/(1-b1^t);
  * m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2; p -= lr_t m/(sqrt(v)+eps). step = t >= 1. */
 int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64_t n, int32_t step,
                     float lr, float beta1, float beta2, float eps, float l2, float grad_scale,
                     spwgnn_stream_t stream);
 
-/* Sigmoid readout (Networks.py:183-186) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
+/* Sigmoid readout (Networks.py:93-96) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream);
 
 /* Per-tower readout over contiguous node ranges [tower_offsets[t], tower_offsets[t+1]):

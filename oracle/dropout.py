@@ -1,7 +1,7 @@
 """Numpy restatement of the engine's dropout key (spwgnn_amd/csrc/device_common.h: mix32,
 drop_row_key, drop_keep) — TEST INFRASTRUCTURE ONLY.
 
-Keras draws its Dropout masks from TensorFlow's RNG (Networks.py:167-168), which cannot be
+Keras draws its Dropout masks from TensorFlow's RNG (Networks.py:77-78), which cannot be
 reproduced; the engine uses its own counter-based key instead, and this module rebuilds the same
 multiplicative masks bit-exactly so the oracle can be run with identical dropout.
 """

@@ -14,16 +14,16 @@ as Keras builds it, an index-gather form, and a per-tower loop form), (c) known-
 tests, and (d) committed self-generated golden vectors (``tests/golden``).
 
 Reference anchors (``/root/reference/src``):
-  * inputs & layout ............ Networks.py:112-119 (objects, sender/receiver relations, propagation)
-  * endpoint gathers ........... Networks.py:122-123  senders = Rsᵀ·objects, receivers = Rrᵀ·objects
-  * feature slicing ............ Networks.py:125-127, 148-163  d = r_pos − s_pos; o = (y, width)
+  * inputs & layout ............ Networks.py:22-29 (objects, sender/receiver relations, propagation)
+  * endpoint gathers ........... Networks.py:32-33  senders = Rsᵀ·objects, receivers = Rrᵀ·objects
+  * feature slicing ............ Networks.py:35-37, 148-163  d = r_pos − s_pos; o = (y, width)
   * MLP blocks ................. Blocks.py:20-28, 60-68  Dense(relu)…, last Dense(linear)
-  * MLP sizes .................. Networks.py:136-140  rm 2→150³→150, om 2→100→100,
+  * MLP sizes .................. Networks.py:46-50  rm 2→150³→150, om 2→100→100,
                                                      rmp 350→150→150→100, omp 300→100→101
-  * encoder relu + dropout ..... Networks.py:165-168
-  * 5 propagation steps ........ Networks.py:173-181  (shared weights each step)
-  * readout .................... Networks.py:183-186  sigmoid(x[:, :, :1]) of the last step
-  * loss / optimizer ........... Networks.py:191-192  Adam(lr=5e-4), binary_crossentropy
+  * encoder relu + dropout ..... Networks.py:75-78
+  * 5 propagation steps ........ Networks.py:83-91  (shared weights each step)
+  * readout .................... Networks.py:93-96  sigmoid(x[:, :, :1]) of the last step
+  * loss / optimizer ........... Networks.py:101-102  Adam(lr=5e-4), binary_crossentropy
 """
 from __future__ import annotations
 
@@ -33,16 +33,16 @@ from typing import Dict, Iterable, List, Optional, Tuple
 import numpy as np
 import torch
 
-# (input width, layer widths) per MLP — Networks.py:136-140 (+ Blocks.py:20-28 / 60-68)
+# (input width, layer widths) per MLP — Networks.py:46-50 (+ Blocks.py:20-28 / 60-68)
 MLP_SPECS: Dict[str, Tuple[int, List[int]]] = {
     "rm": (2, [150, 150, 150, 150]),
     "om": (2, [100, 100]),
     "rmp": (350, [150, 150, 100]),
     "omp": (300, [100, 101]),
 }
-STATE_DIM = 100          # Networks.py:119 / :170 ('propagation' width, "100 is the layer size")
-REF_MP_STEPS = 5         # Networks.py:173
-DROPOUT_RATE = 0.1       # Networks.py:167-168
+STATE_DIM = 100          # Networks.py:29 / :170 ('propagation' width, "100 is the layer size")
+REF_MP_STEPS = 5         # Networks.py:83
+DROPOUT_RATE = 0.1       # Networks.py:77-78
 RELATION_THRESHOLD = 170.0  # main.py:71 / :91
 
 
@@ -115,24 +115,24 @@ def forward_dense(p, objects, Rs, Rr, prop, mp_steps: int = REF_MP_STEPS,
 
     objects (B,N,3)  Rs, Rr (B,N,E)  prop (B,N,100).  ``drop_r`` (B,E,150) / ``drop_o``
     (B,N,100) are multiplicative inverted-dropout masks (None = inference / dropout off).
-    The reference returns sigmoid(logits)[..., None] (Networks.py:184-186).
+    The reference returns sigmoid(logits)[..., None] (Networks.py:94-96).
     """
-    Rs_t = Rs.transpose(1, 2)                       # Permute((2,1))  Networks.py:117-118
+    Rs_t = Rs.transpose(1, 2)                       # Permute((2,1))  Networks.py:27-28
     Rr_t = Rr.transpose(1, 2)
-    senders = torch.bmm(Rs_t, objects)              # Networks.py:122
-    receivers = torch.bmm(Rr_t, objects)            # Networks.py:123
-    diff = receivers[..., 0:2] - senders[..., 0:2]  # Networks.py:148-152
+    senders = torch.bmm(Rs_t, objects)              # Networks.py:32
+    receivers = torch.bmm(Rr_t, objects)            # Networks.py:33
+    diff = receivers[..., 0:2] - senders[..., 0:2]  # Networks.py:58-62
     obj_vec = torch.cat([objects[..., 1:2], objects[..., 2:3]], dim=-1)  # :155-161
-    c_r = torch.relu(_mlp(diff, p, "rm"))           # Networks.py:165
-    c_o = torch.relu(_mlp(obj_vec, p, "om"))        # Networks.py:166
-    if drop_r is not None:                          # Networks.py:167-168
+    c_r = torch.relu(_mlp(diff, p, "rm"))           # Networks.py:75
+    c_o = torch.relu(_mlp(obj_vec, p, "om"))        # Networks.py:76
+    if drop_r is not None:                          # Networks.py:77-78
         c_r = c_r * drop_r
     if drop_o is not None:
         c_o = c_o * drop_o
     P = prop
     states = [P]
     x = None
-    for _ in range(mp_steps):                       # Networks.py:173
+    for _ in range(mp_steps):                       # Networks.py:83
         ps = torch.bmm(Rs_t, P)                     # :174
         pr = torch.bmm(Rr_t, P)                     # :175
         x = _mlp(torch.cat([c_r, ps, pr], dim=-1), p, "rmp")       # :176-177
@@ -224,7 +224,7 @@ def forward_loop_numpy(params: Dict[str, np.ndarray], objects: np.ndarray, Rs: n
 
 
 # ---------------------------------------------------------------------------------------
-# Keras semantics: loss, metric, optimizer (Networks.py:191-192).
+# Keras semantics: loss, metric, optimizer (Networks.py:101-102).
 # ---------------------------------------------------------------------------------------
 KERAS_EPS = 1e-7
 LOGIT_CLIP = math.log((1.0 - KERAS_EPS) / KERAS_EPS)   # ≈ 16.118

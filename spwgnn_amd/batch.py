@@ -1,7 +1,7 @@
 """TowerBatch: the reference's 4-tensor input dict, compacted for the HIP kernels.
 
 The reference feeds Keras (B, N, 3) objects, two dense (B, N, E) one-hot relation matrices and a
-(B, N, 100) propagation state (src/Networks.py:112-119; built by src/main.py:66-93). Every active
+(B, N, 100) propagation state (src/Networks.py:22-29; built by src/main.py:66-93). Every active
 relation column is one sender and one receiver, so the batch becomes a union graph: node rows
 (objects, propagation) and an edge list, packed by the C library into wave-tiles of whole towers
 and 32-edge blocks (spwgnn_plan_size/fill). Conversion happens once per batch on the host (C++);
@@ -121,7 +121,7 @@ class TowerBatch:
     @staticmethod
     def from_dense(objects, sender_relations, receiver_relations, propagation=None, device="cuda",
                    nw_max: Optional[int] = None) -> "TowerBatch":
-        """The reference input dict (Networks.py:112-119) → compact batch (C++ conversion)."""
+        """The reference input dict (Networks.py:22-29) → compact batch (C++ conversion)."""
         to_np = lambda x: x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
         obj = np.ascontiguousarray(to_np(objects), np.float32)
         Rs = np.ascontiguousarray(to_np(sender_relations), np.float32)

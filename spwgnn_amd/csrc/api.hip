@@ -56,9 +56,16 @@ struct Ws {
 static constexpr int kMaxChunks = 256;   // slabs per weight gradient (the ws kernels: one per CU)
 static constexpr int kWgSlots = kMaxReduce; // weight gradients per backward, reduced by one batched launch
 static constexpr int kW2gWgs = 256;   // W2 gradient: one workgroup per CU (MI355X: 256 CUs)
+// Diagnosis switches (A/B of superseded kernels, per-kernel math) exist only in -DSPWGNN_DIAG builds;
+// the shipping library has no environment-dependent code path.
 static bool getenv_flag(const char* name) {
+#ifdef SPWGNN_DIAG
     const char* e = getenv(name);
     return e && *e && *e != '0';
+#else
+    (void)name;
+    return false;
+#endif
 }
 
 static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
@@ -234,10 +241,14 @@ static int32_t validate(const spwgnn_batch* b, const spwgnn_run* r) {
 enum : int { kX6EncEdge = 1, kX6EdgeFwd = 2, kX6NodeFwd = 4, kX6NodeBwd = 8, kX6EdgeBwd = 16, kX6EncEdgeBwd = 32,
              kX6Wgrad = 64 };
 static int kmath(const spwgnn_run* r, int bit) {
+#ifdef SPWGNN_DIAG
     static const int mask = [] {
         const char* e = getenv("SPWGNN_X6_KERNELS");
         return e ? (int)strtol(e, nullptr, 0) : -1;
     }();
+#else
+    constexpr int mask = -1;
+#endif
     return (r->math != MATH_F32 && (mask & bit)) ? r->math : MATH_F32;
 }
 

@@ -13,7 +13,7 @@ namespace spw {
 const ParamTable& param_table() {
     static const ParamTable t = [] {
         ParamTable pt{};
-        // Networks.py:136-140 — (input width, layer widths) per MLP, Keras layer order.
+        // Networks.py:46-50 — (input width, layer widths) per MLP, Keras layer order.
         struct Spec { const char* mlp; int fin; int n; int w[4]; };
         const Spec specs[4] = {{"rm", 2, 4, {150, 150, 150, 150}},
                                {"om", 2, 2, {100, 100, 0, 0}},
@@ -83,7 +83,7 @@ int32_t spwgnn_param_tensor(int32_t index, spwgnn_param_info* out) {
     return SPWGNN_OK;
 }
 
-// main.py:66-81 / JengaBuilder.py:313-326 build Rs/Rr; Networks.py:122-123,174-175,178 consume them.
+// main.py:66-81 / JengaBuilder.py:313-326 build Rs/Rr; Networks.py:32-33,84-85,88 consume them.
 int32_t spwgnn_dense_to_edges(const float* Rs, const float* Rr, int32_t B, int32_t N, int32_t* src,
                               int32_t* dst, int32_t* slot, int64_t capacity, int64_t* n_edges,
                               int32_t* tower_edge_count) {
@@ -193,6 +193,7 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
         wtile[4 * w + 1] = nblk;
         wtile[4 * w + 2] = (int32_t)n0;
         wtile[4 * w + 3] = (int32_t)(n1 - n0);
+        int32_t te = t0;   // tower owning edge e (walks alongside e: edges are tower-major)
         for (int32_t b = 0; b < nblk; ++b, ++blk) {
             uint8_t* csr = blk_csr + (int64_t)blk * 128;
             // csr[0:32] recv order, [32:64] recv local node, [64:96] send order, [96:128] send node
@@ -202,8 +203,11 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
                 const int64_t e = e0 + (int64_t)b * 32 + i;
                 const int64_t o = (int64_t)blk * 32 + i;
                 if (e < e1) {
+                    while (e >= edge_off[te + 1]) ++te;
                     const int32_t s = src[e], d = dst[e];
-                    if (s < n0 || s >= n1 || d < n0 || d >= n1) return SPWGNN_E_RELATION;  // edge leaves its tower
+                    // an edge must stay inside its own tower (not merely inside the packed wave-tile)
+                    if (s < node_off[te] || s >= node_off[te + 1] || d < node_off[te] || d >= node_off[te + 1])
+                        return SPWGNN_E_RELATION;
                     edge_src[o] = s;
                     edge_dst[o] = d;
                     if (edge_id) edge_id[o] = (int32_t)e;

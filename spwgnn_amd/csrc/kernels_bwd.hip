@@ -1,4 +1,4 @@
-// Backward kernels of the propagation network (replaces TF autodiff of Networks.py:121-186).
+// Backward kernels of the propagation network (replaces TF autodiff of Networks.py:31-96).
 //
 // Per step s (reverse order):
 //   k_node_bwd   dP_{s+1} = dPpart + dU_{s+1}·W1bᵀ + dV_{s+1}·W1cᵀ;  dx' = [dP ⊙ (1-P²) | dlogit];
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int r = 0; r < 16; ++r) {
                 const int f = rho(r, 0) + 4 * h + 32 * t;
                 const float p = Pn[t][r];
-                D[t][r] = f < kFN ? D[t][r] * (1.f - p * p) : 0.f;  // tanh' (Networks.py:181)
+                D[t][r] = f < kFN ? D[t][r] * (1.f - p * p) : 0.f;  // tanh' (Networks.py:91)
             }
     }
     // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
             for (int r = 0; r < 16; ++r) {
                 const int f = rho(r, 0) + 4 * h + 32 * t;
                 const float p = Pn[t][r];
-                D[c][t][r] = f < kFN ? D[c][t][r] * (1.f - p * p) : 0.f;  // tanh' (Networks.py:181)
+                D[c][t][r] = f < kFN ? D[c][t][r] * (1.f - p * p) : 0.f;  // tanh' (Networks.py:91)
             }
         // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
         if (has[c]) store_cm<4>(a.dPout + bN(c), D[c], lane, valid[c]);
@@ -829,7 +829,11 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
     }
     if (math == MATH_X6 && a.nw_max <= 16) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
+#ifdef SPWGNN_DIAG   // 1: drop the dA writes (diagnosis only: wrong results)
         static const int dbg = getenv("SPWGNN_EBWD_DBG") ? atoi(getenv("SPWGNN_EBWD_DBG")) : 0;
+#else
+        constexpr int dbg = 0;
+#endif
         if (dbg == 1) {
             if (a.dA_accumulate)
                 hipLaunchKernelGGL((k_edge_bwd_x6<true, 1>), g, b, 0, st, a);

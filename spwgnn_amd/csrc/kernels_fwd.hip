@@ -1,12 +1,12 @@
-// Forward kernels of the propagation network (Networks.py:121-186) for gfx950.
+// Forward kernels of the propagation network (Networks.py:31-96) for gfx950.
 //
 //   k_prep_weights   zero-padded / transposed / permuted copies of the 22 Keras tensors
-//   k_enc_node       om encoder (Networks.py:166,168) + P0 copy + first U/V projections
-//   k_enc_edge       rm encoder (Networks.py:165,167) + step-invariant part of rmp layer 1
+//   k_enc_node       om encoder (Networks.py:76,78) + P0 copy + first U/V projections
+//   k_enc_edge       rm encoder (Networks.py:75,77) + step-invariant part of rmp layer 1
 //   k_edge_fwd       per step: h1 = relu(A + U[s] + V[r]) → h2 = relu(h1·W2 + b2) → receiver
-//                    segment sum (Networks.py:174-178, with rmp layer 3 moved behind the sum)
+//                    segment sum (Networks.py:84-88, with rmp layer 3 moved behind the sum)
 //   k_node_fwd       per step: rmp layer 3 on the summed messages, tanh, omp, state update,
-//                    readout, next-step U/V (Networks.py:178-186)
+//                    readout, next-step U/V (Networks.py:88-96)
 #include <type_traits>
 #include "kernels.h"
 #include <cstdlib>
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const bool valid = n < a.n_nodes;
     const int nc = valid ? n : a.n_nodes - 1;
     const float4 p = reinterpret_cast<const float4*>(a.pos)[nc];
-    const float o0 = p.y, o1 = p.z;  // Networks.py:155-161: (y, width)
+    const float o0 = p.y, o1 = p.z;  // Networks.py:65-71: (y, width)
 
     f32x16 Z[4];
 #pragma unroll
@@ -89,8 +89,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     f32x16 C[4];
     zero_tiles(C);
     tchain_acc<4, 4, 4, kLdN>(Z, C, a.w_om1, lane);
-    bias_act_rho<4, true>(C, a.b_om1, h);  // relu(om(.)) — Networks.py:166
-    if (a.dropout_on) {                    // Networks.py:168
+    bias_act_rho<4, true>(C, a.b_om1, h);  // relu(om(.)) — Networks.py:76
+    if (a.dropout_on) {                    // Networks.py:78
         const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
     store_cm<4>(a.co + bN, C, lane, valid);
 
-    // P0: the 'propagation' input (Networks.py:119,169), ld 100 → workspace ld 128
+    // P0: the 'propagation' input (Networks.py:29,79), ld 100 → workspace ld 128
     f32x16 P[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     const bool valid = n < a.n_nodes;
     const int nc = valid ? n : a.n_nodes - 1;
     const float4 p = reinterpret_cast<const float4*>(a.pos)[nc];
-    const float o0 = p.y, o1 = p.z;  // Networks.py:155-161: (y, width)
+    const float o0 = p.y, o1 = p.z;  // Networks.py:65-71: (y, width)
     f32x16 Z[1][4], C[1][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     if (a.zo1) store_cm<4>(a.zo1 + bN, Z[0], lane, valid);
     zero_tiles(C[0]);
     tchain_x6<4, 7, 4, 1, kX6Ring, NP>(Z, C, a.x_om1, lane);
-    bias_act_rho<4, true>(C[0], a.b_om1, h);  // relu(om(.)) — Networks.py:166
-    if (a.dropout_on) {                       // Networks.py:168
+    bias_act_rho<4, true>(C[0], a.b_om1, h);  // relu(om(.)) — Networks.py:76
+    if (a.dropout_on) {                       // Networks.py:78
         const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
             }
     }
     store_cm<4>(a.co + bN, C[0], lane, valid);
-    // P0: the 'propagation' input (Networks.py:119,169), ld 100 → workspace ld 128 (Z's registers)
+    // P0: the 'propagation' input (Networks.py:29,79), ld 100 → workspace ld 128 (Z's registers)
     f32x16 (&P)[1][4] = Z;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     if (valid) {
         const float4 ps = reinterpret_cast<const float4*>(a.pos)[s];
         const float4 pd = reinterpret_cast<const float4*>(a.pos)[d];
-        dx = pd.x - ps.x;  // Networks.py:148-152 (receiver − sender), (x, y)
+        dx = pd.x - ps.x;  // Networks.py:58-62 (receiver − sender), (x, y)
         dy = pd.y - ps.y;
     }
     f32x16 X[5], Y[5];
@@ -241,8 +241,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
     zero_tiles(Y);
     tchain_acc<5, 5, 12, kLdE>(X, Y, a.w_rm3, lane);
-    bias_act_rho<5, true>(Y, a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:165
-    if (a.dropout_on && valid) {           // Networks.py:167
+    bias_act_rho<5, true>(Y, a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:75
+    if (a.dropout_on && valid) {           // Networks.py:77
         const uint32_t tw = (uint32_t)a.node_tower[s];
         const uint32_t key = drop_row_key(a.seed, 1u, tw, (uint32_t)a.node_local[s], (uint32_t)a.node_local[d]);
 #pragma unroll
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
         if (src[c] >= 0) {
             const float4 ps = reinterpret_cast<const float4*>(a.pos)[src[c]];
             const float4 pd = reinterpret_cast<const float4*>(a.pos)[dst[c]];
-            dx = pd.x - ps.x;  // Networks.py:148-152 (receiver − sender), (x, y)
+            dx = pd.x - ps.x;  // Networks.py:58-62 (receiver − sender), (x, y)
             dy = pd.y - ps.y;
         }
         if (TRAIN && a.ed && h == 0 && blk < a.n_eblocks) a.ed[e] = make_float2(dx, dy);
@@ -324,8 +324,8 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     tchain_x6<5, 10, 5, NC, kX6Ring, NP>(X, Y, a.x_rm3, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        bias_act_rho<5, true>(Y[c], a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:165
-        if (a.dropout_on && src[c] >= 0) {         // Networks.py:167
+        bias_act_rho<5, true>(Y[c], a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:75
+        if (a.dropout_on && src[c] >= 0) {         // Networks.py:77
             const uint32_t tw = (uint32_t)a.node_tower[src[c]];
             const uint32_t key = drop_row_key(a.seed, 1u, tw, (uint32_t)a.node_local[src[c]], (uint32_t)a.node_local[dst[c]]);
 #pragma unroll
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Receiver segment sum of one wave-tile on the matrix core (Networks.py:178 dot(receiver_relations,
+// Receiver segment sum of one wave-tile on the matrix core (Networks.py:88 dot(receiver_relations,
 // x)). C reg r of tile t of the h2 accumulators holds h2[edge rho(r,h)][feature 32t+i] — exactly a
 // B operand whose k index runs over the edges, so  nodes += onehot(dst)·h2  needs no lane movement.
 //  NW16 (≤ 16 nodes): 16x16x4 MFMAs, 10 tiles of 16 nodes × 16 features (40 registers). Lane l of
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const int s = cur.x, d = cur.y;
         const bool valid = s >= 0;
         const int sc = valid ? s : n0, dc = valid ? d : n0;
-        // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:174-177), lane = edge, split
+        // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:84-87), lane = edge, split
         // halves, streamed 4 features at a time straight into h2 = h1·W2 (rmp layer 2).
         const uint64_t vmask = __ballot(valid);
         const float vf = valid ? 1.f : 0.f;
@@ -564,10 +564,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 // ------------------------------------------------------------------------------------------------
 // One propagation step, node side (transposed orientation, 32 nodes per wave).
-//   a  = tanh([H2s | deg]·[W3; b3])              (Networks.py:178, layer 3 after the sum)
-//   o1 = relu([c_o | a | P]·Wo1 + bo1)            (Networks.py:179-180, omp layer 1)
+//   a  = tanh([H2s | deg]·[W3; b3])              (Networks.py:88, layer 3 after the sum)
+//   o1 = relu([c_o | a | P]·Wo1 + bo1)            (Networks.py:89-90, omp layer 1)
 //   x' = o1·Wo2' + bo2'   (x' = x with the logit moved to column 100)
-//   P' = tanh(x'[0:100] + P); logit = x'[100]     (Networks.py:181, 184)
+//   P' = tanh(x'[0:100] + P); logit = x'[100]     (Networks.py:91, 184)
 //   U' = P'·W1b, V' = P'·W1c for the next step
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node_fwd(NodeFwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
@@ -1110,7 +1110,11 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
         return hipGetLastError();
     }
     if (math == MATH_X6) {
+#ifdef SPWGNN_DIAG   // 1: A rows from 8 cached blocks (diagnosis only: wrong results)
         static const int dbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;
+#else
+        constexpr int dbg = 0;
+#endif
         if (a.nw_max <= 16 && dbg == 1)   // diagnosis: A rows from 8 cached blocks
             hipLaunchKernelGGL((k_edge_fwd_x6<true, 1>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         else if (a.nw_max <= 16)

@@ -839,7 +839,7 @@ void k_wgrad_ws(WgWsArgs a) {
             R.d = a.xd[(s * a.x_sb + nb) * 32 + rr];
         } else if (XD == 2) {
             const float4 p = a.xp[min<int64_t>((s * a.x_sb + nb) * 32 + rr, a.count - 1)];
-            R.d = make_float2(p.y, p.z);   // Networks.py:155-161: (y, width)
+            R.d = make_float2(p.y, p.z);   // Networks.py:65-71: (y, width)
         } else {
 #pragma unroll
             for (int k = 0; k < W::NKX; ++k) R.x[k] = *reinterpret_cast<const float4*>(px + offx[k]);
@@ -954,7 +954,7 @@ __global__ void k_wgrad_reduce_all(ReduceBatch rb) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Keras binary_crossentropy (Networks.py:192): clip(ŷ, 1e-7, 1-1e-7) ≡ clamp(z, ±ln((1-ε)/ε)).
+// Keras binary_crossentropy (Networks.py:102): clip(ŷ, 1e-7, 1-1e-7) ≡ clamp(z, ±ln((1-ε)/ε)).
 constexpr float kLogitClip = 16.11809565f;
 
 __global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
@@ -1059,20 +1059,29 @@ hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st) {
+#ifdef SPWGNN_DIAG   // diagnosis variants (wrong results): see k_w2grad_ws's DBG bits
     static const int dbg = getenv("SPWGNN_W2G_DBG") ? atoi(getenv("SPWGNN_W2G_DBG")) : 0;
+#else
+    constexpr int dbg = 0;
+#endif
     const dim3 g(wgs), b(kW2gThreads);
     if (math == MATH_BF16) {
         hipLaunchKernelGGL((k_w2grad_ws<0, 1>), g, b, 0, st, a, blk_per_wg);
         return hipGetLastError();
     }
+    if (dbg == 0) {
+        hipLaunchKernelGGL(k_w2grad_ws<0>, g, b, 0, st, a, blk_per_wg);
+        return hipGetLastError();
+    }
+#ifdef SPWGNN_DIAG
     switch (dbg) {
-        case 0: hipLaunchKernelGGL(k_w2grad_ws<0>, g, b, 0, st, a, blk_per_wg); break;
         case 1: hipLaunchKernelGGL(k_w2grad_ws<1>, g, b, 0, st, a, blk_per_wg); break;
         case 4: hipLaunchKernelGGL(k_w2grad_ws<4>, g, b, 0, st, a, blk_per_wg); break;
         case 8: hipLaunchKernelGGL(k_w2grad_ws<8>, g, b, 0, st, a, blk_per_wg); break;
         case 33: hipLaunchKernelGGL(k_w2grad_ws<33>, g, b, 0, st, a, blk_per_wg); break;
         default: return hipErrorInvalidValue;
     }
+#endif
     return hipGetLastError();
 }
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,

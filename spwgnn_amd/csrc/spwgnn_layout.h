@@ -6,7 +6,7 @@
 
 namespace spw {
 
-// ---- model widths (Networks.py:119,136-140) ----
+// ---- model widths (Networks.py:29,46-50) ----
 constexpr int kFE = 150;    // relation widths (rm hidden/out, rmp hidden)
 constexpr int kFN = 100;    // object / state widths (om, effect, P, omp hidden)
 constexpr int kLdE = 160;   // row stride (floats) of every 150/151-wide array  (5 MFMA tiles of 32)

@@ -14,8 +14,8 @@ import torch
 from . import _lib, params as P
 from .batch import TowerBatch
 
-REF_MP_STEPS = 5       # Networks.py:173
-REF_DROPOUT = 0.1      # Networks.py:167-168
+REF_MP_STEPS = 5       # Networks.py:83
+REF_DROPOUT = 0.1      # Networks.py:77-78
 
 
 def _stream(device: torch.device) -> int:
@@ -64,6 +64,12 @@ class Workspace:
     def __init__(self, device):
         self.device = torch.device(device)
         self.buf: Optional[torch.Tensor] = None
+        self.fwd_key: Optional[tuple] = None   # what the last forward on this workspace stored
+
+    @staticmethod
+    def key(batch: TowerBatch, run: "RunConfig") -> tuple:
+        return (run.math, int(run.mp_steps), bool(run.training), float(run.dropout), int(run.seed),
+                batch.n_nodes, batch.n_eblocks, batch.n_wtiles)
 
     def get(self, nbytes: int) -> torch.Tensor:
         if self.buf is None or self.buf.numel() < nbytes:
@@ -92,6 +98,7 @@ def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Wo
     r = run.cstruct()
     st = _lib.lib().spwgnn_forward(flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(),
                                    logits.data_ptr(), _stream(batch.device))
+    ws.fwd_key = Workspace.key(batch, run) if st == 0 else None
     _lib.check(st, "spwgnn_forward")
     return logits
 
@@ -100,6 +107,11 @@ def backward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: W
              grads: Optional[torch.Tensor] = None, want_dprop: bool = False):
     if not run.training:
         raise _lib.SpwgnnError("backward needs a training forward on the same workspace")
+    if ws.buf is None or ws.fwd_key != Workspace.key(batch, run):
+        # the backward reads what the forward stored (masks, activations, packed weights); the split-
+        # bf16 maths do not store z1/zo1 at all, so a mismatched math or step count reads garbage
+        raise _lib.SpwgnnError("backward needs the training forward of the same batch and RunConfig "
+                               f"on this workspace (stored {ws.fwd_key}, asked {Workspace.key(batch, run)})")
     dlogits = dlogits.contiguous().to(torch.float32)
     _require_gpu(dlogits, "dlogits")
     if grads is None:

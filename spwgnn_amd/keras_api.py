@@ -1,12 +1,12 @@
 """Keras-shaped front end: PropagationNetwork.getModel(...) → model.fit / model.predict.
 
 Mirrors the reference call sites one-to-one so a driver written against the reference drops in:
-  * PropagationNetwork().getModel(n_objects, object_dim=3, relation_dim=1)  — Networks.py:102-194
+  * PropagationNetwork().getModel(n_objects, object_dim=3, relation_dim=1)  — Networks.py:12-104
     (one model per n_objects, cached; all models share rm/om/rmp/omp weights, :107-108, :130-146)
   * model.fit(x_dict, {'target': y}, batch_size=32, epochs=10, validation_split=0.2, shuffle=True,
     verbose=1)                                                            — main.py:92-98
   * model.predict(x_dict) → (B, N, 1) probabilities                       — JengaBuilder.py:328-329
-Compile semantics (Networks.py:191-192): Adam(lr=5e-4, decay=0) per model, binary_crossentropy,
+Compile semantics (Networks.py:101-102): Adam(lr=5e-4, decay=0) per model, binary_crossentropy,
 binary_accuracy. Every step runs through libspwgnn_hip (forward, BCE, backward, Adam).
 """
 from __future__ import annotations
@@ -69,12 +69,12 @@ class CompactDataset:
 
 
 class KerasModel:
-    """One compiled per-N model of the reference (Networks.py:189-194); weights shared via ``net``."""
+    """One compiled per-N model of the reference (Networks.py:99-104); weights shared via ``net``."""
 
     def __init__(self, net: GraphNetwork, n_objects: int, object_dim: int = 3, lr: float = 5e-4,
                  l2: float = 0.0):
         if object_dim != 3:
-            # Networks.py:160-163 + main.py:28-31/59-63: the object_dim=2 path of the reference is
+            # Networks.py:70-73 + main.py:28-31/59-63: the object_dim=2 path of the reference is
             # broken (om gets 1 feature, boxes[...,2] is out of range); only the Jenga layout runs.
             raise ValueError("only object_dim=3 ([x, y, width]) is supported, as in the working reference path")
         self.net = net
@@ -133,9 +133,8 @@ class KerasModel:
         objects = np.asarray(x["objects"], np.float32)
         target = np.asarray(y["target"], np.float32).reshape(objects.shape[0], -1)
         B = objects.shape[0]
-        # Keras: validation = the LAST fraction of the samples, taken before shuffling
-        n_val = int(B * validation_split) if validation_split else 0
-        n_tr = B - n_val
+        n_tr = keras_split_at(B, validation_split)
+        n_val = B - n_tr
         ds = CompactDataset(objects, x["sender_relations"], x["receiver_relations"], x.get("propagation"))
         rng = np.random.default_rng(seed)
         dev = self.net.device
@@ -172,9 +171,20 @@ class KerasModel:
         return hist
 
 
+def keras_split_at(n_samples: int, validation_split: float) -> int:
+    """Number of training samples Keras 2.x keeps for fit(validation_split=v) (main.py:96):
+    split_at = int(n · (1 − v)); the validation set is the LAST n − split_at samples, taken before
+    shuffling."""
+    if not validation_split:
+        return int(n_samples)
+    if not 0.0 < validation_split < 1.0:
+        raise ValueError("validation_split must be in [0, 1)")
+    return int(int(n_samples) * (1.0 - validation_split))
+
+
 class PropagationNetwork:
-    """Networks.py:102-194: getModel caches one compiled model per n_objects, all sharing the
-    weights of the first one built (set_weights / reuse_model, Networks.py:130-146)."""
+    """Networks.py:12-104: getModel caches one compiled model per n_objects, all sharing the
+    weights of the first one built (set_weights / reuse_model, Networks.py:40-56)."""
 
     def __init__(self, device="cuda", seed: int = 0, mp_steps: int = E.REF_MP_STEPS, dropout: float = E.REF_DROPOUT):
         self.Nets: Dict[int, KerasModel] = {}

@@ -1,6 +1,6 @@
 """GraphNetwork: the reference's propagation network as a torch module backed by libspwgnn_hip.
 
-Reference graph: src/Networks.py:106-194 (PropagationNetwork.getModel) over the MLP blocks of
+Reference graph: src/Networks.py:16-104 (PropagationNetwork.getModel) over the MLP blocks of
 src/Blocks.py:12-91. Inputs and output keep the reference layout: objects (B,N,3), sender/receiver
 relations (B,N,E), propagation (B,N,100) → per-object stability probability (B,N,1).
 """
@@ -39,8 +39,8 @@ class _PropagationFn(torch.autograd.Function):
 class GraphNetwork(nn.Module):
     """Propagation network (rm, om, rmp, omp) with shared weights across sizes and steps.
 
-    ``mp_steps`` defaults to the reference's 5 (Networks.py:173); ``dropout`` to its 0.1 on the
-    two encodings (Networks.py:167-168), active only in training mode.
+    ``mp_steps`` defaults to the reference's 5 (Networks.py:83); ``dropout`` to its 0.1 on the
+    two encodings (Networks.py:77-78), active only in training mode.
     """
 
     def __init__(self, mp_steps: int = E.REF_MP_STEPS, dropout: float = E.REF_DROPOUT, seed: int = 0,
@@ -78,7 +78,9 @@ class GraphNetwork(nn.Module):
         ws = E.Workspace(self.device)
         if prop is not None:
             batch = batch.with_prop(prop)
-            dummy = prop
+            # the backward returns dprop as (n_nodes, 100): autograd maps it back through the reshape
+            # to whatever layout the caller passed ((B, N, 100) in the reference)
+            dummy = prop.reshape(batch.n_nodes, 100)
         else:
             dummy = torch.zeros(0, device=self.device)
         if not run.training:
@@ -95,7 +97,7 @@ class GraphNetwork(nn.Module):
         return z.reshape(batch.node_shape)
 
     def forward(self, objects, sender_relations, receiver_relations, propagation=None) -> torch.Tensor:
-        """(B, N, 1) probabilities: sigmoid(x[:, :, :1]) of the last step (Networks.py:183-186)."""
+        """(B, N, 1) probabilities: sigmoid(x[:, :, :1]) of the last step (Networks.py:93-96)."""
         return torch.sigmoid(self.forward_logits(objects, sender_relations, receiver_relations, propagation))[..., None]
 
     def forward_pooled(self, objects, sender_relations, receiver_relations, propagation=None,

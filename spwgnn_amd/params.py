@@ -1,6 +1,6 @@
 """Flat parameter buffer ↔ Keras-layout tensors.
 
-The four MLPs of the reference (rm, om, rmp, omp — src/Networks.py:136-140; Dense stacks of
+The four MLPs of the reference (rm, om, rmp, omp — src/Networks.py:46-50; Dense stacks of
 src/Blocks.py:20-28 / 60-68) are stored in one flat fp32 buffer whose layout is defined by the
 C library (``spwgnn_param_tensor``): kernels in Keras (in, out) row-major layout, biases (out,),
 each tensor on a 64-float boundary. One flat buffer = one gradient bucket for the all-reduce and
@@ -16,7 +16,7 @@ import torch
 
 from . import _lib
 
-# Networks.py:136-140 (mirrors the C table; checked against it in tests)
+# Networks.py:46-50 (mirrors the C table; checked against it in tests)
 MLP_SPECS = {
     "rm": (2, [150, 150, 150, 150]),
     "om": (2, [100, 100]),

@@ -1,12 +1,19 @@
 """Data-parallel training step: towers sharded over ranks, one RCCL all-reduce of the flat gradient.
 
 The reference trains with Keras fit on one CPU process (src/main.py:92-98; Adam + BCE compiled at
-src/Networks.py:191-192). Here every rank owns a shard of the tower batch (towers are independent
+src/Networks.py:101-102). Here every rank owns a shard of the tower batch (towers are independent
 graphs, so the shard needs no halo and no data-path collective), runs forward → BCE → backward
 through libspwgnn_hip, and the 209,501 fp32 gradients (one flat bucket, 0.84 MB) are summed with
 ONE torch.distributed all-reduce (backend "nccl" = RCCL over xGMI on MI355X), then Adam runs on
-every rank with grad_scale = 1/world (mean over ranks of per-rank mean losses = global mean for
-equal shards).
+every rank.
+
+Weighting: the reference's loss is the mean BCE over all B·N nodes of the batch
+(src/Networks.py:102). A rank's backward yields the gradient of the mean over ITS nodes, so each
+rank scales its gradient by n_local / n_global before the sum; Σ_r (n_r/n)·g_r is then exactly
+the gradient of the global mean, for ragged and unequal shards alike (config 4). n_global comes
+from the shard plan (`spwgnn_amd/shard.py`) or, when not given, from one 8-byte all-reduce.
+Micro-batches (`step` with lists) accumulate their node-weighted gradients before the one
+all-reduce and the one Adam update.
 
 The arithmetic engine is pluggable only so the CPU test-suite can drive this control flow under
 gloo with the oracle; the product engine is HipEngine and has no CPU fallback.
@@ -65,22 +72,49 @@ class Trainer:
         self.prof_kernel = 0
         self.prof_events = None
 
-    def run_config(self) -> E.RunConfig:
-        # distinct dropout keys per step and per rank (a rank's towers are different towers)
-        key = (self.seed * 1_000_003 + self.iterations) * 4099 + self.rank
+    def run_config(self, micro: int = 0) -> E.RunConfig:
+        # distinct dropout keys per step, per rank and per micro-batch (different towers)
+        key = ((self.seed * 1_000_003 + self.iterations) * 4099 + self.rank) * 257 + micro
         return E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, seed=key, math=self.math,
                            prof_kernel=self.prof_kernel, prof_events=self.prof_events)
 
-    def step(self, batch: TowerBatch, target: torch.Tensor):
+    def step(self, batch, target, n_global: Optional[int] = None):
+        """One optimizer step. `batch`/`target` may be lists (micro-batches of this rank's shard);
+        `n_global` = nodes in the whole global batch (all ranks, all micro-batches)."""
+        batches = batch if isinstance(batch, (list, tuple)) else [batch]
+        targets = target if isinstance(target, (list, tuple)) else [target]
+        if len(batches) != len(targets) or not batches:
+            raise ValueError("one target per micro-batch")
+        n_local = sum(b.n_nodes for b in batches)
+        if n_global is None:
+            n_global = n_local
+            if self.world > 1:
+                t = torch.tensor([float(n_local)], dtype=torch.float64,
+                                 device=self.params.device if dist.get_backend(self.group) != "gloo" else "cpu")
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                n_global = int(t.item())
         run = self.run_config()
-        z = self.engine.forward(self.params, batch, run)
-        out3, dz = self.engine.loss(z, target)
-        grads = self.engine.backward(self.params, batch, run, dz)
-        gscale = 1.0
+        acc = None
+        outs = []
+        for i, (b, tg) in enumerate(zip(batches, targets)):
+            if i:
+                run = self.run_config(micro=i)
+            z = self.engine.forward(self.params, b, run)
+            out3, dz = self.engine.loss(z, tg)
+            outs.append(out3)
+            g = self.engine.backward(self.params, b, run, dz)
+            w = b.n_nodes / n_global
+            if len(batches) == 1:
+                acc = g
+                if w != 1.0:
+                    acc.mul_(w)
+            elif acc is None:
+                acc = g.mul(w)            # own buffer: the engine reuses its gradient buffer
+            else:
+                acc.add_(g, alpha=w)
         if self.world > 1:
-            dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group)
-            gscale = 1.0 / self.world
+            dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
         self.iterations += 1
-        self.engine.adam(self.params, grads, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
-                         self.l2, gscale)
-        return out3
+        self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
+                         self.l2, 1.0)
+        return outs[0] if len(outs) == 1 else outs

@@ -1,5 +1,7 @@
-"""CPU, world_size 2 over gloo: the data-parallel Trainer (tower shards + one all-reduce of the
-flat gradient + Adam with grad_scale = 1/world) equals a single-process step on the full batch.
+"""CPU, gloo: the data-parallel Trainer (tower shards + one all-reduce of the node-weighted flat
+gradient + Adam) equals a single-process step on the full batch — equal shards (world 2), unequal
+ragged shards of mixed tower sizes (worlds 2 and 4, cut by the cost planner and by hand), and
+micro-batch accumulation.
 
 The arithmetic engine here is the oracle (test infrastructure) injected into the product Trainer,
 so this covers the N>1 control flow without a GPU; the HIP engine runs the same Trainer on MI355X.
@@ -16,6 +18,7 @@ import torch.multiprocessing as mp
 from oracle import model as O
 from spwgnn_amd import data as D, params as P
 from spwgnn_amd.batch import TowerBatch
+from spwgnn_amd.shard import micro_batches, plan_shards, shard_weights, tower_cost
 from spwgnn_amd.trainer import Trainer
 
 
@@ -109,3 +112,103 @@ def test_dp_gloo_world2_equals_full_batch(tmp_path, steps):
     ref = _single(steps)
     assert np.abs(dp - ref).max() < 1e-9
     assert np.abs(ref - P.to_flat(O.random_params(11), dtype=torch.float64).numpy()).max() > 1e-6  # it moved
+
+
+# ---------------------------------------------------------------- ragged / unequal shards
+def _ragged_problem(T=11, seed=5):
+    """Towers of 3..8 boxes, thresholded relations (main.py:71-81), Bernoulli labels."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(3, 9, size=T)
+    raws = [D.synthetic_towers(1, int(n), seed=seed * 100 + i)[0] for i, n in enumerate(sizes)]
+    objs = [(r / D.RELATION_THRESHOLD).astype(np.float32) for r in raws]
+    tgts = [rng.integers(0, 2, size=int(n)).astype(np.float64) for n in sizes]
+    return objs, raws, tgts
+
+
+def _ragged_batch(objs, raws, a, b):
+    return TowerBatch.ragged(objs[a:b], relation_threshold=D.RELATION_THRESHOLD, device="cpu",
+                             raw_positions_list=raws[a:b])
+
+
+def _ragged_single(steps, micro=None):
+    objs, raws, tgts = _ragged_problem()
+    params = P.to_flat(O.random_params(11), dtype=torch.float64)
+    tr = Trainer(params, engine=OracleEngine(), mp_steps=2, dropout=0.0)
+    tr.m = torch.zeros_like(params)
+    tr.v = torch.zeros_like(params)
+    T = len(objs)
+    cuts = [(0, T)] if micro is None else [(a, min(a + micro, T)) for a in range(0, T, micro)]
+    bs = [_ragged_batch(objs, raws, a, b) for a, b in cuts]
+    ts = [torch.tensor(np.concatenate(tgts[a:b])) for a, b in cuts]
+    for _ in range(steps):
+        tr.step(bs if micro else bs[0], ts if micro else ts[0])
+    return params.numpy()
+
+
+def _ragged_worker(rank, world, port, steps, out, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    objs, raws, tgts = _ragged_problem()
+    T = len(objs)
+    tn = np.array([len(o) for o in objs])
+    if mode == "planned":
+        full = _ragged_batch(objs, raws, 0, T)
+        ranges = plan_shards(full.tower_nodes, full.tower_edges, world, mp_steps=2)
+        n_global = int(tn.sum())
+    else:                                   # hand-cut, deliberately unequal; n_global via all-reduce
+        cuts = [0, 3, T] if world == 2 else [0, 1, 4, 9, T]
+        ranges = [(cuts[r], cuts[r + 1]) for r in range(world)]
+        n_global = None
+    a, b = ranges[rank]
+    params = P.to_flat(O.random_params(11), dtype=torch.float64)
+    tr = Trainer(params, engine=OracleEngine(), mp_steps=2, dropout=0.0)
+    tr.m = torch.zeros_like(params)
+    tr.v = torch.zeros_like(params)
+    if mode == "micro":                     # this rank's shard as micro-batches of ≤ 2 towers
+        mbs = micro_batches(a, b, 2)
+        bs = [_ragged_batch(objs, raws, x, y) for x, y in mbs]
+        ts = [torch.tensor(np.concatenate(tgts[x:y])) for x, y in mbs]
+    else:
+        bs = _ragged_batch(objs, raws, a, b)
+        ts = torch.tensor(np.concatenate(tgts[a:b]))
+    for _ in range(steps):
+        tr.step(bs, ts, n_global=n_global)
+    if rank == 0:
+        np.save(out, params.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "planned"), (2, "unequal"), (4, "planned"), (4, "unequal"),
+                                        (2, "micro")])
+def test_dp_gloo_ragged_unequal_shards_equal_full_batch(tmp_path, world, mode):
+    out = str(tmp_path / "p.npy")
+    mp.start_processes(_ragged_worker, args=(world, _free_port(), 2, out, mode), nprocs=world, join=True,
+                       start_method="spawn")
+    dp = np.load(out)
+    ref = _ragged_single(2)
+    assert np.abs(dp - ref).max() < 1e-9
+
+
+def test_micro_batch_accumulation_equals_full_batch():
+    """Single process: micro-batches of 3 towers accumulate to the full-batch step."""
+    assert np.abs(_ragged_single(2, micro=3) - _ragged_single(2)).max() < 1e-9
+
+
+def test_plan_shards_balances_cost():
+    rng = np.random.default_rng(0)
+    n = rng.integers(4, 17, size=5000)
+    e = n * (n - 1)
+    cost = tower_cost(n, e)
+    for world in (1, 2, 3, 4, 8):
+        ranges = plan_shards(n, e, world)
+        assert ranges[0][0] == 0 and ranges[-1][1] == len(n)
+        assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+        per = np.array([cost[a:b].sum() for a, b in ranges])
+        assert np.abs(per - cost.sum() / world).max() <= cost.max()
+        w = shard_weights(n, ranges)
+        assert abs(w.sum() - 1.0) < 1e-12
+    # balanced by cost, not by tower count: big towers first → the first shard holds fewer towers
+    n2 = np.array([16] * 100 + [4] * 100)
+    r = plan_shards(n2, n2 * (n2 - 1), 2)
+    assert r[0][1] < 100

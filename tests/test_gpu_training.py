@@ -226,7 +226,7 @@ def test_keras_front_end_fit_and_predict():
                           torch.tensor(x["receiver_relations"][:5], dtype=torch.float64),
                           torch.zeros(5, 6, 100, dtype=torch.float64), 5).numpy()
     assert np.abs(probs[..., 0] - 1 / (1 + np.exp(-ref))).max() < 1e-5
-    m9 = pn.getModel(9)                      # a second size shares the weights (Networks.py:130-146)
+    m9 = pn.getModel(9)                      # a second size shares the weights (Networks.py:40-56)
     assert m9.net is model.net
 
 

@@ -202,3 +202,26 @@ def test_plan_without_any_edge_and_empty_batch():
     assert np.all(b.edge_src.numpy() == -1) and np.all(b.edge_dst.numpy() == -1)
     with pytest.raises(ValueError):
         TowerBatch.ragged([], device="cpu")
+
+
+def test_plan_rejects_cross_tower_edge_inside_one_packed_tile():
+    """Two 3-box towers pack into one 16-node wave-tile; an edge from tower 0 to tower 1 must still
+    be rejected (the check is against the edge's own tower, not the tile)."""
+    pos = np.zeros((6, 3), np.float32)
+    tn = np.array([3, 3], np.int32)
+    src = np.array([0, 1, 3, 2], np.int32)
+    dst = np.array([1, 0, 4, 4], np.int32)      # 2 → 4 crosses towers
+    with pytest.raises(_lib.SpwgnnError):
+        TowerBatch.from_edges(pos, tn, src, dst, np.array([2, 2], np.int32), device="cpu", nw_max=16)
+    ok = TowerBatch.from_edges(pos, tn, src[:3], np.array([1, 0, 4], np.int32), np.array([2, 1], np.int32),
+                               device="cpu", nw_max=16)
+    assert ok.n_wtiles == 1
+
+
+@pytest.mark.parametrize("B,v", [(7, 0.2), (13, 0.2), (10, 0.2), (96, 0.25), (5, 0.0), (3, 0.5)])
+def test_keras_validation_split_matches_keras2(B, v):
+    """Keras 2.x fit: split_at = int(B·(1 − v)) training samples, the rest is validation (main.py:96)."""
+    from spwgnn_amd.keras_api import keras_split_at
+    assert keras_split_at(B, v) == (int(int(B) * (1.0 - v)) if v else B)
+    if (B, v) == (7, 0.2):
+        assert keras_split_at(B, v) == 5
