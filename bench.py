@@ -1,6 +1,17 @@
 #!/usr/bin/env python3
-"""Benchmark: towers/s of one full training step (forward + BCE + backward [+ RCCL all-reduce] +
-Adam) on synthetic 6-block Jenga towers, 65,536 towers per GPU, 5 propagation steps, fp32.
+"""Benchmark: towers/s of the propagation-network hot path on MI355X, per BASELINE.json config.
+
+Default (the headline metric): one full training step (forward + BCE + backward [+ RCCL
+all-reduce] + Adam) on synthetic 6-block Jenga towers, 65,536 towers per GPU, 5 propagation steps,
+dropout 0.1, fp32-class (x6) arithmetic. `--config K` runs BASELINE.json configs[K-1] instead:
+
+  1  6-block towers, 32 per batch, S=1, thresholded relations (the reference's CPU path; the GPU
+     step is launch-bound at this size — the line exists so the CPU baseline has its GPU twin)
+  2  6-block towers, 4,096 per GPU, S=3, thresholded relations, fp32-class (x6)
+  3  12-block fully connected towers, 65,536 per GPU, S=5, bf16 arithmetic
+  4  ragged 4–16-block towers, 2^20 over 8 GPUs = 131,072 per GPU trained as 2 micro-batches of
+     65,536, thresholded relations, S=5, bf16 arithmetic
+  5  32-block fully connected towers, 8,192 per GPU, S=10, forward only, hipGraph replay
 
 Contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run, one
 rank per GPU). Prints ONE JSON line on rank 0. See DESIGN.md §7 for the roofline accounting.
@@ -32,27 +43,55 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA peak
 PEAK_HBM_GBS = 8000.0
 # x6 math runs each fp32 product as 6 bf16 MFMA products: its fp32-equivalent matrix peak
 PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
+MATH_PEAK = {"x6": PEAK_X6_TFLOPS, "f32": PEAK_FP32_TFLOPS, "bf16": PEAK_BF16_TFLOPS}
+PEAK_NOTE = {"x6": "x6: fp32 products as 6 bf16 MFMA products, peak = 2.5 PF bf16 / 6",
+             "f32": "f32 MFMA peak 157.3 TF", "bf16": "bf16 MFMA dense peak 2.5 PF"}
+MATH_DESC = {"x6": "x6: each fp32 matrix product as 6 bf16 MFMA products of 3-way split operands, fp32 "
+                   "accumulation (DESIGN.md §3b)", "f32": "f32 MFMA",
+             "bf16": "bf16: operands rounded to bf16, one bf16 MFMA product, fp32 accumulation"}
+
+# BASELINE.json configs (index = position + 1; 0 = the headline metric's configuration)
+CONFIGS = {
+    0: dict(nodes=6, towers=65536, S=5, math="x6", relations="full", mode="train"),
+    1: dict(nodes=6, towers=32, S=1, math="x6", relations="threshold", mode="train"),
+    2: dict(nodes=6, towers=4096, S=3, math="x6", relations="threshold", mode="train"),
+    3: dict(nodes=12, towers=65536, S=5, math="bf16", relations="full", mode="train"),
+    4: dict(nodes=(4, 16), towers=131072, S=5, math="bf16", relations="threshold", mode="train", micro=65536),
+    5: dict(nodes=32, towers=8192, S=10, math="x6", relations="full", mode="infer"),
+}
 
 # algorithmic FLOPs per launch of each timed kernel, as f(real edges, nodes, S)
 KERNELS = {
     "edge_fwd": (_lib.K_EDGE_FWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne),
     "edge_bwd": (_lib.K_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne),
+    "node_fwd": (_lib.K_NODE_FWD, lambda Ne, Nn, S: 2.0 * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150) * Nn),
+    "node_bwd": (_lib.K_NODE_BWD, lambda Ne, Nn, S: 2.0 * (2 * 150 * 100 + 101 * 100 + 300 * 100 + 150 * 100) * Nn),
     "wgrad_w2": (_lib.K_WGRAD_W2, lambda Ne, Nn, S: 2.0 * 151 * 150 * Ne * S),
     "enc_edge": (_lib.K_ENC_EDGE, lambda Ne, Nn, S: 2.0 * (2 * 150 + 4 * 150 * 150) * Ne),
     "enc_edge_bwd": (_lib.K_ENC_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 4 * 150 * 150 * Ne),
 }
-LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "wgrad_w2": 1, "enc_edge": 1, "enc_edge_bwd": 1}
+LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "node_fwd": "S", "node_bwd": "S", "wgrad_w2": 1,
+                     "enc_edge": 1, "enc_edge_bwd": 1}
+# device kernel name prefix in the rocprofv3 PMC summaries (tools/pmcsum.py)
+PMC_PREFIX = {"edge_fwd": "k_edge_fwd", "edge_bwd": "k_edge_bwd", "node_fwd": "k_node_fwd",
+              "node_bwd": "k_node_bwd", "wgrad_w2": "k_w2grad", "enc_edge": "k_enc_edge<",
+              "enc_edge_bwd": "k_enc_edge_bwd"}
+
+
+def fwd_flops(Ne: int, Nn: int, S: int) -> float:
+    """Forward FLOPs as the kernels compute them (rmp layer 3 behind the receiver sum)."""
+    return 2.0 * (Ne * (2 * 150 + 4 * 150 * 150) + Nn * (2 * 100 + 100 * 100)
+                  + S * (Ne * 150 * 150 + Nn * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150))
+                  - Nn * 2 * 100 * 150)
 
 
 def step_flops(Ne: int, Nn: int, S: int) -> float:
     """Algorithmic FLOPs of one fwd+bwd training step in the form the kernels compute."""
-    fwd = Ne * (2 * 150 + 4 * 150 * 150) + Nn * (2 * 100 + 100 * 100) \
-        + S * (Ne * 150 * 150 + Nn * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150)) - Nn * 2 * 100 * 150
     bwd_edge = Ne * (4 * 150 * 150 + 4 * 151 * 150 + 3 * 100) + S * Ne * (150 * 150 + 151 * 150)
     bwd_node = Nn * (100 * 100 + 101 * 100 + 3 * 100) + S * Nn * (
         2 * 150 * 100 + 101 * 100 + 300 * 100 + 150 * 100     # activation grads
         + 2 * 100 * 150 + 151 * 100 + 301 * 100 + 101 * 101)  # weight grads
-    return 2.0 * (fwd + bwd_edge + bwd_node)
+    return fwd_flops(Ne, Nn, S) + 2.0 * (bwd_edge + bwd_node)
 
 
 class HipEvents:
@@ -78,32 +117,96 @@ class HipEvents:
             self.hip.hipEventDestroy(C.c_void_p(e))
 
 
-def cpu_baseline_pair(n_objects: int, S: int, seconds: float):
-    """The oracle at up to 16 host threads (the reported baseline) and at 1 thread."""
-    many = cpu_baseline(n_objects, S, seconds)
-    one = cpu_baseline(n_objects, S, max(3.0, seconds / 3), threads=1)
-    many["value_1thread"] = one["value"]
-    many["sample"] += f"; 1 thread: {one['value']:.1f} towers/s ({one['sample'].split(', ')[2]})"
-    return many
+# ------------------------------------------------------------------------------ workloads
+def make_workload(cfg: dict, rank: int, device):
+    """The synthetic batch (or micro-batches) of one rank and their targets."""
+    B, S = cfg["towers"], cfg["S"]
+    rng = np.random.default_rng(rank)
+    if isinstance(cfg["nodes"], tuple):            # config 4: ragged, micro-batched shard
+        from spwgnn_amd import shard
+        lo, hi = cfg["nodes"]
+        pos, sizes, src, dst, te, _ = D.ragged_batch(B, lo, hi, seed=4000 + rank,
+                                                     threshold=D.RELATION_THRESHOLD if cfg["relations"] == "threshold" else None)
+        batches, targets = [], []
+        for a, b in shard.micro_batches(0, B, cfg.get("micro", B)):
+            part = D.edge_slice(pos, sizes, src, dst, te, a, b)
+            bt = TowerBatch.from_edges(*part, device=device)
+            batches.append(bt)
+            targets.append(torch.tensor(rng.integers(0, 2, size=bt.n_nodes).astype(np.float32), device=device))
+        return batches, targets
+    N = cfg["nodes"]
+    raw = D.synthetic_towers(B, N, seed=1000 + rank + 97 * N)
+    objects = (raw / D.RELATION_THRESHOLD).astype(np.float32)
+    if cfg["relations"] == "full":
+        batch = TowerBatch.fully_connected(objects, device=device)
+    else:
+        Rs, Rr = D.relation_matrices(raw, D.RELATION_THRESHOLD)
+        batch = TowerBatch.from_dense(objects, Rs, Rr, None, device=device)
+    target = torch.tensor(rng.integers(0, 2, size=B * N).astype(np.float32), device=device)
+    return [batch], [target]
 
 
-def cpu_baseline(n_objects: int, S: int, seconds: float, threads=None):
-    """The oracle (torch-CPU restatement of Networks.py, literal dense one-hot form, fp32 like
-    Keras floatx) timed fwd+bwd on a bounded sample on this host's cores."""
+def workload_name(cfg: dict, world: int, dropout: float) -> str:
+    N = cfg["nodes"]
+    nd = f"{N[0]}-{N[1]}-block ragged" if isinstance(N, tuple) else f"{N}-block"
+    rel = "fully connected" if cfg["relations"] == "full" else "thresholded relations (raw distance < 170)"
+    if cfg["mode"] == "infer":
+        return f"forward, {nd} towers {rel}, {cfg['towers']} towers/GPU, {cfg['S']} MP steps, hipGraph replay"
+    mb = f" as micro-batches of {cfg['micro']}" if cfg.get("micro") else ""
+    return (f"train step fwd+BCE+bwd+{'allreduce+' if world > 1 else ''}Adam, {nd} towers {rel}, "
+            f"{cfg['towers']} towers/GPU{mb}, {cfg['S']} MP steps, dropout {dropout}, {cfg['math']} math")
+
+
+# ------------------------------------------------------------------------------ CPU baseline
+def cpu_sample(cfg: dict, n_sample: int):
+    """A bounded sample of the config's towers for the oracle: (objects, Rs, Rr) groups of equal N."""
+    N = cfg["nodes"]
+    thr = D.RELATION_THRESHOLD if cfg["relations"] == "threshold" else None
+    if isinstance(N, tuple):
+        pos, sizes, src, dst, te, raw = D.ragged_batch(n_sample, N[0], N[1], seed=77, threshold=thr)
+        groups = []
+        for n in np.unique(sizes):
+            r = np.stack([raw[t] for t in np.nonzero(sizes == n)[0]])
+            groups.append(((r / D.RELATION_THRESHOLD).astype(np.float32),) + D.relation_matrices(r, thr))
+        return groups
+    raw = D.synthetic_towers(n_sample, N, seed=123)
+    return [((raw / D.RELATION_THRESHOLD).astype(np.float32),) + D.relation_matrices(raw, thr)]
+
+
+def cpu_time(cfg: dict, seconds: float, threads: int, form: str):
+    """The oracle (torch-CPU restatement of Networks.py, fp32 like Keras floatx) on a bounded sample:
+    fwd+bwd for training configs, forward only for inference; `form` = "dense" (the literal one-hot
+    bmm graph Keras executes) or "gather" (index gather + index_add)."""
     from oracle import model as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0)))) if threads is None else threads
     torch.set_num_threads(threads)
-    B = 256
-    obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, n_objects, seed=123, fully_connected=True)
-    p = O.to_torch(O.glorot_uniform_params(0), dtype=torch.float32, requires_grad=True)
-    ts = [torch.tensor(a, dtype=torch.float32) for a in (obj, Rs, Rr, prop)]
-    t = torch.tensor(tgt, dtype=torch.float32)
+    S = cfg["S"]
+    infer = cfg["mode"] == "infer"
+    n_sample = 16 if infer else (64 if cfg["nodes"] in (12,) or isinstance(cfg["nodes"], tuple) else 256)
+    n_sample = min(n_sample, cfg["towers"])
+    groups = cpu_sample(cfg, n_sample)
+    p = O.to_torch(O.glorot_uniform_params(0), dtype=torch.float32, requires_grad=not infer)
+    prepared = []
+    for obj, Rs, Rr in groups:
+        B, N = obj.shape[:2]
+        t = torch.tensor(np.random.default_rng(0).integers(0, 2, size=(B, N)).astype(np.float32))
+        if form == "dense":
+            args = tuple(torch.tensor(a, dtype=torch.float32) for a in (obj, Rs, Rr)) + (torch.zeros(B, N, 100),)
+        else:
+            e = np.array(O.dense_to_edges(Rs, Rr), np.int64).reshape(-1, 4)   # (tower, slot, sender, receiver)
+            args = (torch.tensor(obj.reshape(B * N, 3)), torch.as_tensor(e[:, 0] * N + e[:, 2]),
+                    torch.as_tensor(e[:, 0] * N + e[:, 3]), torch.zeros(B * N, 100))
+        prepared.append((args, t))
 
     def one():
-        for v in p.values():
-            v.grad = None
-        z = O.forward_dense(p, *ts, S)
-        O.keras_bce_from_logits(z, t).backward()
+        for args, t in prepared:
+            if infer:
+                with torch.no_grad():
+                    (O.forward_dense if form == "dense" else O.forward_gather)(p, *args, S)
+                continue
+            for v in p.values():
+                v.grad = None
+            z = (O.forward_dense if form == "dense" else O.forward_gather)(p, *args, S)
+            O.keras_bce_from_logits(z.reshape(t.shape), t).backward()
 
     one()
     n, t0 = 0, time.perf_counter()
@@ -111,86 +214,127 @@ def cpu_baseline(n_objects: int, S: int, seconds: float, threads=None):
         one()
         n += 1
         el = time.perf_counter() - t0
-        if (el > seconds and n >= 3) or n >= 200:
+        if (el > seconds and n >= 3) or n >= 500:
             break
-    return {"value": B * n / el, "unit": "towers/s", "cores": threads, "kind": "port",
-            "sample": f"oracle.forward_dense fp32 fwd+bwd, {B} towers x {n} iters, N={n_objects}, S={S}, "
-                      f"{el:.1f}s, torch CPU threads={threads}"}
+    return n_sample * n / el, f"{n_sample} towers x {n} iters, {el:.1f}s"
 
 
-# device kernel whose PMC summary (profiles/pmc_summary.json, tools/pmcsum.py) holds the HBM
-# bytes of a bench kernel
-PMC_NAMES = {
-    "f32": {"edge_fwd": "k_edge_fwd<true>", "edge_bwd": "k_edge_bwd<true, true>", "enc_edge": "k_enc_edge<true>",
-            "enc_edge_bwd": "k_enc_edge_bwd", "wgrad_w2": "k_wgrad_t<4, 2, 160, 160>"},
-    "x6": {"edge_fwd": "k_edge_fwd_x6<true, 0, 3>", "edge_bwd": "k_edge_bwd_x6<true, 0, 3>",
-           "enc_edge": "k_enc_edge_x6<true, 2, 3>", "enc_edge_bwd": "k_enc_edge_bwd_x6<2, 3>",
-           "wgrad_w2": "k_w2grad_ws<0, 3>"},
-}
+def cpu_baseline(cfg: dict, seconds: float):
+    """SURVEY §8d / BASELINE.md CPU plan: the oracle at up to 16 host threads (the reported value: the
+    literal dense form Keras runs), its gather form, and 1 thread; timed on this host's cores."""
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    dense, dsamp = cpu_time(cfg, seconds, threads, "dense")
+    gather, gsamp = cpu_time(cfg, seconds / 2, threads, "gather")
+    one, osamp = cpu_time(cfg, max(3.0, seconds / 4), 1, "dense")
+    what = "fwd" if cfg["mode"] == "infer" else "fwd+bwd"
+    return {"value": round(dense, 1), "unit": "towers/s", "cores": threads, "kind": "port",
+            "sample": f"oracle.forward_dense fp32 {what} ({dsamp}), N={cfg['nodes']}, S={cfg['S']}, "
+                      f"{cfg['relations']} relations, torch CPU threads={threads}; gather form "
+                      f"{gather:.1f} towers/s ({gsamp}); dense at 1 thread {one:.1f} towers/s ({osamp})",
+            "value_gather": round(gather, 1), "value_1thread": round(one, 1)}
 
 
-PMC_WORKLOAD = (65536, 6, 5)   # (towers per GPU, nodes, MP steps) of profiles/pmc_summary.json
+# ------------------------------------------------------------------------------ PMC traffic
+def pmc_path(config: int) -> str:
+    return os.path.join(ROOT, "profiles", "pmc_summary.json" if config == 0 else f"pmc_summary_config{config}.json")
 
 
-def load_pmc(kernel: str, math: str = "x6"):
-    """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) from the committed PMC
-    summary, or None when absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    name = PMC_NAMES.get(math, {}).get(kernel)
-    if name is None or not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            d = json.load(f).get(name, {})
-        if "hbm_read_bytes" not in d or "hbm_write_bytes" not in d:
-            return None
-        return float(d["hbm_read_bytes"] + d["hbm_write_bytes"])
-    except Exception:
-        return None
-
-
-def step_hbm(ms_per_step: float):
-    """Whole-step HBM bytes from the committed PMC summary (one entry per kernel: mean bytes per
-    dispatch × dispatches; the summary's run covers as many steps as k_adam dispatches)."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def load_pmc(config: int, kernel: str, math: str, workload: str):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, averaged over
+    the launches of every variant of that kernel) from the committed rocprofv3 summary of this
+    config, or None when absent or collected on another workload."""
+    path = pmc_path(config)
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        steps = d.get("k_adam", {}).get("dispatches", 0)
-        if not steps:
+        meta = d.get("_workload", {})
+        if meta and (meta.get("workload") != workload or meta.get("math") != math):
             return None
-        tot = sum(v.get("hbm_read_bytes", 0.0) * v["dispatches"] + v.get("hbm_write_bytes", 0.0) * v["dispatches"]
-                  for v in d.values() if "dispatches" in v)
-        per = tot / steps
-        gbs = per / (ms_per_step * 1e-3) / 1e9
-        return {"bytes_per_step": round(per), "achieved_gbs": round(gbs, 1), "peak_gbs": PEAK_HBM_GBS,
-                "frac": round(gbs / PEAK_HBM_GBS, 4),
-                "source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per kernel)"}
+        tot = cnt = 0.0
+        for name, v in d.items():
+            if name.startswith(PMC_PREFIX[kernel]) and "hbm_read_bytes" in v and "hbm_write_bytes" in v:
+                tot += (v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["dispatches"]
+                cnt += v["dispatches"]
+        return tot / cnt if cnt else None
     except Exception:
         return None
 
 
+def step_hbm(config: int, ms_per_step: float, math: str, workload: str):
+    """Whole-step HBM bytes from the committed PMC summary of this config (mean bytes per dispatch ×
+    dispatches, over the steps of that profiling run), divided by THIS run's step time."""
+    path = pmc_path(config)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        meta = d.get("_workload", {})
+        if meta and (meta.get("workload") != workload or meta.get("math") != math):
+            return None
+        # one Adam per training step; one weight prep per forward (inference replays)
+        steps = meta.get("steps") or d.get("k_adam", {}).get("dispatches", 0) or \
+            d.get("k_prep_weights", {}).get("dispatches", 0)
+        if not steps:
+            return None
+        tot = sum(v.get("hbm_read_bytes", 0.0) * v["dispatches"] + v.get("hbm_write_bytes", 0.0) * v["dispatches"]
+                  for v in d.values() if isinstance(v, dict) and "dispatches" in v)
+        per = tot / steps
+        gbs = per / (ms_per_step * 1e-3) / 1e9
+        return {"bytes_per_step": round(per), "achieved_gbs": round(gbs, 1), "peak_gbs": PEAK_HBM_GBS,
+                "frac": round(gbs / PEAK_HBM_GBS, 4),
+                "source": f"{os.path.relpath(path, ROOT)}: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per kernel from a "
+                          "separate profiling run of this workload, divided by this run's step time"}
+    except Exception:
+        return None
+
+
+def roofline(kernel: str, kern_ms, Ne, Nn, S, math, config, workload):
+    """The timed kernel's roofline: algorithmic FLOPs per launch ÷ its mean HIP-event launch time,
+    against the matrix peak of the math it runs in; every timed kernel is fused GEMM work far above
+    the ridge point, so the bound is the matrix pipe. `traffic` = measured HBM bytes per
+    launch from the committed PMC summary of the same workload (null if none)."""
+    avg_ms = float(np.mean(kern_ms))
+    kflops = KERNELS[kernel][1](Ne, Nn, S)
+    achieved = kflops / (avg_ms * 1e-3) / 1e12
+    mpeak = MATH_PEAK[math]
+    traffic = load_pmc(config, kernel, math, workload)
+    h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(mpeak, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / mpeak, 4), "traffic": traffic, "kernel": kernel,
+            "avg_launch_ms": round(avg_ms, 4), "launches": len(kern_ms), "flop_per_launch": kflops,
+            "hbm_gbs": round(h_gbs, 1) if h_gbs else None,
+            "hbm_frac": round(h_gbs / PEAK_HBM_GBS, 4) if h_gbs else None, "peak_note": PEAK_NOTE[math]}
+
+
+# ------------------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--towers", type=int, default=65536, help="towers per GPU")
-    ap.add_argument("--nodes", type=int, default=6)
-    ap.add_argument("--mp-steps", type=int, default=5)
+    ap.add_argument("--config", type=int, default=0, choices=sorted(CONFIGS),
+                    help="BASELINE.json config (1-5); 0 = the headline metric's configuration")
+    ap.add_argument("--towers", type=int, default=None, help="towers per GPU (overrides the config)")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--mp-steps", type=int, default=None)
+    ap.add_argument("--math", default=None, choices=["x6", "f32", "bf16"],
+                    help="matrix-product arithmetic (spwgnn.h SPWGNN_MATH_*), overrides the config")
     ap.add_argument("--dropout", type=float, default=0.1)
-    ap.add_argument("--roofline-kernel", default="edge_bwd", choices=sorted(KERNELS))
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--roofline-kernel", default=None, choices=sorted(KERNELS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-f32-leg", action="store_true", help="skip the f32-math reference measurement")
-    ap.add_argument("--math", default="x6", choices=["x6", "f32", "bf16"],
-                    help="matrix-product arithmetic (spwgnn.h SPWGNN_MATH_*)")
-    ap.add_argument("--infer", action="store_true",
-                    help="BASELINE config 5: forward-only inference replayed from a hipGraph "
-                         "(defaults: 32-block towers, S=10, 8192 towers/GPU)")
+    ap.add_argument("--no-f32-leg", action="store_true", help="skip the other-math reference measurements")
+    ap.add_argument("--infer", action="store_true", help="alias of --config 5")
     args = ap.parse_args()
+    if args.infer:
+        args.config = 5
+    cfg = dict(CONFIGS[args.config])
+    for k, a in (("towers", args.towers), ("nodes", args.nodes), ("S", args.mp_steps), ("math", args.math)):
+        if a is not None:
+            cfg[k] = a
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -207,39 +351,43 @@ def main():
         else:
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
+    if cfg["mode"] == "infer":
+        return run_infer(args, cfg, world, rank, device)
+    return run_train(args, cfg, world, rank, device)
 
-    if args.infer:
-        return run_infer(args, world, rank, device)
-    B, N, S = args.towers, args.nodes, args.mp_steps
-    raw = D.synthetic_towers(B, N, seed=1000 + rank)
-    objects = (raw / D.RELATION_THRESHOLD).astype(np.float32)
-    batch = TowerBatch.fully_connected(objects, device=device)
-    rng = np.random.default_rng(rank)
-    target = torch.tensor(rng.integers(0, 2, size=B * N).astype(np.float32), device=device)
+
+def run_train(args, cfg, world, rank, device):
+    S, math = cfg["S"], cfg["math"]
+    batches, targets = make_workload(cfg, rank, device)
     params = P.to_flat(P.glorot_uniform(0), device=device)
     if world > 1:
         dist.broadcast(params, 0)
-    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=args.math)
-
+    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math)
+    step_in = (batches[0], targets[0]) if len(batches) == 1 else (batches, targets)
     for _ in range(args.warmup):
-        trainer.step(batch, target)
+        trainer.step(*step_in)
     torch.cuda.synchronize()
 
-    kid, flops_fn = KERNELS[args.roofline_kernel]
-    per = LAUNCHES_PER_STEP[args.roofline_kernel]
-    nl = (S if per == "S" else per) * args.steps
+    kname = args.roofline_kernel or "edge_bwd"
+    kid = KERNELS[kname][0]
+    per = LAUNCHES_PER_STEP[kname]
+    per_step = (S if per == "S" else per) * len(batches)
+    nl = per_step * args.steps
     ev = HipEvents(2 * nl)
     trainer.prof_kernel = kid
-    trainer.prof_events = ev.ev
-    # the library fills events in launch order; re-offset the array every step
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    per_step = nl // args.steps
     for k in range(args.steps):
-        trainer.prof_events = ev.ev[2 * per_step * k: 2 * per_step * (k + 1)]
-        out3 = trainer.step(batch, target)
+        # the library fills events in launch order: one slice of the array per micro-batch launch set
+        evs = ev.ev[2 * per_step * k: 2 * per_step * (k + 1)]
+        if len(batches) == 1:
+            trainer.prof_events = evs
+            out3 = trainer.step(*step_in)
+        else:
+            trainer.prof_events = None
+            out3 = _micro_step(trainer, batches, targets, evs, per_step // len(batches))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -250,39 +398,19 @@ def main():
     el = float(el_t.item())
     kern_ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(nl)]
     ev.close()
-    loss = float(out3[0].item())
+    o3 = out3 if not isinstance(out3, list) else out3[0]
+    loss = float(o3[0].item())
 
-    Ne, Nn = batch.n_edges, batch.n_nodes
-    avg_ms = float(np.mean(kern_ms))
-    kflops = flops_fn(Ne, Nn, S)
-    achieved = kflops / (avg_ms * 1e-3) / 1e12
-    value = world * B * args.steps / el
-    total_flops = step_flops(Ne, Nn, S)
-    # roofline of the timed kernel: its algorithmic fp32 FLOPs against the matrix peak of the math
-    # it runs in (x6: bf16 peak / 6); its PMC HBM bytes per launch are reported as `traffic`
-    mpeak = {"x6": PEAK_X6_TFLOPS, "f32": PEAK_FP32_TFLOPS, "bf16": PEAK_BF16_TFLOPS}[args.math]
-    # the committed PMC summary was collected at the default workload (tools/round_artifacts.sh):
-    # its bytes are only quoted for that shape
-    pmc_shape = (B, N, S) == PMC_WORKLOAD
-    traffic = load_pmc(args.roofline_kernel, args.math) if pmc_shape else None
-    m_frac = achieved / mpeak
-    h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
-    h_frac = h_gbs / PEAK_HBM_GBS if h_gbs else None
-    # every timed kernel is fused GEMM work far above the ridge point (≫ 100 algorithmic
-    # FLOP per compulsory HBM byte), so its roofline is the matrix pipe: achieved = algorithmic FLOPs
-    # per launch ÷ mean launch time. The PMC bytes are the measured traffic beside it (hbm_gbs is
-    # that traffic's rate, not an algorithmic figure).
-    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(mpeak, 1), "unit": "TFLOP/s",
-            "frac": round(m_frac, 4)}
-    roof.update({"kernel": args.roofline_kernel, "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
-                 "launches": nl, "flop_per_launch": kflops, "mfma_tflops": round(achieved, 2),
-                 "mfma_peak": round(mpeak, 1), "mfma_frac": round(m_frac, 4),
-                 "hbm_gbs": round(h_gbs, 1) if h_gbs else None, "hbm_frac": round(h_frac, 4) if h_frac else None,
-                 "peak_note": {"x6": "x6: fp32 products as 6 bf16 MFMA products, peak = 2.5 PF bf16 / 6",
-                               "f32": "f32 MFMA peak", "bf16": "bf16 MFMA dense peak"}[args.math]})
+    Ne = sum(b.n_edges for b in batches)
+    Nn = sum(b.n_nodes for b in batches)
+    B = sum(b.n_towers for b in batches)
+    wl = workload_name(cfg, world, args.dropout)
+    # kernel FLOPs per launch: one launch covers one micro-batch
+    roof = roofline(kname, kern_ms, Ne / len(batches), Nn / len(batches), S, math, args.config, wl)
+    metric = METRIC if args.config == 0 else f"towers/sec fwd+bwd, BASELINE config {args.config}"
     out = {
-        "metric": METRIC,
-        "value": round(value, 1),
+        "metric": metric,
+        "value": round(world * B * args.steps / el, 1),
         "unit": "towers/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -291,61 +419,74 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if args.math == "bf16" else "f32",
-        "math": {"x6": "x6: each fp32 matrix product as 6 bf16 MFMA products of 3-way split operands, fp32 "
-                       "accumulation (DESIGN.md §3b)", "f32": "f32 MFMA",
-                 "bf16": "bf16: operands rounded to bf16, one bf16 MFMA product, fp32 accumulation"}[args.math],
+        "dtype": "bf16" if math == "bf16" else "f32",
+        "math": MATH_DESC[math],
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
-        "config": {"workload": f"train step fwd+BCE+bwd+{'allreduce+' if world > 1 else ''}Adam, "
-                               f"{N}-block towers fully connected (E={N*(N-1)}), {B} towers/GPU, "
-                               f"{S} MP steps, dropout {args.dropout}",
-                   "towers_per_gpu": B, "global_batch": B * world, "nodes_per_tower": N, "mp_steps": S,
+        "config": {"workload": wl, "baseline_config": args.config, "towers_per_gpu": B, "global_batch": B * world,
+                   "nodes_per_tower": list(cfg["nodes"]) if isinstance(cfg["nodes"], tuple) else cfg["nodes"],
+                   "nodes_per_gpu": Nn, "edges_per_gpu": Ne, "mp_steps": S, "math": math,
                    "parallelism": f"dp{world}"},
-        "step_tflops": round(total_flops * world * args.steps / el / 1e12, 2),
+        "step_tflops": round(step_flops(Ne, Nn, S) * world * args.steps / el / 1e12, 2),
         "loss": round(loss, 5),
         "roofline": roof,
         "cpu_baseline": None,
     }
-    if world == 1 and args.math == "x6" and not args.no_f32_leg:
+    if world == 1 and args.config == 0 and math == "x6" and not args.no_f32_leg:
         # the same step in the other SPWGNN_MATH_* modes, for reference: f32 MFMA (fp32-class like
         # x6) and bf16 (operands rounded to bf16, one product — BASELINE configs 3-4's arithmetic)
         for m in ("f32", "bf16"):
             trm = Trainer(params.clone(), mp_steps=S, dropout=args.dropout, seed=7, math=m)
             for _ in range(2):
-                trm.step(batch, target)
+                trm.step(*step_in)
             torch.cuda.synchronize()
             km = max(3, args.steps // 2)
             t1 = time.perf_counter()
             for _ in range(km):
-                trm.step(batch, target)
+                trm.step(*step_in)
             torch.cuda.synchronize()
             em = time.perf_counter() - t1
             out[f"{m}_math"] = {"value": round(B * km / em, 1), "ms_per_step": round(em / km * 1e3, 3), "steps": km}
             del trm
             torch.cuda.empty_cache()
-    out["hbm"] = step_hbm(out["ms_per_step"]) if pmc_shape else None
+    out["hbm"] = step_hbm(args.config, out["ms_per_step"], math, wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_pair(N, S, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
+def _micro_step(trainer, batches, targets, evs, per_mb):
+    """Trainer.step over micro-batches with the timed kernel's events handed to each micro-batch's
+    launches (the library records at most prof_count pairs per call)."""
+    orig = trainer.run_config
+
+    def rc(micro=0):
+        r = orig(micro)
+        r.prof_kernel = trainer_kid[0]
+        r.prof_events = evs[2 * per_mb * micro: 2 * per_mb * (micro + 1)]
+        return r
+    trainer_kid = [trainer.prof_kernel]
+    trainer.run_config = rc
+    try:
+        return trainer.step(batches, targets)
+    finally:
+        trainer.run_config = orig
+
+
 INFER_METRIC = "towers/sec fwd (inference), 32-block towers, 10 MP steps, hipGraph-captured forward"
 
 
-def run_infer(args, world, rank, device):
+def run_infer(args, cfg, world, rank, device):
     """Config 5: the forward of a whole batch captured once into a hipGraph (torch.cuda.CUDAGraph
     over the library's launches on the capture stream) and replayed; weak scaling, replicas."""
     from spwgnn_amd import engine as E
-    B = args.towers if args.towers != 65536 else 8192
-    N = args.nodes if args.nodes != 6 else 32
-    S = args.mp_steps if args.mp_steps != 5 else 10
+    B, N, S, math = cfg["towers"], cfg["nodes"], cfg["S"], cfg["math"]
     raw = D.synthetic_towers(B, N, seed=5000 + rank)
     batch = TowerBatch.fully_connected((raw / D.RELATION_THRESHOLD).astype(np.float32), device=device)
     params = P.to_flat(P.glorot_uniform(0), device=device)
-    run = E.RunConfig(S, training=False)
+    run = E.RunConfig(S, training=False, math=math)
     ws = E.Workspace(device)
     z = torch.empty(batch.n_nodes, dtype=torch.float32, device=device)
     side = torch.cuda.Stream(device)
@@ -359,14 +500,18 @@ def run_infer(args, world, rank, device):
     for _ in range(args.warmup):
         graph.replay()
     torch.cuda.synchronize()
-    # dominant kernel timed with HIP events on an un-captured pass (same stream, same launches)
-    kid, flops_fn = _lib.K_EDGE_FWD, KERNELS["edge_fwd"][1]
-    ev = HipEvents(2 * S)
-    prun = E.RunConfig(S, training=False, prof_kernel=kid, prof_events=ev.ev)
-    E.forward(params, batch, prun, ws, logits=z)
-    torch.cuda.synchronize()
-    kern_ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(S)]
-    ev.close()
+    # dominant kernel timed with HIP events on un-captured passes (same stream, same launches)
+    kname = args.roofline_kernel or "edge_fwd"
+    kid = KERNELS[kname][0]
+    per = S if LAUNCHES_PER_STEP[kname] == "S" else 1
+    kern_ms = []
+    for _ in range(3):
+        ev = HipEvents(2 * per)
+        prun = E.RunConfig(S, training=False, math=math, prof_kernel=kid, prof_events=ev.ev)
+        E.forward(params, batch, prun, ws, logits=z)
+        torch.cuda.synchronize()
+        kern_ms += [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(per)]
+        ev.close()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -382,27 +527,22 @@ def run_infer(args, world, rank, device):
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
     Ne, Nn = batch.n_edges, batch.n_nodes
-    avg_ms = float(np.mean(kern_ms))
-    kflops = flops_fn(Ne, Nn, S)
-    achieved = kflops / (avg_ms * 1e-3) / 1e12
-    # forward FLOPs as the kernels compute them (rmp layer 3 behind the receiver sum)
-    fwd_flops = 2.0 * (Ne * (2 * 150 + 4 * 150 * 150) + Nn * (2 * 100 + 100 * 100)
-                       + S * (Ne * 150 * 150 + Nn * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150))
-                       - Nn * 2 * 100 * 150)
+    wl = workload_name(cfg, world, 0.0)
     out = {
         "metric": INFER_METRIC, "value": round(world * B * args.steps / el, 1), "unit": "towers/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (Jenga-geometry towers, glorot weights)",
-        "config": {"workload": f"forward, {N}-block towers fully connected (E={N * (N - 1)}), {B} towers/GPU, "
-                               f"{S} MP steps, hipGraph replay", "towers_per_gpu": B, "global_batch": B * world,
-                   "nodes_per_tower": N, "mp_steps": S, "parallelism": f"replicas{world}"},
-        "step_tflops": round(fwd_flops * world * args.steps / el / 1e12, 2),
-        "roofline": {"kernel": "edge_fwd", "bound": "mfma", "achieved": round(achieved, 2),
-                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                     "avg_launch_ms": round(avg_ms, 4), "launches": S, "flop_per_launch": kflops, "traffic": None},
+        "vs_baseline": None, "dtype": "bf16" if math == "bf16" else "f32", "math": MATH_DESC[math],
+        "data": "synthetic (Jenga-geometry towers, glorot weights)",
+        "config": {"workload": wl, "baseline_config": 5, "towers_per_gpu": B, "global_batch": B * world,
+                   "nodes_per_tower": N, "mp_steps": S, "math": math, "parallelism": f"replicas{world}"},
+        "step_tflops": round(fwd_flops(Ne, Nn, S) * world * args.steps / el / 1e12, 2),
+        "roofline": roofline(kname, kern_ms, Ne, Nn, S, math, 5, wl),
         "cpu_baseline": None,
     }
+    out["hbm"] = step_hbm(5, out["ms_per_step"], math, wl)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -122,7 +122,7 @@ def forward_dense(p, objects, Rs, Rr, prop, mp_steps: int = REF_MP_STEPS,
     senders = torch.bmm(Rs_t, objects)              # Networks.py:32
     receivers = torch.bmm(Rr_t, objects)            # Networks.py:33
     diff = receivers[..., 0:2] - senders[..., 0:2]  # Networks.py:58-62
-    obj_vec = torch.cat([objects[..., 1:2], objects[..., 2:3]], dim=-1)  # :155-161
+    obj_vec = torch.cat([objects[..., 1:2], objects[..., 2:3]], dim=-1)  # Networks.py:65-71
     c_r = torch.relu(_mlp(diff, p, "rm"))           # Networks.py:75
     c_o = torch.relu(_mlp(obj_vec, p, "om"))        # Networks.py:76
     if drop_r is not None:                          # Networks.py:77-78
@@ -133,14 +133,14 @@ def forward_dense(p, objects, Rs, Rr, prop, mp_steps: int = REF_MP_STEPS,
     states = [P]
     x = None
     for _ in range(mp_steps):                       # Networks.py:83
-        ps = torch.bmm(Rs_t, P)                     # :174
-        pr = torch.bmm(Rr_t, P)                     # :175
-        x = _mlp(torch.cat([c_r, ps, pr], dim=-1), p, "rmp")       # :176-177
-        eff = torch.tanh(torch.bmm(Rr, x))          # :178
-        x = _mlp(torch.cat([c_o, eff, P], dim=-1), p, "omp")       # :179-180
-        P = torch.tanh(x[..., 1:] + P)              # :181 (prop_layer = x[:,:,1:], :170)
+        ps = torch.bmm(Rs_t, P)                     # Networks.py:84
+        pr = torch.bmm(Rr_t, P)                     # Networks.py:85
+        x = _mlp(torch.cat([c_r, ps, pr], dim=-1), p, "rmp")       # Networks.py:86-87
+        eff = torch.tanh(torch.bmm(Rr, x))          # Networks.py:88
+        x = _mlp(torch.cat([c_o, eff, P], dim=-1), p, "omp")       # Networks.py:89-90
+        P = torch.tanh(x[..., 1:] + P)              # Networks.py:91 (prop_layer = x[:,:,1:], :80)
         states.append(P)
-    logits = x[..., 0]                              # :184 sigmoid(x[:,:,:1]) -> logit
+    logits = x[..., 0]                              # Networks.py:94 sigmoid(x[:,:,:1]) -> logit
     if return_state:
         return logits, states
     return logits

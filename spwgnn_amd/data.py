@@ -49,10 +49,10 @@ def jenga_tower(n: int, rng: random.Random) -> np.ndarray:
             boxes[layer].append((float(x), BOTTOM_EDGE + int(RECT_HEIGHT / 2) + RECT_HEIGHT * layer, float(w)))
             n -= 1
             continue
-        left_edge -= (layer > 0) * int(RECT_WIDTH_AVERAGE / 2)   # :172
+        left_edge -= (layer > 0) * int(RECT_WIDTH_AVERAGE / 2)   # JengaBuilder.py:171
         w = rng.randint(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE)
         left_edge += w
-        while left_edge - w / 2 < right_edge and n > 0:          # :175-185
+        while left_edge - w / 2 < right_edge and n > 0:          # JengaBuilder.py:174-184
             boxes[layer].append((left_edge - w / 2, y, float(w)))
             n -= 1
             left_edge += rng.randint(0, MAX_SPACE_RECTS)
@@ -139,3 +139,53 @@ def synthetic_batch(n_towers: int, n_objects: int, seed: int = 0, fully_connecte
     objects = (raw / RELATION_THRESHOLD).astype(np.float32)
     prop = np.zeros((n_towers, n_objects, 100), np.float32)
     return objects, Rs, Rr, prop, target
+
+
+def ragged_batch(n_towers: int, n_min: int, n_max: int, seed: int = 0,
+                 threshold: Optional[float] = RELATION_THRESHOLD):
+    """BASELINE config 4's input: towers of U{n_min..n_max} Jenga boxes in random order, relations
+    from the raw positions (distance < threshold, main.py:71-81; None = fully connected), objects /170.
+
+    Returns the compact edge form `TowerBatch.from_edges` takes: (pos (Nn, 3) f32, tower_nodes (T,),
+    src (Ne,), dst (Ne,), tower_edges (T,), raw (list of (N_t, 3) pixel arrays)). Edges are tower-major
+    and sender-major inside a tower (the slot order of main.py:72-81). Vectorised per tower size."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(n_min, n_max + 1, size=n_towers).astype(np.int32)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    pos = np.zeros((int(off[-1]), 3), np.float32)
+    raw_list = [None] * n_towers
+    e_tower, e_src, e_dst = [], [], []
+    for n in range(n_min, n_max + 1):
+        idx = np.nonzero(sizes == n)[0]
+        if len(idx) == 0:
+            continue
+        raw = synthetic_towers(len(idx), n, seed=seed * 1000 + n)
+        rows = off[idx][:, None] + np.arange(n)[None, :]
+        pos[rows.reshape(-1)] = (raw / RELATION_THRESHOLD).reshape(-1, 3)
+        for j, t in enumerate(idx):
+            raw_list[t] = raw[j]
+        m_idx, j_idx = np.nonzero(~np.eye(n, dtype=bool))
+        if threshold is None:
+            keep = np.ones((len(idx), len(m_idx)), bool)
+        else:
+            keep = np.linalg.norm(raw[:, m_idx, 0:2] - raw[:, j_idx, 0:2], axis=2) < threshold
+        tt, kk = np.nonzero(keep)
+        e_tower.append(idx[tt])
+        e_src.append(off[idx[tt]] + m_idx[kk])
+        e_dst.append(off[idx[tt]] + j_idx[kk])
+    et = np.concatenate(e_tower) if e_tower else np.zeros(0, np.int64)
+    order = np.argsort(et, kind="stable")      # tower-major, slot order kept inside a tower
+    src = np.concatenate(e_src)[order].astype(np.int32) if e_src else np.zeros(0, np.int32)
+    dst = np.concatenate(e_dst)[order].astype(np.int32) if e_dst else np.zeros(0, np.int32)
+    tower_edges = np.bincount(et, minlength=n_towers).astype(np.int32)
+    return pos, sizes, src, dst, tower_edges, raw_list
+
+
+def edge_slice(pos, tower_nodes, src, dst, tower_edges, a: int, b: int):
+    """Towers [a, b) of a compact edge-form batch (as `ragged_batch` returns), node ids rebased to 0:
+    a micro-batch or a rank's shard of it."""
+    off = np.concatenate([[0], np.cumsum(tower_nodes)]).astype(np.int64)
+    eoff = np.concatenate([[0], np.cumsum(tower_edges)]).astype(np.int64)
+    n0, n1, e0, e1 = off[a], off[b], eoff[a], eoff[b]
+    return (pos[n0:n1], tower_nodes[a:b], (src[e0:e1] - n0).astype(np.int32), (dst[e0:e1] - n0).astype(np.int32),
+            tower_edges[a:b])

@@ -134,3 +134,160 @@ def test_config5_full_size_inference_hipgraph():
     pick = np.sort(np.random.default_rng(3).choice(B, 4, replace=False))
     ok, err = _close(got[pick], _oracle_logits(params, raw[pick], S))
     assert ok, err
+
+
+# ---------------------------------------------------------------------------------------------
+# Config 2 (N = 6, B = 4,096, S = 3, fp32 training) and configs 3–4 in bf16 arithmetic
+# (BASELINE.json names bf16 for them; SPWGNN_MATH_BF16 = operands rounded to bf16, one MFMA product,
+# fp32 accumulation). bf16 tolerances as test_gpu_parity.test_bf16_math_forward_backward:
+# logits |Δ| ≤ 0.05, each gradient tensor's cosine with the fp64 oracle's ≥ 0.99.
+# ---------------------------------------------------------------------------------------------
+BF16_LOGIT_ATOL = 0.05
+BF16_COS = 0.99
+
+
+def _cos(a, b):
+    return float((a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
+
+
+def _train_grads(flat, batch, tgt, S, math, dropout=0.0):
+    ws = E.Workspace("cuda")
+    run = E.RunConfig(S, training=True, math=math, dropout=dropout)
+    z = E.forward(flat, batch, run, ws)
+    out3, dz = E.bce(z, torch.as_tensor(np.ascontiguousarray(tgt), device="cuda").reshape(-1), E.BceScratch("cuda"))
+    g, _ = E.backward(flat, batch, run, ws, dz)
+    torch.cuda.synchronize()
+    res = (z.cpu().numpy(), float(out3[0]), P.from_flat(g))
+    del ws, z, dz, g
+    torch.cuda.empty_cache()
+    return res
+
+
+class _Capture:
+    """The HIP engine, keeping a host copy of the (accumulated) gradient the Adam step receives."""
+
+    def __init__(self):
+        from spwgnn_amd.trainer import HipEngine
+        self.e = HipEngine("cuda")
+        self.g = None
+
+    def __getattr__(self, k):
+        return getattr(self.e, k)
+
+    def adam(self, params, grads, *a):
+        self.g = grads.detach().cpu().double().numpy()
+        self.e.adam(params, grads, *a)
+
+
+@pytest.mark.parametrize("math", ["x6", "f32"])
+def test_config2_training_parity_small(math):
+    """Config 2's shape (6-block towers, thresholded training relations, S = 3): forward, loss and
+    every weight gradient of a 16-tower batch equal the fp64 oracle (fp32 tolerance)."""
+    params = O.random_params(41)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(16, 6, seed=21, fully_connected=False)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    z, loss, g = _train_grads(P.to_flat(params, device="cuda"), batch, tgt, 3, math)
+    loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, 3)
+    ok, err = _close(z.reshape(z_ref.shape), z_ref)
+    assert ok, err
+    assert abs(loss - loss_ref) < 1e-5
+    for k, r in g_ref.items():
+        assert np.abs(g[k] - r).max() <= 1e-5 * np.abs(r).max() + 1e-7, k
+
+
+def test_config2_full_batch_training():
+    """Config 2 at its full size (4,096 six-block towers, thresholded relations, S = 3) through the
+    Trainer (fwd → BCE → bwd → Adam): sampled towers' logits equal the oracle; the batch gradient equals
+    the node-weighted sum of its two halves' gradients; the Adam step moves the parameters by the
+    Keras-Adam update of that gradient."""
+    from spwgnn_amd.trainer import Trainer
+    B, N, S = 4096, 6, 3
+    params = O.random_params(42)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, N, seed=22, fully_connected=False)
+    flat = P.to_flat(params, device="cuda")
+    full = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    z, _, g = _train_grads(flat, full, tgt, S, "x6")
+    pick = np.sort(np.random.default_rng(4).choice(B, 16, replace=False))
+    z_ref = O.forward_dense(O.to_torch(params), *(torch.tensor(a[pick], dtype=torch.float64) for a in (obj, Rs, Rr, prop)),
+                            S).numpy()
+    ok, err = _close(z.reshape(B, N)[pick], z_ref)
+    assert ok, err
+    halves = [slice(0, B // 2), slice(B // 2, B)]
+    hg = [_train_grads(flat, TowerBatch.from_dense(obj[h], Rs[h], Rr[h], prop[h], device="cuda"), tgt[h], S, "x6")[2]
+          for h in halves]
+    for k in g:
+        comb = (hg[0][k] + hg[1][k]) / 2
+        assert np.abs(comb - g[k]).max() <= 1e-5 * np.abs(g[k]).max() + 1e-9, k
+    cap = _Capture()
+    tr = Trainer(flat.clone(), engine=cap, mp_steps=S, dropout=0.0, math="x6")
+    tr.step(full, torch.as_tensor(tgt, device="cuda").reshape(-1))
+    torch.cuda.synchronize()
+    assert np.array_equal(cap.g, P.to_flat(g, device="cpu").double().numpy())   # deterministic
+    want = O.KerasAdam(lr=5e-4, beta1=0.9, beta2=0.999, eps=1e-7).step(flat.cpu().double().numpy(), cap.g)
+    assert np.abs(tr.params.cpu().double().numpy() - want).max() < 1e-7
+
+
+def test_config3_bf16_full_size():
+    """Config 3 in its BASELINE arithmetic (bf16): 65,536 fully connected 12-block towers, S = 5,
+    training forward + backward at full size. Sampled towers' logits are within the bf16 tolerance of
+    the fp64 oracle; the full-batch gradients equal the mean of its two halves' gradients (linearity
+    of the node-mean BCE; fp32 accumulation, 1e-4 of each tensor's max); the gradients of a sampled
+    16-tower sub-batch have cosine ≥ 0.99 with the oracle's."""
+    B, N, S = 65536, 12, 5
+    params = O.random_params(43)
+    raw = D.synthetic_towers(B, N, seed=13)
+    obj = (raw / D.RELATION_THRESHOLD).astype(np.float32)
+    tgt = np.random.default_rng(6).integers(0, 2, size=(B, N)).astype(np.float32)
+    flat = P.to_flat(params, device="cuda")
+    z, _, g = _train_grads(flat, TowerBatch.fully_connected(obj, device="cuda"), tgt, S, "bf16")
+    z = z.reshape(B, N)
+    pick = np.sort(np.random.default_rng(8).choice(B, 16, replace=False))
+    z_ref = _oracle_logits(params, raw[pick], S)
+    assert np.abs(z[pick] - z_ref).max() <= BF16_LOGIT_ATOL, np.abs(z[pick] - z_ref).max()
+    hg = [_train_grads(flat, TowerBatch.fully_connected(obj[h], device="cuda"), tgt[h], S, "bf16")[2]
+          for h in (slice(0, B // 2), slice(B // 2, B))]
+    for k in g:
+        comb = (hg[0][k] + hg[1][k]) / 2
+        assert np.abs(comb - g[k]).max() <= 1e-4 * np.abs(g[k]).max() + 1e-9, k
+    # the sampled sub-batch's gradients vs the oracle (bf16 tolerance)
+    Rs, Rr = O.relation_matrices(raw[pick], None)
+    _, _, gs = _train_grads(flat, TowerBatch.fully_connected(obj[pick], device="cuda"), tgt[pick], S, "bf16")
+    _, _, g_ref = O.loss_and_grads(params, obj[pick], Rs, Rr, np.zeros((len(pick), N, 100), np.float32), tgt[pick], S)
+    for k in g_ref:
+        assert _cos(gs[k], g_ref[k]) >= BF16_COS, (k, _cos(gs[k], g_ref[k]))
+
+
+def test_config4_bf16_shard_training():
+    """Config 4's per-GPU shard in bf16: 131,072 ragged 4–16-block towers trained as the shard plan
+    prescribes (two micro-batches of 65,536 whose node-weighted gradients the Trainer accumulates before
+    its one Adam update). Checks: sampled towers' logits within the bf16 tolerance of the oracle;
+    the accumulated micro-batch gradient equals the single-batch gradient of the whole shard (linearity
+    of the node-mean BCE); the Trainer's update is Keras Adam on that gradient."""
+    from spwgnn_amd import shard
+    from spwgnn_amd.trainer import Trainer
+    B, S = 131072, 5
+    params = O.random_params(44)
+    pos, sizes, src, dst, te, raws = D.ragged_batch(B, 4, 16, seed=9)
+    tgt = np.random.default_rng(10).integers(0, 2, size=int(sizes.sum())).astype(np.float32)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    flat = P.to_flat(params, device="cuda")
+    whole = TowerBatch.from_edges(pos, sizes, src, dst, te, device="cuda")
+    z, _, g = _train_grads(flat, whole, tgt, S, "bf16")
+    del whole
+    torch.cuda.empty_cache()
+    for t in np.sort(np.random.default_rng(11).choice(B, 12, replace=False)):
+        ref = _oracle_logits(params, raws[t][None], S, D.RELATION_THRESHOLD)[0]
+        assert np.abs(z[off[t]:off[t + 1]] - ref).max() <= BF16_LOGIT_ATOL, int(t)
+    mbs = shard.micro_batches(0, B, 65536)
+    assert len(mbs) == 2
+    batches = [TowerBatch.from_edges(*D.edge_slice(pos, sizes, src, dst, te, a, b), device="cuda") for a, b in mbs]
+    tgts = [torch.as_tensor(tgt[off[a]:off[b]], device="cuda") for a, b in mbs]
+
+    cap = _Capture()
+    tr = Trainer(flat.clone(), engine=cap, mp_steps=S, dropout=0.0, math="bf16")
+    tr.step(batches, tgts, n_global=int(sizes.sum()))
+    torch.cuda.synchronize()
+    gw = P.to_flat(g, device="cpu").double().numpy()
+    assert np.abs(cap.g - gw).max() <= 1e-4 * np.abs(gw).max(), np.abs(cap.g - gw).max()
+    want = O.KerasAdam(lr=5e-4, beta1=0.9, beta2=0.999, eps=1e-7).step(flat.cpu().double().numpy(), cap.g)
+    assert np.abs(tr.params.cpu().double().numpy() - want).max() < 1e-7

@@ -225,3 +225,22 @@ def test_keras_validation_split_matches_keras2(B, v):
     assert keras_split_at(B, v) == (int(int(B) * (1.0 - v)) if v else B)
     if (B, v) == (7, 0.2):
         assert keras_split_at(B, v) == 5
+
+
+def test_ragged_batch_matches_per_tower_relations():
+    """data.ragged_batch (config 4's vectorised builder) equals the per-tower loop of main.py:71-81 on
+    every tower: same thresholded sender-major edges, positions /170; edge_slice rebases a sub-range."""
+    pos, sz, s, d, te, raw = D.ragged_batch(300, 4, 16, seed=5)
+    assert sz.min() >= 4 and sz.max() <= 16 and len(raw) == 300
+    off = np.concatenate([[0], np.cumsum(sz)])
+    eo = np.concatenate([[0], np.cumsum(te)])
+    for t in range(300):
+        n, r = sz[t], raw[t]
+        m, j = np.nonzero(~np.eye(n, dtype=bool))
+        k = np.linalg.norm(r[m, :2] - r[j, :2], axis=1) < D.RELATION_THRESHOLD
+        assert np.array_equal(s[eo[t]:eo[t + 1]], off[t] + m[k])
+        assert np.array_equal(d[eo[t]:eo[t + 1]], off[t] + j[k])
+        assert np.array_equal(pos[off[t]:off[t + 1]], (r / D.RELATION_THRESHOLD).astype(np.float32))
+    p2, n2, s2, d2, e2 = D.edge_slice(pos, sz, s, d, te, 100, 200)
+    assert np.array_equal(s2 + off[100], s[eo[100]:eo[200]]) and np.array_equal(n2, sz[100:200])
+    assert len(p2) == off[200] - off[100] and s2.min() >= 0 and d2.max() < len(p2)
