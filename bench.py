@@ -74,7 +74,7 @@ LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "node_fwd": "S", "node_bw
                      "enc_edge": 1, "enc_edge_bwd": 1}
 # device kernel name prefix in the rocprofv3 PMC summaries (tools/pmcsum.py)
 PMC_PREFIX = {"edge_fwd": "k_edge_fwd", "edge_bwd": "k_edge_bwd", "node_fwd": "k_node_fwd",
-              "node_bwd": "k_node_bwd", "wgrad_w2": "k_w2grad", "enc_edge": "k_enc_edge<",
+              "node_bwd": "k_node_bwd", "wgrad_w2": "k_w2grad", "enc_edge": "k_enc_edge",
               "enc_edge_bwd": "k_enc_edge_bwd"}
 
 
@@ -254,6 +254,8 @@ def load_pmc(config: int, kernel: str, math: str, workload: str):
             return None
         tot = cnt = 0.0
         for name, v in d.items():
+            if kernel == "enc_edge" and name.startswith("k_enc_edge_bwd"):
+                continue
             if name.startswith(PMC_PREFIX[kernel]) and "hbm_read_bytes" in v and "hbm_write_bytes" in v:
                 tot += (v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["dispatches"]
                 cnt += v["dispatches"]

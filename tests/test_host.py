@@ -177,19 +177,29 @@ def test_removal_candidates_order():
         assert np.array_equal(c[i], np.delete(boxes, i, axis=0))   # JengaBuilder.py:244-249 order
 
 
-def test_bench_pmc_names_match_committed_summary():
-    """bench.py's roofline `traffic` looks kernels up by their rocprofv3 names in the committed
-    PMC summary; a template change that renames a kernel must be caught here, not as a null."""
+def test_bench_pmc_names_match_committed_summaries():
+    """bench.py's roofline `traffic` looks kernels up by name prefix in the committed PMC summary of
+    each config; a kernel rename must be caught here, not show up as a null. Every committed summary
+    with a `_workload` tag is quoted only for that workload."""
+    import glob
     import importlib.util
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    with open(os.path.join(root, "profiles", "pmc_summary.json")) as f:
-        summary = json.load(f)
-    for kernel, name in bench.PMC_NAMES["x6"].items():
-        assert name in summary, (kernel, name)
-        assert bench.load_pmc(kernel, "x6") is not None, kernel
+    for path in sorted(glob.glob(os.path.join(root, "profiles", "pmc_summary*.json"))):
+        with open(path) as f:
+            summary = json.load(f)
+        m = re.search(r"config(\d)", os.path.basename(path))
+        config = int(m.group(1)) if m else 0
+        meta = summary.get("_workload", {})
+        wl, math = meta.get("workload"), meta.get("math") or "x6"
+        kernels = ["edge_fwd"] if config == 5 else ["edge_fwd", "edge_bwd", "enc_edge", "enc_edge_bwd", "wgrad_w2"]
+        for k in kernels:
+            assert bench.load_pmc(config, k, math, wl) is not None, (path, k)
+        if meta:
+            assert bench.load_pmc(config, kernels[0], math, wl + " (other)") is None
+        assert bench.step_hbm(config, 10.0, math, wl) is not None, path
 
 
 def test_plan_without_any_edge_and_empty_batch():
