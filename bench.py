@@ -67,14 +67,15 @@ KERNELS = {
     "node_fwd": (_lib.K_NODE_FWD, lambda Ne, Nn, S: 2.0 * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150) * Nn),
     "node_bwd": (_lib.K_NODE_BWD, lambda Ne, Nn, S: 2.0 * (2 * 150 * 100 + 101 * 100 + 300 * 100 + 150 * 100) * Nn),
     "wgrad_w2": (_lib.K_WGRAD_W2, lambda Ne, Nn, S: 2.0 * 151 * 150 * Ne * S),
+    "dA": (_lib.K_DA, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne * S),
     "enc_edge": (_lib.K_ENC_EDGE, lambda Ne, Nn, S: 2.0 * (2 * 150 + 4 * 150 * 150) * Ne),
     "enc_edge_bwd": (_lib.K_ENC_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 4 * 150 * 150 * Ne),
 }
-LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "node_fwd": "S", "node_bwd": "S", "wgrad_w2": 1,
+LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "node_fwd": "S", "node_bwd": "S", "wgrad_w2": 1, "dA": 1,
                      "enc_edge": 1, "enc_edge_bwd": 1}
 # device kernel name prefix in the rocprofv3 PMC summaries (tools/pmcsum.py)
 PMC_PREFIX = {"edge_fwd": "k_edge_fwd", "edge_bwd": "k_edge_bwd", "node_fwd": "k_node_fwd",
-              "node_bwd": "k_node_bwd", "wgrad_w2": "k_w2grad", "enc_edge": "k_enc_edge",
+              "node_bwd": "k_node_bwd", "wgrad_w2": "k_w2grad", "enc_edge": "k_enc_edge", "dA": "k_dA",
               "enc_edge_bwd": "k_enc_edge_bwd"}
 
 

@@ -133,6 +133,7 @@ typedef struct spwgnn_run {
 #define SPWGNN_K_ENC_EDGE 5
 #define SPWGNN_K_ENC_EDGE_BWD 6
 #define SPWGNN_K_WGRAD_W2 7
+#define SPWGNN_K_DA 8          /* dA = Σ_s dh1pre_s rebuilt after the backward step loop (bf16 math) */
 
 /* Workspace bytes for (n_nodes, n_eblocks, mp_steps, training). */
 int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training);

@@ -573,11 +573,21 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     return SPWGNN_OK;
 }
 
+// dA = Σ_s dh1pre_s: rebuilt once after the step loop (k_dA_x6) instead of float atomics into HBM in
+// every step's edge backward (the atomics bounded that kernel; A/B on one box: x6 step 28.11 →
+// 27.39 ms, bf16 config 3 71.5 → 69.3 ms — DESIGN.md §3f). SPWGNN_DA_ATOMIC (diagnosis builds only)
+// restores the per-step atomics for A/B.
+static bool rebuild_dA(const spwgnn_run* r, const spwgnn_batch* b) {
+    const int m = kmath(r, kX6EdgeBwd);
+    return b->nw_max <= 16 && m != MATH_F32 && !getenv_flag("SPWGNN_DA_ATOMIC");
+}
+
 int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w, char* base,
                      const float* dlogits, float* grads, float* dprop, hipStream_t st) {
     (void)params;  // the packed copies made by the forward on this workspace are used
     Ctx c{w, base};
     const int S = r->mp_steps;
+    const bool rebuild = rebuild_dA(r, b);
     const int64_t nN = b->n_nodes;
     const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
     SPW_CHECK(hipMemsetAsync(grads, 0, param_table().total * sizeof(float), st));
@@ -629,6 +639,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.nw_max = b->nw_max;
         eb.wpg = b->nw_max <= 16 ? 4 : edge_wpg(edge_bwd_lds_per_wave(b->nw_max));
         eb.dA_accumulate = !first;
+        eb.no_dA = rebuild;
         eb.wtile = b->wtile;
         eb.esrc = b->edge_src;
         eb.edst = b->edge_dst;
@@ -662,6 +673,23 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             nb.x_w1ct = c.x6(X6_W1CT);
         }
         SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
+    }
+    if (rebuild) {
+        DaArgs da{};
+        da.n_eblocks = b->n_eblocks;
+        da.S = S;
+        da.g3_step = w.G3_at(1) - w.G3_at(0);
+        da.m1_step = w.m1_at(1) - w.m1_at(0);
+        da.m2_step = w.m2_at(1) - w.m2_at(0);
+        da.edst = b->edge_dst;
+        da.mask1 = c.u(w.mask1);
+        da.mask2 = c.u(w.mask2);
+        da.G3 = c.f(w.G3);
+        da.dA = c.f(w.dA);
+        da.x_w2t = c.x6(X6_W2T);
+        SPW_CHECK(prof.before(SPWGNN_K_DA));
+        SPW_CHECK(launch_dA(da, kmath(r, kX6EdgeBwd), st));
+        SPW_CHECK(prof.after(SPWGNN_K_DA));
     }
     EncEdgeBwdArgs eeb{};
     eeb.n_eblocks = b->n_eblocks;

@@ -130,6 +130,7 @@ struct NodeBwdArgs {
 struct EdgeBwdArgs {
     int n_wtiles, nw_max, wpg;
     int dA_accumulate;
+    int no_dA;         // x6/bf16: no dA here — k_dA_x6 rebuilds Σ_s dh1pre_s after the step loop
     const int32_t *wtile, *esrc, *edst;
     const uint32_t* csr;
     const uint32_t *mask1, *mask2;
@@ -137,6 +138,16 @@ struct EdgeBwdArgs {
     float *dA, *dU, *dV;
     float* dh2_out;    // dh2pre rows, chunk-major blocks (kCmBlk), for the W2 gradient
     const uint4* x_w2t; // x6 image of W2ᵀ (half rows, kh 76) — the LDS B operand (math == MATH_X6)
+};
+
+struct DaArgs {           // k_dA_x6: dA = Σ_s dh1pre_s, recomputed per 32-edge block
+    int n_eblocks, S;
+    int64_t g3_step, m1_step, m2_step;   // per-step strides (floats / u32 words)
+    const int32_t* edst;
+    const uint32_t *mask1, *mask2;
+    const float* G3;
+    float* dA;                           // row-major [e][160]
+    const uint4* x_w2t;
 };
 
 struct EncEdgeBwdArgs {
@@ -250,6 +261,7 @@ hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st);
+hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1, MATH_BF16 = 2 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);

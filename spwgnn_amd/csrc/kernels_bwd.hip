@@ -650,7 +650,7 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 // dh1pre = dh1 ⊙ [h1 > 0] goes to dA (plain stores on the first backward step, atomics after)
 // and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
 // 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
-template <bool ACCUM, int DBG = 0, int NP = 3>
+template <bool ACCUM, bool NODA = false, int NP = 3>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
     constexpr int PF = 1, kWaves = 8;
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
@@ -795,7 +795,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
                 for (int r = 8 * s; r < 8 * s + 8; ++r) {
                     float* p = dArow + rho(r, h) * kLdE + 32 * t;
-                    if constexpr (DBG == 1) {
+                    if constexpr (NODA) {
                     } else if (ACCUM) unsafeAtomicAdd(p, acc[t][r]);
                     else *p = acc[t][r];
                 }
@@ -821,29 +821,26 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
-    if (math == MATH_BF16 && a.nw_max <= 16) {
-        const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);
-        if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true, 0, 1>), g, b, 0, st, a);
-        else hipLaunchKernelGGL((k_edge_bwd_x6<false, 0, 1>), g, b, 0, st, a);
-        return hipGetLastError();
-    }
-    if (math == MATH_X6 && a.nw_max <= 16) {
+    if (math != MATH_F32 && a.nw_max <= 16) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
-#ifdef SPWGNN_DIAG   // 1: drop the dA writes (diagnosis only: wrong results)
-        static const int dbg = getenv("SPWGNN_EBWD_DBG") ? atoi(getenv("SPWGNN_EBWD_DBG")) : 0;
-#else
-        constexpr int dbg = 0;
-#endif
-        if (dbg == 1) {
-            if (a.dA_accumulate)
-                hipLaunchKernelGGL((k_edge_bwd_x6<true, 1>), g, b, 0, st, a);
-            else
-                hipLaunchKernelGGL((k_edge_bwd_x6<false, 1>), g, b, 0, st, a);
-        } else if (a.dA_accumulate)
-            hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
-        else
-            hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
+        // no_dA: dA = Σ_s dh1pre_s is rebuilt once after the step loop by k_dA_x6 (launch_dA)
+        if (a.no_dA) {
+            if (math == MATH_BF16) hipLaunchKernelGGL((k_edge_bwd_x6<false, true, 1>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_edge_bwd_x6<false, true>), g, b, 0, st, a);
+            return hipGetLastError();
+        }
+#ifdef SPWGNN_DIAG   // per-step dA stores + float atomics (SPWGNN_DA_ATOMIC A/B builds only)
+        if (math == MATH_BF16) {
+            if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true, false, 1>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_edge_bwd_x6<false, false, 1>), g, b, 0, st, a);
+        } else {
+            if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
+        }
         return hipGetLastError();
+#else
+        return hipErrorInvalidValue;
+#endif
     }
     if (a.nw_max <= 16) {
         if (a.dA_accumulate)
@@ -857,6 +854,131 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
         else
             hipLaunchKernelGGL((k_edge_bwd<false, false>), dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
     }
+    return hipGetLastError();
+}
+
+// dA = Σ_s dh1pre_s, rebuilt once after the backward step loop instead of accumulated by every
+// step's edge kernel (float atomics into a row-major HBM array: the edge backward's bound, DESIGN.md
+// §10). Per 32-edge block a wave recomputes each step's dh1pre_s = ((G3_s[receiver] ⊙ [h2_s > 0])·W2ᵀ)
+// ⊙ [h1_s > 0] exactly as k_edge_bwd_x6 does (same operand order, same k order: bit-identical
+// values), sums the steps in registers in the order the atomics did (S-1 first, then S-2 .. 0: the
+// same fp32 sums, bit-identical dA) and stores dA once with plain stores.
+// W2ᵀ (x6 image) is the LDS B operand; blocks are independent (no tile structure needed).
+template <int NP = 3>
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_dA_x6(DaArgs a) {
+    constexpr int kWaves = 8, PF = 2;
+    static_assert(10 % PF == 0, "ring slots carry over between (block, step) pairs");
+    __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
+    for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2t[idx];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint4* wlp = wl + lane;
+    // a contiguous range of blocks per wave: a tower's blocks (same receiver rows) stay on one CU
+    const int nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wave;
+    const int per = (a.n_eblocks + nw - 1) / nw;
+    const int b0 = gw * per, b1 = min(b0 + per, a.n_eblocks);
+    if (b0 >= b1) return;
+    // one (block, step) pair: its receiver row pointer (G3 of that step) and its mask words
+    struct Pair { const float4* G4; uint32_t w[5], m1w[5]; };
+    auto load_pair = [&](int blk, int s, int d) {
+        Pair p;
+        const bool valid = d >= 0;
+        p.G4 = reinterpret_cast<const float4*>(a.G3 + s * a.g3_step + cm_index<kKhE>(valid ? d : 0, 0) + h * 128);
+        const uint32_t* m2 = a.mask2 + s * a.m2_step + (int64_t)blk * 160 + i;
+        const uint32_t* m1 = a.mask1 + s * a.m1_step + (int64_t)blk * kLdE + i;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            p.w[t] = valid ? m2[32 * t] : 0u;
+            p.m1w[t] = m1[32 * t];
+        }
+        return p;
+    };
+    struct KB { float4 g[2]; };
+    auto ld = [&](const float4* G4, int kb, KB& r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
+    };
+    int blk = b0, s = a.S - 1;
+    int d = a.edst[(int64_t)blk * 32 + i];
+    Pair cur = load_pair(blk, s, d);
+    KB ring[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) ld(cur.G4, k, ring[k]);
+    f32x16 dacc[5];
+    zero_tiles(dacc);
+    for (;;) {
+        // the next pair (steps S-1 .. 0 of a block, then the next block; clamped at the range end)
+        const bool last_step = s == 0;
+        const bool has_next = !last_step || blk + 1 < b1;
+        const int nblk = last_step ? min(blk + 1, b1 - 1) : blk;
+        const int ns = last_step ? a.S - 1 : s - 1;
+        const int nd = last_step ? a.edst[(int64_t)nblk * 32 + i] : d;
+        const Pair nxt = load_pair(nblk, max(ns, 0), nd);
+        const uint64_t mlo = h == 0 ? ((uint64_t)cur.w[1] << 32 | cur.w[0])
+                                    : ((uint64_t)cur.w[4] << 52 | (uint64_t)cur.w[3] << 20 | (cur.w[2] >> 12));
+        const uint32_t mhi = h == 0 ? (cur.w[2] & 0xfffu) : (cur.w[4] >> 12);
+        f32x16 acc[5];
+        zero_tiles(acc);
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % PF];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int q = 2 * kb + c;
+                const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
+                xv[4 * c + 0] = (bits & 1u) ? cr.g[c].x : 0.f;
+                xv[4 * c + 1] = (bits & 2u) ? cr.g[c].y : 0.f;
+                xv[4 * c + 2] = (bits & 4u) ? cr.g[c].z : 0.f;
+                xv[4 * c + 3] = (bits & 8u) ? cr.g[c].w : 0.f;
+            }
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            if (kb + PF < 10) ld(cur.G4, kb + PF, cr);
+            else ld(nxt.G4, kb + PF - 10, cr);
+            bf16x8 ap[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+            for (int T = 0; T < 5; ++T) {
+                const uint4* wp = wlp + (kb * 5 + T) * 3 * 64;
+                bf16x8 bp[3];
+                bp[0] = as_bf16x8(wp[0]);
+                bp[1] = as_bf16x8(wp[64]);
+                bp[2] = as_bf16x8(wp[128]);
+                acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const uint32_t mw1 = cur.m1w[t];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dacc[t][r] += ((mw1 >> rho(r, h)) & 1u) ? acc[t][r] : 0.f;
+        }
+        if (last_step) {   // the block's S steps are summed: one plain store of its dA rows
+            float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * t] = dacc[t][r];
+            zero_tiles(dacc);
+        }
+        if (!has_next) break;
+        blk = nblk;
+        s = ns;
+        d = nd;
+        cur = nxt;
+    }
+}
+
+hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st) {
+    const dim3 g(edge_grid(a.n_eblocks, 8)), b(512);
+    if (math == MATH_BF16) hipLaunchKernelGGL((k_dA_x6<1>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_dA_x6<3>), g, b, 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st) {

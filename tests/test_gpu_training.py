@@ -178,6 +178,33 @@ def test_trainer_step_matches_oracle_adam():
     assert np.abs(got - ref).max() < 2e-6     # 3 Adam steps of 5e-4-sized updates, fp32
 
 
+def test_trainer_step_l2_regularizer():
+    """The optional L2(1e-3) kernel/bias regularizer of Blocks.py:23-27 (unpinned in the reference:
+    whether Keras adds it to the compiled loss depends on its version): three f32-math
+    trainer steps with l2 = 1e-3 against the fp64 oracle's gradients + Keras Adam on g + 2·l2·w."""
+    params = O.random_params(13)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(16, 6, seed=23, fully_connected=False)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, None, device="cuda")
+    flat = P.to_flat(params, device="cuda")
+    tr = Trainer(flat, mp_steps=5, dropout=0.0, math="f32", l2=1e-3)
+    opt = O.KerasAdam(l2=1e-3)
+    ref = P.to_flat(params, dtype=torch.float64).numpy()
+    for _ in range(3):
+        tr.step(batch, torch.tensor(tgt.reshape(-1), device="cuda"))
+        _, _, g = O.loss_and_grads(P.from_flat(torch.tensor(ref)), obj, Rs, Rr, prop, tgt, 5)
+        ref = opt.step(ref, P.to_flat(g, dtype=torch.float64).numpy())
+    torch.cuda.synchronize()
+    got = flat.cpu().numpy()
+    assert np.abs(got - ref).max() < 2e-6
+    # the regularizer changed the trajectory (it is not silently dropped)
+    plain = O.KerasAdam()
+    ref0 = P.to_flat(params, dtype=torch.float64).numpy()
+    for _ in range(3):
+        _, _, g = O.loss_and_grads(P.from_flat(torch.tensor(ref0)), obj, Rs, Rr, prop, tgt, 5)
+        ref0 = plain.step(ref0, P.to_flat(g, dtype=torch.float64).numpy())
+    assert np.abs(got - ref0).max() > 1e-5
+
+
 def test_trainer_step_x6_adam_rule():
     """x6 math: each trainer step = Keras Adam (fp64 oracle) applied to the step's own gradients,
     and the first step's gradients match the oracle's.
