@@ -281,6 +281,24 @@ struct Prof {
         if (e_ != hipSuccess) return (int32_t)e_;     \
     } while (0)
 
+// dA = Σ_s dh1pre_s: rebuilt once after the step loop (k_dA_x6) instead of float atomics into HBM in
+// every step's edge backward (the atomics bounded that kernel; A/B on one box: x6 step 28.11 →
+// 27.39 ms, bf16 config 3 71.5 → 69.3 ms — DESIGN.md §3f). SPWGNN_DA_ATOMIC (diagnosis builds only)
+// restores the per-step atomics for A/B.
+static bool rebuild_dA(const spwgnn_run* r, const spwgnn_batch* b) {
+    const int m = kmath(r, kX6EdgeBwd);
+    return b->nw_max <= 16 && m != MATH_F32 && !getenv_flag("SPWGNN_DA_ATOMIC");
+}
+
+// bf16 math stores the encoder-side edge arrays that only ever feed MFMA operands — z2, z3, c_r, dz4..dz1
+// and dA — as bf16 (exact: the operands are rounded to bf16 anyway). Every kernel that
+// writes or reads them must run in bf16 math for the layouts to agree.
+static bool store_b16(const spwgnn_run* r, const spwgnn_batch* b) {
+    return r->training && r->math == MATH_BF16 && kmath(r, kX6EncEdge) == MATH_BF16 &&
+           kmath(r, kX6EncEdgeBwd) == MATH_BF16 && kmath(r, kX6Wgrad) == MATH_BF16 && rebuild_dA(r, b) &&
+           !getenv_flag("SPWGNN_WG_OLD");
+}
+
 static int32_t run_forward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w,
                            char* base, float* logits, hipStream_t st) {
     Ctx c{w, base};
@@ -372,6 +390,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.cr = c.f(w.cr);
     ee.A = c.f(w.A);
     ee.zmask = r->training ? c.u(w.zmask) : nullptr;
+    ee.b16 = store_b16(r, b);
     ee.dropout_on = drop;
     ee.thresh = thresh;
     ee.scale = scale;
@@ -459,6 +478,7 @@ struct WgSpec {
     // reduce target
     int tk = -1, tb = -1, k_rows = 0, k_row0 = 0, bias_row = -1, perm = 0;
     bool recompute = false;   // XM_H1 / YM_DH2 context below
+    int b16 = 0;              // kB16X / kB16Y: bf16-stored operands (bf16 math, store_b16)
     const float2* xd = nullptr;          // z1 rebuilt from d (k_wgrad_ws XD 1)
     const float4* xp = nullptr;          // zo1 rebuilt from the node positions (XD 2)
     const float *w0 = nullptr, *b0 = nullptr;
@@ -534,7 +554,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         chunks = wgs;
         const bool mask = !(g.kx_pad == 160 && g.ny_pad == 160);   // node arrays: rows ≥ count masked
         if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
-        SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, math, st));
+        SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, math, st, g.b16));
         if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     } else {
     // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
@@ -550,7 +570,9 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     if (ws)
         SPW_CHECK(launch_w2grad_ws(a, (int)chunks, bpw, math, st));
     else if (math == MATH_BF16)
-        SPW_CHECK(launch_wgrad_bf16(a, (int)chunks, st));
+        SPW_CHECK(launch_wgrad_bf16(a, (int)chunks, st, g.b16));
+    else if (g.b16)
+        return SPWGNN_E_ARG;
     else
         SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
     if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
@@ -573,21 +595,13 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     return SPWGNN_OK;
 }
 
-// dA = Σ_s dh1pre_s: rebuilt once after the step loop (k_dA_x6) instead of float atomics into HBM in
-// every step's edge backward (the atomics bounded that kernel; A/B on one box: x6 step 28.11 →
-// 27.39 ms, bf16 config 3 71.5 → 69.3 ms — DESIGN.md §3f). SPWGNN_DA_ATOMIC (diagnosis builds only)
-// restores the per-step atomics for A/B.
-static bool rebuild_dA(const spwgnn_run* r, const spwgnn_batch* b) {
-    const int m = kmath(r, kX6EdgeBwd);
-    return b->nw_max <= 16 && m != MATH_F32 && !getenv_flag("SPWGNN_DA_ATOMIC");
-}
-
 int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w, char* base,
                      const float* dlogits, float* grads, float* dprop, hipStream_t st) {
     (void)params;  // the packed copies made by the forward on this workspace are used
     Ctx c{w, base};
     const int S = r->mp_steps;
     const bool rebuild = rebuild_dA(r, b);
+    const bool b16 = store_b16(r, b);
     const int64_t nN = b->n_nodes;
     const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
     SPW_CHECK(hipMemsetAsync(grads, 0, param_table().total * sizeof(float), st));
@@ -687,12 +701,14 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         da.G3 = c.f(w.G3);
         da.dA = c.f(w.dA);
         da.x_w2t = c.x6(X6_W2T);
+        da.b16 = b16;
         SPW_CHECK(prof.before(SPWGNN_K_DA));
         SPW_CHECK(launch_dA(da, kmath(r, kX6EdgeBwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_DA));
     }
     EncEdgeBwdArgs eeb{};
     eeb.n_eblocks = b->n_eblocks;
+    eeb.b16 = b16;
     eeb.dA = c.f(w.dA);
     eeb.zmask = c.u(w.zmask);
     eeb.w1at = c.pk(PK_W1AT);
@@ -746,6 +762,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
+        g.b16 = b16 ? kB16Y : 0;   // Y = dz1
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
@@ -757,11 +774,13 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.w0 = c.pk(PK_RM0);
             g.b0 = c.pk(PB_RM0);
         }
+        g.b16 = b16 ? kB16Y : 0;   // X rebuilt from d; Y = dz2
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
     }
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    const int b16xy = b16 ? (kB16X | kB16Y) : 0;
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
         // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);

@@ -87,6 +87,31 @@ __device__ __forceinline__ void load_cm(const float* __restrict__ blk, f32x16 (&
             X[t][4 * q + 3] = v.w;
         }
 }
+// ---- bf16 storage (bf16 math): an array that only ever feeds MFMA operands is stored
+// as bf16 with the element index of its fp32 layout (a 16-byte float4 piece becomes an 8-byte uint2
+// at the same element offset). The bf16 math rounds every operand to bf16 (RNE) anyway, so storing
+// the rounded value is exact: the products see the same bits.
+__device__ __forceinline__ uint2 pack4_bf16(float4 v) { return make_uint2(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w)); }
+__device__ __forceinline__ float4 unpack4_bf16(uint2 u) {
+    return make_float4(bf16_lo(u.x), bf16_hi(u.x), bf16_lo(u.y), bf16_hi(u.y));
+}
+template <int NT>
+__device__ __forceinline__ void store_cm_b16(uint16_t* __restrict__ blk, const f32x16 (&X)[NT], int lane, bool valid) {
+    constexpr int KH = NT == 5 ? kKhE : kKhN;
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            if (32 * t + 8 * q + 4 < 2 * KH) {
+                const float4 v = valid ? make_float4(X[t][4 * q], X[t][4 * q + 1], X[t][4 * q + 2], X[t][4 * q + 3])
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+                *reinterpret_cast<uint2*>(blk + cm_offk<KH>(j, f0)) = pack4_bf16(v);
+            }
+        }
+}
+
 // split-halves chunk of a chunk-major row: x[s] = feature KH·h + s of row j
 template <int KH>
 __device__ __forceinline__ void load_half_cm(const float* __restrict__ blk, int lane, float (&x)[KH]) {

@@ -84,6 +84,7 @@ struct EncEdgeArgs {
     float *z1, *z2, *z3, *cr, *A;   // chunk-major blocks (z1 null: the W1 gradient rebuilds it from ed)
     float2* ed;                     // training: per-edge (dx, dy), rows of the 32-edge blocks
     uint32_t* zmask;                // [blk][4 layers: z1,z2,z3,cr][3 words][64 lanes] — activation > 0 bits
+    int b16;                        // bf16 math: z2, z3, c_r stored as bf16 (same element layout)
     int dropout_on;
     uint32_t thresh;
     float scale;
@@ -142,6 +143,7 @@ struct EdgeBwdArgs {
 
 struct DaArgs {           // k_dA_x6: dA = Σ_s dh1pre_s, recomputed per 32-edge block
     int n_eblocks, S;
+    int b16;                             // bf16 math: dA stored as bf16 (row-major [e][160])
     int64_t g3_step, m1_step, m2_step;   // per-step strides (floats / u32 words)
     const int32_t* edst;
     const uint32_t *mask1, *mask2;
@@ -152,6 +154,7 @@ struct DaArgs {           // k_dA_x6: dA = Σ_s dh1pre_s, recomputed per 32-edge
 
 struct EncEdgeBwdArgs {
     int n_eblocks;
+    int b16;                        // bf16 math: dA read and dz4..dz1 stored as bf16
     const float* dA;                // row-major [e][160] (accumulated by k_edge_bwd)
     const uint32_t* zmask;          // from k_enc_edge
     const float *w1at, *rm3t, *rm2t, *rm1t;
@@ -220,6 +223,8 @@ struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 3
     int64_t nbs, S, x_sb, y_sb, count, stages_per_wg;
     int x_ones, pad0;
 };
+// bf16 storage of the weight gradients' edge operands (bf16 math, §3g): bit 0 X, bit 1 Y
+enum : int { kB16X = 1, kB16Y = 2 };
 struct ReduceArgs {
     const float* slab;
     int chunks, kx_pad, ny_pad;
@@ -266,8 +271,8 @@ hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1, MATH_BF16 = 2 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
-                           hipStream_t st);
-hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st);
+                           hipStream_t st, int b16 = 0);
+hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st, int b16 = 0);
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st);
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);

@@ -517,7 +517,9 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // The same backward chain in split-bf16 math: two 32-edge column tiles per wave (kernels_fwd.hip
 // k_enc_edge_x6). dA rows (row-major) are loaded whole up front as half rows (lane half h: features
 // 76h .. 76h+75, image kind kh = 76), into the registers the second layer's output uses later.
-template <int NC, int NP = 3>
+// B16 (bf16 math): dA is read and dz4..dz1 (the weight gradients' Y operands only) are stored as bf16
+// (exact, §3g).
+template <int NC, int NP = 3, bool B16 = false>
 __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -528,9 +530,15 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int64_t e = (int64_t)min(blk0 + c, a.n_eblocks - 1) * 32 + j;
-            const float4* row = reinterpret_cast<const float4*>(a.dA + e * kLdE + kKhE * h);
+            if constexpr (B16) {
+                const uint2* row = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.dA) + e * kLdE + kKhE * h);
 #pragma unroll
-            for (int q = 0; q < kKhE / 4; ++q) raw[c][q] = row[q];
+                for (int q = 0; q < kKhE / 4; ++q) raw[c][q] = unpack4_bf16(row[q]);
+            } else {
+                const float4* row = reinterpret_cast<const float4*>(a.dA + e * kLdE + kKhE * h);
+#pragma unroll
+                for (int q = 0; q < kKhE / 4; ++q) raw[c][q] = row[q];
+            }
             zero_tiles(D[c]);
         }
         tgemm_x6<5, (kKhE + 7) / 8, NC, 6, NP>(
@@ -547,7 +555,8 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             if (c == 1 && !has1) break;
-            store_cm<5>(base + (int64_t)(blk0 + c) * kCmBlk, Z[c], lane, true);
+            if constexpr (B16) store_cm_b16<5>(reinterpret_cast<uint16_t*>(base) + (int64_t)(blk0 + c) * kCmBlk, Z[c], lane, true);
+            else store_cm<5>(base + (int64_t)(blk0 + c) * kCmBlk, Z[c], lane, true);
         }
     };
     auto bits = [&](int layer, f32x16 (&Z)[NC][5], float scale) {
@@ -864,7 +873,7 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
 // values), sums the steps in registers in the order the atomics did (S-1 first, then S-2 .. 0: the
 // same fp32 sums, bit-identical dA) and stores dA once with plain stores.
 // W2ᵀ (x6 image) is the LDS B operand; blocks are independent (no tile structure needed).
-template <int NP = 3>
+template <int NP = 3, bool B16 = false>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_dA_x6(DaArgs a) {
     constexpr int kWaves = 8, PF = 2;
     static_assert(10 % PF == 0, "ring slots carry over between (block, step) pairs");
@@ -960,11 +969,19 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int r = 0; r < 16; ++r) dacc[t][r] += ((mw1 >> rho(r, h)) & 1u) ? acc[t][r] : 0.f;
         }
         if (last_step) {   // the block's S steps are summed: one plain store of its dA rows
-            float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
+            if constexpr (B16) {   // bf16 math: dA feeds MFMA operands only (§3g)
+                __bf16* dArow = reinterpret_cast<__bf16*>(a.dA) + (int64_t)blk * 32 * kLdE + i;
 #pragma unroll
-            for (int t = 0; t < 5; ++t)
+                for (int t = 0; t < 5; ++t)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * t] = dacc[t][r];
+                    for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * t] = (__bf16)dacc[t][r];
+            } else {
+                float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
+#pragma unroll
+                for (int t = 0; t < 5; ++t)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * t] = dacc[t][r];
+            }
             zero_tiles(dacc);
         }
         if (!has_next) break;
@@ -977,14 +994,17 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st) {
     const dim3 g(edge_grid(a.n_eblocks, 8)), b(512);
-    if (math == MATH_BF16) hipLaunchKernelGGL((k_dA_x6<1>), g, b, 0, st, a);
+    if (math == MATH_BF16 && a.b16) hipLaunchKernelGGL((k_dA_x6<1, true>), g, b, 0, st, a);
+    else if (math == MATH_BF16) hipLaunchKernelGGL((k_dA_x6<1>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_dA_x6<3>), g, b, 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st) {
     if (math == MATH_BF16) {
         constexpr int NC = 2;
-        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1>), dim3((a.n_eblocks + 4 * NC - 1) / (4 * NC)), dim3(256), 0, st, a);
+        const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
+        if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, true>), g, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1>), g, dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (math == MATH_X6) {

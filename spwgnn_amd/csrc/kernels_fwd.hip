@@ -266,7 +266,9 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // The rm encoder in split-bf16 math: two 32-edge blocks per wave (column tiles c), so each 16-byte
 // weight fragment feeds two MFMAs (the x6 images stream from L2 at half the per-MFMA rate);
 // 1 wave per SIMD (in + out activations: 320 registers).
-template <bool TRAIN, int NC, int NP = 3>
+// B16 (bf16 math): z2, z3 and c_r — MFMA operands only (the weight gradients' X) — are stored as bf16
+// (exact, §3g); A stays fp32 (h1 = relu(A + U + V) adds it before the rounding).
+template <bool TRAIN, int NC, int NP = 3, bool B16 = false>
 __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -296,12 +298,15 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
             }
     }
     const bool has1 = NC > 1 && blk0 + 1 < a.n_eblocks;
-    auto save = [&](float* base, uint32_t* words, const f32x16 (&Z)[NC][5]) {
+    auto save = [&](float* base, uint32_t* words, const f32x16 (&Z)[NC][5], bool b16 = false) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             if (c == 1 && !has1) break;
             const int blk = blk0 + c;
-            if (base) store_cm<5>(base + (int64_t)blk * kCmBlk, Z[c], lane, true);
+            if (base) {
+                if (B16 && b16) store_cm_b16<5>(reinterpret_cast<uint16_t*>(base) + (int64_t)blk * kCmBlk, Z[c], lane, true);
+                else store_cm<5>(base + (int64_t)blk * kCmBlk, Z[c], lane, true);
+            }
             if (words) store_pos_bits<5>(words + (int64_t)blk * 4 * 3 * 64, Z[c], lane);
         }
     };
@@ -314,12 +319,12 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     tchain_x6<5, 10, 5, NC, kX6Ring, NP>(X, Y, a.x_rm1, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, true>(Y[c], a.b_rm1, h);
-    if (TRAIN) save(a.z2, a.zmask + 3 * 64, Y);
+    if (TRAIN) save(a.z2, a.zmask + 3 * 64, Y, true);
     zero2(X);
     tchain_x6<5, 10, 5, NC, kX6Ring, NP>(Y, X, a.x_rm2, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, true>(X[c], a.b_rm2, h);
-    if (TRAIN) save(a.z3, a.zmask + 6 * 64, X);
+    if (TRAIN) save(a.z3, a.zmask + 6 * 64, X, true);
     zero2(Y);
     tchain_x6<5, 10, 5, NC, kX6Ring, NP>(X, Y, a.x_rm3, lane);
 #pragma unroll
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
                 }
         }
     }
-    if (TRAIN) save(a.cr, a.zmask + 9 * 64, Y);
+    if (TRAIN) save(a.cr, a.zmask + 9 * 64, Y, true);
     zero2(X);
     tchain_x6<5, 10, 5, NC, kX6Ring, NP>(Y, X, a.x_w1a, lane);
 #pragma unroll
@@ -1085,7 +1090,8 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
         constexpr int NC = 2;
         const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
         if (math == MATH_BF16) {
-            if (train) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1>), g, dim3(256), 0, st, a);
+            if (train && a.b16) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1, true>), g, dim3(256), 0, st, a);
+            else if (train) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1>), g, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((k_enc_edge_x6<false, NC, 1>), g, dim3(256), 0, st, a);
         } else if (train) {
             hipLaunchKernelGGL((k_enc_edge_x6<true, NC>), g, dim3(256), 0, st, a);

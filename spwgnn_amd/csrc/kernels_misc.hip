@@ -130,7 +130,7 @@ __device__ __forceinline__ void group_rc(int g, int& rr, int& c4) {
 // the column groups c4 = (tid >> 5) + 8k (k < W/32), so the in-block offsets are fixed per thread
 // and a block costs one row map plus W/32 16-byte loads (the 32 lanes of a column group read 512
 // contiguous bytes).
-template <int W>
+template <int W, bool B16 = false>   // B16: bf16-stored operand (bf16 math, §3g)
 struct CmStage {
     static constexpr int KH = W == 160 ? kKhE : kKhN, BLK = KH * 64, NG = W / 32;
     int off[NG];     // in-block offset of group k for in-block row 0, -1 for padding columns (≥ 2·KH)
@@ -149,10 +149,14 @@ struct CmStage {
     __device__ __forceinline__ void fetch(const float* __restrict__ base, int64_t phys, bool in) {
         // the physical row's own position in its block (logical and physical 32-row blocks differ
         // when a step's row count is not a multiple of 32)
-        const float* b = base + (phys >> 5) * BLK + (phys & 31) * 4;
+        const int64_t ib = (phys >> 5) * BLK + (phys & 31) * 4;
+        const float* b = base + ib;
+        const uint16_t* b16 = reinterpret_cast<const uint16_t*>(base) + ib;
 #pragma unroll
         for (int k = 0; k < NG; ++k)
-            raw[k] = (in && off[k] >= 0) ? *reinterpret_cast<const float4*>(b + off[k]) : f4zero();
+            raw[k] = (in && off[k] >= 0) ? (B16 ? unpack4_bf16(*reinterpret_cast<const uint2*>(b16 + off[k]))
+                                                : *reinterpret_cast<const float4*>(b + off[k]))
+                                         : f4zero();
     }
     // f(rr, c4, v): the staged float4 of row rr, column group c4
     template <class F>
@@ -263,7 +267,7 @@ struct EdgeStage {
 
 // Operand staging shared by the wgrad kernels: every operand is fetched a 32-row block ahead into
 // registers (fetch), then handed out as float4 groups (emit_x / emit_y: f(row rr, column group c4, v)).
-template <int XM, int YM, int KXP, int NYP>
+template <int XM, int YM, int KXP, int NYP, bool YB16 = false>
 struct WgStage {
     static constexpr int GX = KXP / 4, GY = NYP / 4;
     static constexpr int NGX = (32 * GX + kWgThreads - 1) / kWgThreads;   // float4 groups per thread
@@ -272,7 +276,7 @@ struct WgStage {
     XRaw xr[(XCM || XH1) ? 1 : NGX];
     YRaw yr[(YCM || YD2) ? 1 : NGY];
     CmStage<KXP> xc;
-    CmStage<NYP> yc;
+    CmStage<NYP, YB16> yc;
     EdgeStage xe, ye;
     int64_t xcount, ycount, r_begin, r_end;
     __device__ __forceinline__ void init(const WgradArgs& a, int64_t r_begin_, int64_t r_end_, int tid) {
@@ -468,7 +472,7 @@ struct X6Img {
 // The same gradient in split-bf16 math (x6): operands are split once when staged (every element
 // feeds MX or MY tiles), 16x16x32 bf16 MFMAs, one k-step per 32-row block: 6·MX·MY MFMAs of 16
 // cycles per wave per block instead of 8·MX·MY f32 MFMAs of 32.
-template <int XM, int YM, int KXP, int NYP, int OCC, int NP = 3>
+template <int XM, int YM, int KXP, int NYP, int OCC, int NP = 3, bool YB16 = false>
 __global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
     constexpr int MX = KXP / 32, MY = NYP / 32;
     using IX = X6Img<KXP>;
@@ -490,7 +494,7 @@ __global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
     for (int x = 0; x < MX; ++x) ox[x] = IX::roff(lane, MX * wx + x);
 #pragma unroll
     for (int y = 0; y < MY; ++y) oy[y] = IY::roff(lane, MY * wy + y);
-    WgStage<XM, YM, KXP, NYP> st;
+    WgStage<XM, YM, KXP, NYP, YB16> st;
     st.init(a, r_begin, r_end, tid);
     st.fetch(a, r_begin, tid);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
@@ -734,7 +738,8 @@ struct WsSet4 {
 // XD: X = [z1 | 1] rebuilt from the per-edge (dx, dy) (XD 1), or [zo1 | 1] from the node's (y, w)
 // (XD 2), with the encoders' own first-layer arithmetic (dense2 + relu on the same pack):
 // bit-identical to the activations the encoders no longer store.
-template <int KXP, int NYP, int YROW, bool MASK, int NP = 3, int XD = 0>
+// B16 (bf16 math, §3g): X (kB16X) and/or Y (kB16Y) stored as bf16 with the fp32 element layout.
+template <int KXP, int NYP, int YROW, bool MASK, int NP = 3, int XD = 0, int B16 = 0>
 __global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_wgrad_ws(WgWsArgs a) {
     using W = WsStage<KXP, NYP, YROW, MASK>;
@@ -832,9 +837,12 @@ void k_wgrad_ws(WgWsArgs a) {
         const int64_t tg = t0 + (t < T ? t : T - 1);
         const int64_t s = tg / a.nbs, nb = tg - s * a.nbs;
         if (MASK) R.nvalid = (int)min<int64_t>(32, a.count - nb * 32);
-        const float* px = a.x + (s * a.x_sb + nb) * (W::KHX * 64) + rr * 4;
-        const float* py = YROW ? a.y + ((s * a.y_sb + nb) * 32 + yr) * 160
-                               : a.y + (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
+        const int64_t ix = (s * a.x_sb + nb) * (W::KHX * 64) + rr * 4;   // element indices
+        const int64_t iy = YROW ? ((s * a.y_sb + nb) * 32 + yr) * 160 : (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
+        const float* px = a.x + ix;
+        const float* py = a.y + iy;
+        const uint16_t* hx = reinterpret_cast<const uint16_t*>(a.x) + ix;
+        const uint16_t* hy = reinterpret_cast<const uint16_t*>(a.y) + iy;
         if (XD == 1) {
             R.d = a.xd[(s * a.x_sb + nb) * 32 + rr];
         } else if (XD == 2) {
@@ -842,10 +850,14 @@ void k_wgrad_ws(WgWsArgs a) {
             R.d = make_float2(p.y, p.z);   // Networks.py:65-71: (y, width)
         } else {
 #pragma unroll
-            for (int k = 0; k < W::NKX; ++k) R.x[k] = *reinterpret_cast<const float4*>(px + offx[k]);
+            for (int k = 0; k < W::NKX; ++k)
+                R.x[k] = (B16 & kB16X) ? unpack4_bf16(*reinterpret_cast<const uint2*>(hx + offx[k]))
+                                       : *reinterpret_cast<const float4*>(px + offx[k]);
         }
 #pragma unroll
-        for (int k = 0; k < W::NKY; ++k) R.y[k] = *reinterpret_cast<const float4*>(py + offy[k]);
+        for (int k = 0; k < W::NKY; ++k)
+            R.y[k] = (B16 & kB16Y) ? unpack4_bf16(*reinterpret_cast<const uint2*>(hy + offy[k]))
+                                   : *reinterpret_cast<const float4*>(py + offy[k]);
     };
     auto build = [&](const WsSet4& R, char* Xs) {
         char* Ys = Xs + W::IMX;
@@ -1048,9 +1060,13 @@ hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st
     return hipErrorInvalidValue;
 }
 // bf16 math: the two small position-operand gradients (the stored-operand ones run on k_wgrad_ws)
-hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st) {
+hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st, int b16) {
     const dim3 g(chunks), b(kWgThreads);
-    if (a.xmode == XM_EDGE_D && a.ymode == YM_CM && a.kx_pad == 32 && a.ny_pad == 160)
+    if (a.xmode == XM_EDGE_D && a.ymode == YM_CM && a.kx_pad == 32 && a.ny_pad == 160 && b16 == kB16Y)
+        hipLaunchKernelGGL((k_wgrad_x6<XM_EDGE_D, YM_CM, 32, 160, 2, 1, true>), g, b, 0, st, a);   // Y = dz1 (bf16)
+    else if (b16)
+        return hipErrorInvalidValue;
+    else if (a.xmode == XM_EDGE_D && a.ymode == YM_CM && a.kx_pad == 32 && a.ny_pad == 160)
         hipLaunchKernelGGL((k_wgrad_x6<XM_EDGE_D, YM_CM, 32, 160, 2, 1>), g, b, 0, st, a);
     else if (a.xmode == XM_NODE_O && a.ymode == YM_CM && a.kx_pad == 32 && a.ny_pad == 128)
         hipLaunchKernelGGL((k_wgrad_x6<XM_NODE_O, YM_CM, 32, 128, 2, 1>), g, b, 0, st, a);
@@ -1085,11 +1101,16 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
     return hipGetLastError();
 }
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
-                           hipStream_t st) {
+                           hipStream_t st, int b16) {
     const dim3 g(wgs), b(kWsThreads);
+    if (b16 && math != MATH_BF16) return hipErrorInvalidValue;
     if (a.xd) {   // the rm.1 gradient with X = [z1 | 1] rebuilt from (dx, dy)
         if (kx_pad != 160 || ny_pad != 160 || yrow || mask) return hipErrorInvalidValue;
-        if (math == MATH_BF16)
+        if (b16 == kB16Y)
+            hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1, kB16Y>), g, b, 0, st, a);
+        else if (b16)
+            return hipErrorInvalidValue;
+        else if (math == MATH_BF16)
             hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1>), g, b, 0, st, a);
         else
             hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 3, 1>), g, b, 0, st, a);
@@ -1101,6 +1122,12 @@ hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, i
             hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 1, 2>), g, b, 0, st, a);
         else
             hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 3, 2>), g, b, 0, st, a);
+        return hipGetLastError();
+    }
+    if (b16) {   // the encoder-side edge operands of bf16 math (rm.2, rm.3: X, Y; W1a: X = c_r, Y = dA rows)
+        if (kx_pad != 160 || ny_pad != 160 || mask || b16 != (kB16X | kB16Y)) return hipErrorInvalidValue;
+        if (yrow) hipLaunchKernelGGL((k_wgrad_ws<160, 160, 1, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a);
         return hipGetLastError();
     }
 #define SPW_WS(KX, NY, YR, MK)                                                                   \
