@@ -330,6 +330,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the other-math reference measurements")
+    ap.add_argument("--no-kernel-table", action="store_true", help="skip the per-kernel roofline table")
     ap.add_argument("--infer", action="store_true", help="alias of --config 5")
     args = ap.parse_args()
     if args.infer:
@@ -452,12 +453,45 @@ def run_train(args, cfg, world, rank, device):
             del trm
             torch.cuda.empty_cache()
     out["hbm"] = step_hbm(args.config, out["ms_per_step"], math, wl)
+    if world == 1 and len(batches) == 1 and not args.no_kernel_table:
+        out["kernels"] = kernel_table(trainer, step_in, S, Ne, Nn, math, args.config, wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_table(trainer, step_in, S, Ne, Nn, math, config, wl, steps=2):
+    """Every timed kernel's roofline in the same run (after the timed region): `steps` extra training
+    steps per kernel with HIP events around each of its launches (the library's prof hook takes one
+    kernel id per call). Per kernel: mean launch ms, ms per step, achieved TFLOP/s, frac of the math's
+    matrix peak, measured HBM bytes per launch from the committed PMC summary of this workload."""
+    table = {}
+    for name, (kid, _) in KERNELS.items():
+        per = LAUNCHES_PER_STEP[name]
+        n = (S if per == "S" else per) * steps
+        ev = HipEvents(2 * n)
+        trainer.prof_kernel = kid
+        pstep = n // steps
+        for k in range(steps):
+            trainer.prof_events = ev.ev[2 * pstep * k: 2 * pstep * (k + 1)]
+            trainer.step(*step_in)
+        torch.cuda.synchronize()
+        try:
+            ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(n)]
+        except RuntimeError:   # kernel not launched by this configuration (no events recorded)
+            ms = []
+        ev.close()
+        if not ms:
+            continue
+        r = roofline(name, ms, Ne, Nn, S, math, config, wl)
+        table[name] = {"avg_launch_ms": r["avg_launch_ms"], "ms_per_step": round(r["avg_launch_ms"] * pstep, 4),
+                       "tflops": r["achieved"], "frac": r["frac"], "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
+    trainer.prof_kernel = 0
+    trainer.prof_events = None
+    return table
 
 
 def _micro_step(trainer, batches, targets, evs, per_mb):
