@@ -290,9 +290,10 @@ static bool rebuild_dA(const spwgnn_run* r, const spwgnn_batch* b) {
     return b->nw_max <= 16 && m != MATH_F32 && !getenv_flag("SPWGNN_DA_ATOMIC");
 }
 
-// bf16 math stores the encoder-side edge arrays that only ever feed MFMA operands — z2, z3, c_r, dz4..dz1
-// and dA — as bf16 (exact: the operands are rounded to bf16 anyway). Every kernel that
-// writes or reads them must run in bf16 math for the layouts to agree.
+// bf16 math (training) stores the encoder-side edge arrays that only ever feed MFMA operands — z2, z3,
+// c_r, dz4..dz1 and dA — as bf16 (exact: the operands are rounded to bf16 anyway), and the step-invariant
+// A as bf16 (rounded once before h1 = relu(A + U + V)). Every kernel that writes or
+// reads them must run in bf16 math for the layouts to agree.
 static bool store_b16(const spwgnn_run* r, const spwgnn_batch* b) {
     return r->training && r->math == MATH_BF16 && kmath(r, kX6EncEdge) == MATH_BF16 &&
            kmath(r, kX6EncEdgeBwd) == MATH_BF16 && kmath(r, kX6Wgrad) == MATH_BF16 && rebuild_dA(r, b) &&
@@ -422,6 +423,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.H2s = c.f(w.H2s_at(s));
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
+        ef.a_b16 = store_b16(r, b);
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
         SPW_CHECK(launch_edge_fwd(ef, kmath(r, kX6EdgeFwd), st));
@@ -529,6 +531,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.RE = w.RE;
         a.RN = w.RN;
         a.S = (int)(g.rows / w.RE);
+        a.a_b16 = (g.b16 & kB16A) != 0;
     }
     // stored chunk-major operands in x6 math: the warp-specialized kernel, one workgroup per CU
     if (math != MATH_F32 && g.xmode == XM_CM && (g.ymode == YM_CM || g.ymode == YM_ROW) &&
@@ -787,6 +790,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
+        g.b16 = b16 ? kB16A : 0;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,

@@ -99,6 +99,7 @@ struct EdgeFwdArgs {
     float* H2s;
     uint32_t *mask1, *mask2;
     float* h1_out;     // training: h1 rows, chunk-major blocks (kCmBlk), for the W2 gradient
+    int a_b16;         // bf16 math (training): A stored as bf16
     const uint4* x_w2; // x6 image of W2 (half rows, kh 76) — the LDS B operand (math == MATH_X6)
 };
 
@@ -211,6 +212,7 @@ struct WgradArgs {
     const uint32_t* mask2;         // per step at s·(RE/32)·160
     int64_t RE, RN;
     int S;                         // steps (XM_H1 / YM_DH2 walk rows as (edge block, step) stages)
+    int a_b16;                     // bf16 math: A stored as bf16 (k_w2grad_ws)
     float* slab;           // [chunks][kx_pad][ny_pad]
 };
 struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 32-row blocks
@@ -224,7 +226,7 @@ struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 3
     int x_ones, pad0;
 };
 // bf16 storage of the weight gradients' edge operands (bf16 math, §3g): bit 0 X, bit 1 Y
-enum : int { kB16X = 1, kB16Y = 2 };
+enum : int { kB16X = 1, kB16Y = 2, kB16A = 4 };   // kB16A: the W2 gradient's A rows
 struct ReduceArgs {
     const float* slab;
     int chunks, kx_pad, ny_pad;

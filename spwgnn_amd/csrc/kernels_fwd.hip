@@ -266,8 +266,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // The rm encoder in split-bf16 math: two 32-edge blocks per wave (column tiles c), so each 16-byte
 // weight fragment feeds two MFMAs (the x6 images stream from L2 at half the per-MFMA rate);
 // 1 wave per SIMD (in + out activations: 320 registers).
-// B16 (bf16 math): z2, z3 and c_r — MFMA operands only (the weight gradients' X) — are stored as bf16
-// (exact, §3g); A stays fp32 (h1 = relu(A + U + V) adds it before the rounding).
+// B16 (bf16 math, training): z2, z3 and c_r — MFMA operands only (the weight gradients' X) — are
+// stored as bf16 (exact), and so is A (rounded once before h1 = relu(A + U + V) adds it; §3g).
 template <bool TRAIN, int NC, int NP = 3, bool B16 = false>
 __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_x6(EncEdgeArgs a) {
     tchain_x6<5, 10, 5, NC, kX6Ring, NP>(Y, X, a.x_w1a, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, false>(X[c], a.b_w1a, h);
-    save(a.A, nullptr, X);   // chunk-major; k_edge_fwd masks padding edges
+    save(a.A, nullptr, X, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -890,7 +890,7 @@ struct NodeSum16X6 {
 
 // Wave-tiles of ≤ 16 nodes: 8 waves (2 per SIMD, 256 registers: the 16-node sum and a one-k-block
 // ring); up to 32 nodes: 4 waves (1 per SIMD) with a 5-k-block ring.
-template <bool NW16, int DBG = 0, int NP = 3>
+template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false>   // AB16: A stored as bf16 (§3g)
 __global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? 1 : 5;
@@ -905,10 +905,10 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     const uint4* wlp = wl + lane;
     auto load_sd = [&](int blk) { return make_int2(a.esrc[(int64_t)blk * 32 + i], a.edst[(int64_t)blk * 32 + i]); };
     // a block's h1 operand sources: A rows and the gathered U[s], V[r] rows (chunk q at +256q / +64q)
-    struct Src { const float* A; const float4 *U, *V; };
+    struct Src { int64_t ai; const float4 *U, *V; };   // ai: element index of the A rows
     auto src_of = [&](int blk, int2 sd, int n0) {
         const int sc = sd.x >= 0 ? sd.x : n0, dc = sd.x >= 0 ? sd.y : n0;
-        return Src{a.A + (int64_t)(DBG == 1 ? (blk & 7) : blk) * kCmBlk + h * 128 + i * 4,
+        return Src{(int64_t)(DBG == 1 ? (blk & 7) : blk) * kCmBlk + h * 128 + i * 4,
                    reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128),
                    reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128)};
     };
@@ -918,7 +918,10 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int q = min(2 * kb + c, kKhE / 4 - 1);
-            r.a[c] = *reinterpret_cast<const float4*>(sr.A + 256 * q);
+            if constexpr (AB16)
+                r.a[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q));
+            else
+                r.a[c] = *reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
             r.u[c] = sr.U[64 * q];
             r.v[c] = sr.V[64 * q];
         }
@@ -1109,7 +1112,11 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
     if (math == MATH_BF16) {
-        if (a.nw_max <= 16)
+        if (a.nw_max <= 16 && a.a_b16)
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+        else if (a.a_b16)
+            return hipErrorInvalidValue;
+        else if (a.nw_max <= 16)
             hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((k_edge_fwd_x6<false, 0, 1>), dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);

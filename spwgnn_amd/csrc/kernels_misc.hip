@@ -537,13 +537,14 @@ constexpr int kW2gImg = 3 * X6Img<160>::PART;   // one operand's split image (30
 
 struct W2gSet {
     float4 a[5], u[5], v[5], g[5];
+    uint2 ah[5];   // A rows stored as bf16 (AB16): unpacked where they are used (build)
     uint32_t m[5];
     int in;
 };
 
 // DBG (diagnosis builds, SPWGNN_W2G_DBG): 1 no MFMAs, 2 gathers from stage 0, 4 no staging
 // arithmetic, 8 matrix waves at s_setprio 1, 32 no gathers
-template <int dbg, int NP = 3>
+template <int dbg, int NP = 3, bool AB16 = false>   // AB16: A stored as bf16 (bf16 math, §3g)
 __global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
     using IM = X6Img<160>;
@@ -635,7 +636,9 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
         stage_of(t, b, s);
         R.in = idx.x >= 0;
         const int sn = R.in ? idx.x : 0, dn = R.in ? idx.y : 0;
-        const float* pa = a.A + b * kCmBlk + rr * 4;
+        const int64_t ia = b * kCmBlk + rr * 4;
+        const float* pa = a.A + ia;
+        const uint16_t* ha = reinterpret_cast<const uint16_t*>(a.A) + ia;
         const int64_t ns = (int64_t)s * nstep_n;
         const float* pu = a.U + ns + (int64_t)(sn >> 5) * kCmBlk + (sn & 31) * 4;
         const int64_t dno = ns + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
@@ -644,7 +647,8 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
         const uint32_t* pm = a.mask2 + ((int64_t)s * nblk + b) * 160 + rr;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            R.a[k] = *reinterpret_cast<const float4*>(pa + off[k]);
+            if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(ha + off[k]);
+            else R.a[k] = *reinterpret_cast<const float4*>(pa + off[k]);
             R.u[k] = *reinterpret_cast<const float4*>(pu + off[k]);
             R.v[k] = *reinterpret_cast<const float4*>(pv + off[k]);
             R.g[k] = *reinterpret_cast<const float4*>(pg + off[k]);
@@ -657,7 +661,7 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             if (k == 4 && !k4ok) break;
-            float4 x = f4relu(f4add3(R.a[k], R.u[k], R.v[k]));
+            float4 x = f4relu(f4add3(AB16 ? unpack4_bf16(R.ah[k]) : R.a[k], R.u[k], R.v[k]));
             if (k == 4 && c0 == 5) x.z = 1.f;   // feature 150: the b2 ones column
             // dh2pre = G3 ⊙ [h2 > 0]: sign-extended single-bit fields as AND masks
             const int w = (int)(R.in ? R.m[k] : 0u);
@@ -1082,9 +1086,11 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
 #endif
     const dim3 g(wgs), b(kW2gThreads);
     if (math == MATH_BF16) {
-        hipLaunchKernelGGL((k_w2grad_ws<0, 1>), g, b, 0, st, a, blk_per_wg);
+        if (a.a_b16) hipLaunchKernelGGL((k_w2grad_ws<0, 1, true>), g, b, 0, st, a, blk_per_wg);
+        else hipLaunchKernelGGL((k_w2grad_ws<0, 1>), g, b, 0, st, a, blk_per_wg);
         return hipGetLastError();
     }
+    if (a.a_b16) return hipErrorInvalidValue;
     if (dbg == 0) {
         hipLaunchKernelGGL(k_w2grad_ws<0>, g, b, 0, st, a, blk_per_wg);
         return hipGetLastError();
