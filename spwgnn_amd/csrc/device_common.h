@@ -47,10 +47,14 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 __device__ __forceinline__ float bf16_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 // (a, b) → three packed bf16 pairs h, m, l (element 0 = a in the low half)
+// The empty asm hides where h and m came from: otherwise the compiler rebuilds bf16_lo(h) as a
+// second v_cvt_pk_bf16_f32 of `a` alone plus the shift (13 VALU per pair instead of 11).
 __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
     h = pk_bf16(a, b);
+    asm("" : "+v"(h));
     const float ra = a - bf16_lo(h), rb = b - bf16_hi(h);
     m = pk_bf16(ra, rb);
+    asm("" : "+v"(m));
     l = pk_bf16(ra - bf16_lo(m), rb - bf16_hi(m));
 }
 __device__ __forceinline__ bf16x8 as_bf16x8(i16x4 lo, i16x4 hi) {
