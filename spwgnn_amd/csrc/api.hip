@@ -41,7 +41,7 @@ struct Ws {
     int64_t a_at(int s) const { return a + (int64_t)s * RN * kRowN; }
     int64_t o1_at(int s) const { return o1 + (int64_t)s * RN * kRowN; }
     int64_t m1_at(int s) const { return mask1 + (int64_t)s * NB * kLdE; }
-    int64_t m2_at(int s) const { return mask2 + (int64_t)s * NB * 160; }
+    int64_t m2_at(int s) const { return mask2 + (int64_t)s * NB * kM2Blk; }
     int64_t dx_at(int s) const { return dx + (int64_t)s * RN * kRowN; }
     int64_t do1_at(int s) const { return do1 + (int64_t)s * RN * kRowN; }
     int64_t g_at(int s) const { return g + (int64_t)s * RN * kRowN; }
@@ -117,7 +117,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         w.cr = take(eCM);
         w.mask1 = take(w.NB * kLdE * S);
         w.zmask = take(w.NB * 4 * 3 * 64);
-        w.mask2 = take(w.NB * 160 * S);
+        w.mask2 = take(w.NB * kM2Blk * S);
         w.dx = take(nN * S);
         w.do1 = take(nN * S);
         w.g = take(nN * S);

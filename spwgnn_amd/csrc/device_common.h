@@ -106,6 +106,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+// tanh(x) = 1 − 2/(2^(2x·log2 e) + 1) on the transcendental unit (v_exp_f32, v_rcp_f32): 5
+// instructions instead of libm tanhf's ≈ 22 (two thirds of the node forward's non-split VALU).
+// Absolute error ≤ 4.2e-7 (libm: 6e-8) — the size of the split-bf16 products' own error (§3b);
+// ±1 at ±∞, NaN propagates. Used by the split-bf16 node forward; f32 math keeps tanhf.
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+    return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
 // The 2-input first Dense of the encoders with one explicit rounding order: left to the compiler,
 // unrolled copies of x0·w0 + x1·w1 + b were contracted / paired differently, so an edge's value
 // depended on which copy (column tile) processed it.

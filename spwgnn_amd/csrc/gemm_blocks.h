@@ -112,6 +112,23 @@ __device__ __forceinline__ void store_cm_b16(uint16_t* __restrict__ blk, const f
         }
 }
 
+// ---- h2 > 0 bits (mask2) of one 32-edge block: kM2Blk words, [edge][8]; word t < 5 holds the bits
+// of features 32t .. 32t+31 (bit = feature within the tile), words 5..7 are zero padding — an edge's
+// five words are one 16-byte + one 4-byte load.
+constexpr int kM2Blk = 256;
+__device__ __forceinline__ void load_m2(const uint32_t* __restrict__ blk_words, int edge, uint32_t (&w)[5]) {
+    const uint32_t* p = blk_words + edge * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    w[0] = v.x;
+    w[1] = v.y;
+    w[2] = v.z;
+    w[3] = v.w;
+    w[4] = p[4];
+}
+// writer side: word (edge, t) lives in register (8·edge + t) >> 6, lane (8·edge + t) & 63 of the
+// four-register image that k_edge_fwd stores with one full-wave store per register
+__host__ __device__ __forceinline__ constexpr int m2_pos(int edge, int t) { return 8 * edge + t; }
+
 // split-halves chunk of a chunk-major row: x[s] = feature KH·h + s of row j
 template <int KH>
 __device__ __forceinline__ void load_half_cm(const float* __restrict__ blk, int lane, float (&x)[KH]) {

@@ -209,7 +209,7 @@ struct WgradArgs {
     const float* pos;
     const int32_t *esrc, *edst;
     const float *A, *U, *V, *G3;   // chunk-major; U, V, G3 per step at s·RN·kRowE
-    const uint32_t* mask2;         // per step at s·(RE/32)·160
+    const uint32_t* mask2;         // per step at s·(RE/32)·kM2Blk
     int64_t RE, RN;
     int S;                         // steps (XM_H1 / YM_DH2 walk rows as (edge block, step) stages)
     int a_b16;                     // bf16 math: A stored as bf16 (k_w2grad_ws)

@@ -319,9 +319,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
         const int64_t e = (int64_t)blk * 32 + i;
         p.d = a.edst[e];
         p.s = a.esrc[e];
-        const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
-#pragma unroll
-        for (int t = 0; t < 5; ++t) p.w[t] = m2[32 * t];
+        load_m2(a.mask2 + (int64_t)blk * kM2Blk, i, p.w);
         return p;
     };
     int wt = ONEHOT ? blockIdx.x * kEdgeWaves + wave : blockIdx.x * a.wpg + wave;
@@ -659,9 +657,12 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 // dh1pre = dh1 ⊙ [h1 > 0] goes to dA (plain stores on the first backward step, atomics after)
 // and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
 // 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
+#ifndef SPWGNN_EBWD_PF
+#define SPWGNN_EBWD_PF 2
+#endif
 template <bool ACCUM, bool NODA = false, int NP = 3>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
-    constexpr int PF = 1, kWaves = 8;
+    constexpr int PF = SPWGNN_EBWD_PF, kWaves = 8;
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
     for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2t[idx];
     __syncthreads();
@@ -676,9 +677,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const int64_t e = (int64_t)blk * 32 + i;
         p.d = a.edst[e];
         p.s = a.esrc[e];
-        const uint32_t* m2 = a.mask2 + (int64_t)blk * 160 + i;
-#pragma unroll
-        for (int t = 0; t < 5; ++t) p.w[t] = m2[32 * t];
+        load_m2(a.mask2 + (int64_t)blk * kM2Blk, i, p.w);
         return p;
     };
     auto g_of = [&](int d, int n0) {
@@ -711,9 +710,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const int d = cur.d;
         const bool valid = d >= 0;
         const uint32_t* m1 = a.mask1 + (int64_t)blk * kLdE + i;
-        uint32_t m1w[5];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) m1w[t] = m1[32 * t];
+        uint32_t m1w[5];   // loaded a few k-blocks before the dh1pre masking uses them
         uint32_t w[5];
 #pragma unroll
         for (int t = 0; t < 5; ++t) w[t] = valid ? cur.w[t] : 0u;
@@ -726,6 +723,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         zero_tiles(acc);
 #pragma unroll
         for (int kb = 0; kb < 10; ++kb) {
+            if (kb == 7) {
+#pragma unroll
+                for (int t = 0; t < 5; ++t) m1w[t] = m1[32 * t];
+            }
             KB& cr = ring[kb % PF];
             float xv[8];
 #pragma unroll
@@ -894,11 +895,11 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         Pair p;
         const bool valid = d >= 0;
         p.G4 = reinterpret_cast<const float4*>(a.G3 + s * a.g3_step + cm_index<kKhE>(valid ? d : 0, 0) + h * 128);
-        const uint32_t* m2 = a.mask2 + s * a.m2_step + (int64_t)blk * 160 + i;
         const uint32_t* m1 = a.mask1 + s * a.m1_step + (int64_t)blk * kLdE + i;
+        load_m2(a.mask2 + s * a.m2_step + (int64_t)blk * kM2Blk, i, p.w);
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-            p.w[t] = valid ? m2[32 * t] : 0u;
+            p.w[t] = valid ? p.w[t] : 0u;
             p.m1w[t] = m1[32 * t];
         }
         return p;

@@ -544,20 +544,19 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
         }
         if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
-            uint32_t* m2row = a.mask2 + (int64_t)blk * 160;
-            uint32_t mw[3] = {0u, 0u, 0u};
+            uint32_t* m2row = a.mask2 + (int64_t)blk * kM2Blk;
+            uint32_t mw[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int t = 0; t < 5; ++t)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const uint64_t bal = __ballot(acc[t][r] > 0.f);
-                    const int w0 = t * 32 + rho(r, 0), w1 = t * 32 + rho(r, 1);
+                    const int w0 = m2_pos(rho(r, 0), t), w1 = m2_pos(rho(r, 1), t);
                     mw[w0 >> 6] = writelane_imm((uint32_t)bal, w0 & 63, mw[w0 >> 6]);
                     mw[w1 >> 6] = writelane_imm((uint32_t)(bal >> 32), w1 & 63, mw[w1 >> 6]);
                 }
-            m2row[lane] = mw[0];
-            m2row[64 + lane] = mw[1];
-            if (lane < 32) m2row[128 + lane] = mw[2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = mw[k];
         }
         nsum.add(acc, d);
     }
@@ -682,7 +681,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = rho(r, 0) + 4 * h + 32 * t;
-                E[c][t][r] = f < kFN ? tanhf(E[c][t][r]) : 0.f;
+                E[c][t][r] = f < kFN ? fast_tanh(E[c][t][r]) : 0.f;
             }
         if (a.a_out && has[c]) store_cm<4>(a.a_out + bN(c), E[c], lane, valid[c]);
     }
@@ -731,7 +730,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = rho(r, 0) + 4 * h + 32 * t;
-                X[c][t][r] = f < kFN ? tanhf(X[c][t][r] + P[t][r]) : 0.f;   // X := P'
+                X[c][t][r] = f < kFN ? fast_tanh(X[c][t][r] + P[t][r]) : 0.f;   // X := P'
             }
         if (has[c]) store_cm<4>(a.Pn + bN(c), X[c], lane, valid[c]);
     }
@@ -890,10 +889,13 @@ struct NodeSum16X6 {
 
 // Wave-tiles of ≤ 16 nodes: 8 waves (2 per SIMD, 256 registers: the 16-node sum and a one-k-block
 // ring); up to 32 nodes: 4 waves (1 per SIMD) with a 5-k-block ring.
+#ifndef SPWGNN_EFWD_PF
+#define SPWGNN_EFWD_PF 1
+#endif
 template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false>   // AB16: A stored as bf16 (§3g)
 __global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
-    constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? 1 : 5;
+    constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? SPWGNN_EFWD_PF : 5;
     static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
     __shared__ uint4 wl[50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
     for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
@@ -1023,8 +1025,8 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             }
         }
         if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
-            uint32_t* m2row = a.mask2 + (int64_t)blk * 160;
-            uint32_t mw2[3] = {0u, 0u, 0u};
+            uint32_t* m2row = a.mask2 + (int64_t)blk * kM2Blk;
+            uint32_t mw2[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int t = 0; t < 5; ++t)
 #pragma unroll
@@ -1035,15 +1037,14 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
-                        const int w0 = t * 32 + rho(r0 + r, 0), w1 = t * 32 + rho(r0 + r, 1);
+                        const int w0 = m2_pos(rho(r0 + r, 0), t), w1 = m2_pos(rho(r0 + r, 1), t);
                         mw2[w0 >> 6] = writelane_imm_batched((uint32_t)bal[r], w0 & 63, mw2[w0 >> 6]);
                         mw2[w1 >> 6] = writelane_imm_batched((uint32_t)(bal[r] >> 32), w1 & 63, mw2[w1 >> 6]);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-            m2row[lane] = mw2[0];
-            m2row[64 + lane] = mw2[1];
-            if (lane < 32) m2row[128 + lane] = mw2[2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = mw2[k];
         }
         nsum.add(acc, d, NW16 ? lane : h);
         cur_sd = nsd;

@@ -230,13 +230,13 @@ struct EdgeStage {
                 rv[k] = *reinterpret_cast<const float4*>(pv + o);
             }
         } else {
-            const uint32_t* pm = a.mask2 + (s * (a.RE >> 5) + (e >> 5)) * 160 + rr;
+            const uint32_t* pm = a.mask2 + (s * (a.RE >> 5) + (e >> 5)) * kM2Blk + rr * 8;
             const int c0 = tid >> 5;
 #pragma unroll
             for (int k = 0; k < NG; ++k) {
                 const int o = off[k] < 0 ? 0 : off[k];
                 ru[k] = *reinterpret_cast<const float4*>(pu + o);
-                mw[k] = pm[((4 * (c0 + 8 * k)) >> 5) * 32];   // word (tile of f0, edge rr)
+                mw[k] = pm[(4 * (c0 + 8 * k)) >> 5];   // word (edge rr, tile of f0)
             }
         }
     }
@@ -644,7 +644,8 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
         const int64_t dno = ns + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
         const float* pv = a.V + dno;
         const float* pg = a.G3 + dno;
-        const uint32_t* pm = a.mask2 + ((int64_t)s * nblk + b) * 160 + rr;
+        uint32_t mw[5];
+        load_m2(a.mask2 + ((int64_t)s * nblk + b) * kM2Blk, rr, mw);
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(ha + off[k]);
@@ -652,7 +653,7 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
             R.u[k] = *reinterpret_cast<const float4*>(pu + off[k]);
             R.v[k] = *reinterpret_cast<const float4*>(pv + off[k]);
             R.g[k] = *reinterpret_cast<const float4*>(pg + off[k]);
-            R.m[k] = pm[k * 32];
+            R.m[k] = mw[k];
         }
     };
     auto build = [&](const W2gSet& R, char* Xs) {
