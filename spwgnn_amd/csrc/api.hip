@@ -749,7 +749,11 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     enb.dzo2 = c.f(w.dzo2);
     enb.dzo1 = c.f(w.dzo1);
     enb.scale = scale;
-    SPW_CHECK(launch_enc_node_bwd(enb, st));
+    if (kmath(r, kX6NodeBwd) != MATH_F32) {
+        enb.x_wo1ct = c.x6(X6_WO1CT);
+        enb.x_om1t = c.x6(X6_OM1T);
+    }
+    SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), st));
 
     // ---- weight gradients ----
     const int64_t RE = w.RE, RN = w.RN;

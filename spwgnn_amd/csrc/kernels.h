@@ -32,6 +32,7 @@ enum X6Id : int {
     X6_W3A, X6_WO1C, X6_WO1A, X6_WO1P, X6_WO2, X6_W1B, X6_W1C,   // node side
     X6_W1BT, X6_W1CT, X6_WO2T, X6_WO1PT, X6_WO1CT, X6_WO1AT, X6_W3T,   // its backward
     X6_OM1,                                       // object encoder
+    X6_OM1T,                                      // its backward
     X6_COUNT
 };
 // (image, fp32 pack, output tiles, k-blocks, kh) — the images every x6 run builds
@@ -46,6 +47,7 @@ constexpr X6Spec kX6Specs[X6_COUNT] = {
     {X6_W1BT, PK_W1BT, 4, 10, kKhE}, {X6_W1CT, PK_W1CT, 4, 10, kKhE}, {X6_WO2T, PK_WO2T, 4, 7, 0},
     {X6_WO1PT, PK_WO1PT, 4, 7, 0}, {X6_WO1CT, PK_WO1CT, 4, 7, 0}, {X6_WO1AT, PK_WO1AT, 4, 7, 0},
     {X6_W3T, PK_W3T, 5, 7, 0},     {X6_OM1, PK_OM1, 4, 7, 0},
+    {X6_OM1T, PK_OM1T, 4, 7, 0},
 };
 struct X6Desc {
     const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
@@ -177,6 +179,7 @@ struct EncNodeBwdArgs {
     int S;
     float *dzo2, *dzo1;
     float scale;
+    const uint4 *x_wo1ct, *x_om1t;    // split-bf16 maths: x6 images of Wo1cᵀ and om.1ᵀ
 };
 
 // ---- weight gradients: dW = Σ_rows X[row]ᵀ·Y[row] (deterministic split-row slabs) ----
@@ -269,7 +272,7 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st);
-hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st);
+hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, int math, hipStream_t st);
 enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1, MATH_BF16 = 2 };   // = SPWGNN_MATH_* (spwgnn.h)
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,

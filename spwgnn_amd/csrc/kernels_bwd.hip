@@ -1016,8 +1016,62 @@ hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st
     hipLaunchKernelGGL(k_enc_edge_bwd, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
-hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, hipStream_t st) {
+// The om encoder's backward in split-bf16 math: k_enc_node_bwd's two 100×100 products (Σ_s do1_s ·
+// Wo1cᵀ and om.1ᵀ) on tchain_x6 instead of the f32 matrix core (one 32-node column tile per wave, two
+// waves per SIMD, as k_enc_node_x6).
+template <int NP>
+__global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nb * 32 >= a.n_nodes) return;
+    const int n = nb * 32 + j;
+    const bool valid = n < a.n_nodes;
+    const int64_t bN = (int64_t)nb * kCmBlkN;   // chunk-major node block
+    f32x16 D[1][4], E[1][4], Z[4];
+    // Σ_s do1_s in backward step order S-1..0 (the Y of the Wo1c weight gradient)
+    load_cm<4>(a.do1 + (int64_t)(a.S - 1) * a.do1_step + bN, E[0], lane);
+    for (int s = a.S - 2; s >= 0; --s) {
+        load_cm<4>(a.do1 + (int64_t)s * a.do1_step + bN, Z, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) E[0][t] += Z[t];
+    }
+    store_cm<4>(a.dco + bN, E[0], lane, valid);
+    zero_tiles(D[0]);
+    tchain_x6<4, 7, 4, 1, kX6Ring, NP>(E, D, a.x_wo1ct, lane);   // dc_o = (Σ_s do1_s)·Wo1cᵀ
+    load_cm<4>(a.co + bN, Z, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) D[0][t][r] = Z[t][r] > 0.f ? D[0][t][r] * a.scale : 0.f;
+    store_cm<4>(a.dzo2 + bN, D[0], lane, valid);
+    zero_tiles(E[0]);
+    tchain_x6<4, 7, 4, 1, kX6Ring, NP>(D, E, a.x_om1t, lane);
+    if (a.zo1) {
+        load_cm<4>(a.zo1 + bN, Z, lane);
+    } else {   // the forward's own first-layer arithmetic (k_enc_node_x6), not a stored row
+        const float4 p = reinterpret_cast<const float4*>(a.pos)[valid ? n : a.n_nodes - 1];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                Z[t][r] = relu(dense2(p.y, p.z, a.w_om0[f], a.w_om0[128 + f], a.b_om0[f]));
+            }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) E[0][t][r] = Z[t][r] > 0.f ? E[0][t][r] : 0.f;
+    store_cm<4>(a.dzo1 + bN, E[0], lane, valid);
+}
+
+hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
+    if (math != MATH_F32 && a.wo1ct && a.x_wo1ct && a.x_om1t) {
+        if (math == MATH_BF16) hipLaunchKernelGGL(k_enc_node_bwd_x6<1>, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_enc_node_bwd_x6<3>, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_enc_node_bwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
