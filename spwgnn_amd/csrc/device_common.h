@@ -106,6 +106,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+// g if bit f of bits is set, else +0: a sign-extended one-bit field as an AND mask (v_bfe_i32 +
+// v_and_b32; written as a select the compiler emits and + compare + cndmask)
+__device__ __forceinline__ float mask_bit(float g, uint32_t bits, int f) {
+    return __uint_as_float(__float_as_uint(g) & (uint32_t)__builtin_amdgcn_sbfe((int)bits, f, 1));
+}
 // tanh(x) = 1 − 2/(2^(2x·log2 e) + 1) on the transcendental unit (v_exp_f32, v_rcp_f32): 5
 // instructions instead of libm tanhf's ≈ 22 (two thirds of the node forward's non-split VALU).
 // Absolute error ≤ 4.2e-7 (libm: 6e-8) — the size of the split-bf16 products' own error (§3b);

@@ -171,7 +171,7 @@ __device__ __forceinline__ void apply_pos_bits(const uint32_t* __restrict__ word
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-            X[t][r] = ((w[(16 * t + r) >> 5] >> ((16 * t + r) & 31)) & 1u) ? X[t][r] * scale : 0.f;
+            X[t][r] = mask_bit(X[t][r] * scale, w[(16 * t + r) >> 5], (16 * t + r) & 31);
 }
 
 // ---- split-halves row chunk: lane half h holds features [KH*h, KH*h+KH) of its row.

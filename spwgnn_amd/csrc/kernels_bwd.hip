@@ -733,10 +733,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int c = 0; c < 2; ++c) {
                 const int q = 2 * kb + c;
                 const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
-                xv[4 * c + 0] = (bits & 1u) ? cr.g[c].x : 0.f;
-                xv[4 * c + 1] = (bits & 2u) ? cr.g[c].y : 0.f;
-                xv[4 * c + 2] = (bits & 4u) ? cr.g[c].z : 0.f;
-                xv[4 * c + 3] = (bits & 8u) ? cr.g[c].w : 0.f;
+                xv[4 * c + 0] = mask_bit(cr.g[c].x, bits, 0);
+                xv[4 * c + 1] = mask_bit(cr.g[c].y, bits, 1);
+                xv[4 * c + 2] = mask_bit(cr.g[c].z, bits, 2);
+                xv[4 * c + 3] = mask_bit(cr.g[c].w, bits, 3);
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
@@ -765,9 +765,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32t+i, rows = edges rho(r,h))
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-            const uint32_t mw1 = m1w[t];
+            const uint32_t mh = m1w[t] >> (4 * h);   // bit rho(r, 0) = edge rho(r, h)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][r] = ((mw1 >> rho(r, h)) & 1u) ? acc[t][r] : 0.f;
+            for (int r = 0; r < 16; ++r) acc[t][r] = mask_bit(acc[t][r], mh, rho(r, 0));
         }
         float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
         // one-hot [node row][edge]: element e of half h ↔ edge rho(8s + e, h)
@@ -938,10 +938,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int c = 0; c < 2; ++c) {
                 const int q = 2 * kb + c;
                 const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
-                xv[4 * c + 0] = (bits & 1u) ? cr.g[c].x : 0.f;
-                xv[4 * c + 1] = (bits & 2u) ? cr.g[c].y : 0.f;
-                xv[4 * c + 2] = (bits & 4u) ? cr.g[c].z : 0.f;
-                xv[4 * c + 3] = (bits & 8u) ? cr.g[c].w : 0.f;
+                xv[4 * c + 0] = mask_bit(cr.g[c].x, bits, 0);
+                xv[4 * c + 1] = mask_bit(cr.g[c].y, bits, 1);
+                xv[4 * c + 2] = mask_bit(cr.g[c].z, bits, 2);
+                xv[4 * c + 3] = mask_bit(cr.g[c].w, bits, 3);
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
@@ -965,9 +965,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         }
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-            const uint32_t mw1 = cur.m1w[t];
+            const uint32_t mh = cur.m1w[t] >> (4 * h);   // bit rho(r, 0) = edge rho(r, h)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) dacc[t][r] += ((mw1 >> rho(r, h)) & 1u) ? acc[t][r] : 0.f;
+            for (int r = 0; r < 16; ++r) dacc[t][r] += mask_bit(acc[t][r], mh, rho(r, 0));
         }
         if (last_step) {   // the block's S steps are summed: one plain store of its dA rows
             if constexpr (B16) {   // bf16 math: dA feeds MFMA operands only (§3g)
