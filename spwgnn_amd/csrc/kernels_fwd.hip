@@ -1013,6 +1013,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             }
         }
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
+        const uint32_t vh = (uint32_t)vmask >> (4 * h);   // bit rho(r, 0): edge rho(r, h) is real
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const float b = a.b2[32 * t + i];
@@ -1020,8 +1021,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             for (int r = 0; r < 16; ++r) {
                 float v = relu(acc[t][r] + b);
                 if (t == 4 && i == kDegCol - 128) v = 1.f;  // degree column (multiplies b3)
-                const bool rv = (vmask >> (rho(r, 0) + 4 * h)) & 1;
-                acc[t][r] = rv ? v : 0.f;
+                acc[t][r] = mask_bit(v, vh, rho(r, 0));
             }
         }
         if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
