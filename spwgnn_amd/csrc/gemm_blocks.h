@@ -323,6 +323,22 @@ __device__ __forceinline__ void ngemm_acc(const float (&a)[KH], f32x16 (&acc)[NT
 // kernels: wl[col * kWlK + k] = W[k][col], k < 152 (the two 76-feature halves). A lane's 4
 // consecutive k of one column are one ds_read_b128; kWlK ≡ 28 (mod 32) keeps 8 consecutive
 // lanes on distinct 4-bank groups.
+// The x6 W2 / W2ᵀ LDS images (50 steps × 3 parts × 64 lanes uint4 = 150 KB) reach past ds_read's
+// 16-bit byte offset. Fragment idx (uint4 units, lane included in the base) is read from one of three
+// bases 64 KB apart, each in its own register: the opaque offsets keep the compiler from rebuilding
+// every address beyond 64 KB with a v_or (≈ 10 VALU per k-block).
+struct WlBases {
+    const uint4* b[3];
+    __device__ __forceinline__ explicit WlBases(const uint4* wlp) {
+        int o1 = 4096, o2 = 8192;
+        asm("" : "+v"(o1));
+        asm("" : "+v"(o2));
+        b[0] = wlp;
+        b[1] = wlp + o1;
+        b[2] = wlp + o2;
+    }
+    __device__ __forceinline__ uint4 at(int idx) const { return b[idx >> 12][idx & 4095]; }
+};
 constexpr int kWlK = 156;
 constexpr int kWlFloats = 160 * kWlK;
 constexpr int kEdgeWaves = 8;   // waves per edge workgroup (one workgroup per CU: 97.5 KiB of LDS)

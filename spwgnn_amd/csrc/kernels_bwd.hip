@@ -670,7 +670,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
     const int wstep = gridDim.x * kWaves;
-    const uint4* wlp = wl + lane;
+    const WlBases wlb(wl + lane);
     struct Pre { int d, s; uint32_t w[5]; };
     auto load_pre = [&](int blk) {
         Pre p;
@@ -753,11 +753,11 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
 #pragma unroll
             for (int T = 0; T < 5; ++T) {
-                const uint4* wp = wlp + (kb * 5 + T) * 3 * 64;
+                const int u = (kb * 5 + T) * 3 * 64;
                 bf16x8 bp[3];
-                bp[0] = as_bf16x8(wp[0]);
-                bp[1] = as_bf16x8(wp[64]);
-                bp[2] = as_bf16x8(wp[128]);
+                bp[0] = as_bf16x8(wlb.at(u));
+                bp[1] = as_bf16x8(wlb.at(u + 64));
+                bp[2] = as_bf16x8(wlb.at(u + 128));
                 acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
             }
             __builtin_amdgcn_sched_barrier(0);   // no motion across k-blocks (register pressure)
@@ -883,7 +883,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     __syncthreads();
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint4* wlp = wl + lane;
+    const WlBases wlb(wl + lane);
     // a contiguous range of blocks per wave: a tower's blocks (same receiver rows) stay on one CU
     const int nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wave;
     const int per = (a.n_eblocks + nw - 1) / nw;
@@ -954,11 +954,11 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
 #pragma unroll
             for (int T = 0; T < 5; ++T) {
-                const uint4* wp = wlp + (kb * 5 + T) * 3 * 64;
+                const int u = (kb * 5 + T) * 3 * 64;
                 bf16x8 bp[3];
-                bp[0] = as_bf16x8(wp[0]);
-                bp[1] = as_bf16x8(wp[64]);
-                bp[2] = as_bf16x8(wp[128]);
+                bp[0] = as_bf16x8(wlb.at(u));
+                bp[1] = as_bf16x8(wlb.at(u + 64));
+                bp[2] = as_bf16x8(wlb.at(u + 128));
                 acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
             }
             __builtin_amdgcn_sched_barrier(0);

@@ -904,7 +904,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
     const int wstep = gridDim.x * kWaves;
-    const uint4* wlp = wl + lane;
+    const WlBases wlb(wl + lane);
     auto load_sd = [&](int blk) { return make_int2(a.esrc[(int64_t)blk * 32 + i], a.edst[(int64_t)blk * 32 + i]); };
     // a block's h1 operand sources: A rows and the gathered U[s], V[r] rows (chunk q at +256q / +64q)
     struct Src { int64_t ai; const float4 *U, *V; };   // ai: element index of the A rows
@@ -1004,11 +1004,11 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             }
 #pragma unroll
             for (int T = 0; T < 5; ++T) {
-                const uint4* wp = wlp + (kb * 5 + T) * 3 * 64;
+                const int u = (kb * 5 + T) * 3 * 64;
                 bf16x8 bp[3];
-                bp[0] = as_bf16x8(wp[0]);
-                bp[1] = as_bf16x8(wp[64]);
-                bp[2] = as_bf16x8(wp[128]);
+                bp[0] = as_bf16x8(wlb.at(u));
+                bp[1] = as_bf16x8(wlb.at(u + 64));
+                bp[2] = as_bf16x8(wlb.at(u + 128));
                 acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
             }
         }
