@@ -84,6 +84,24 @@ __device__ __forceinline__ f32x16 mfma32_x6(const bf16x8 (&a)[3], const bf16x8 (
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
 }
+// The six products of NT output tiles interleaved (product p for every tile before product p+1):
+// consecutive MFMAs write different accumulators, which the matrix pipe overlaps better than one
+// tile's chain of six (measured, tools/mb/x6dep.hip: 0.77 -> 0.80 of the bf16 peak at two waves per
+// SIMD with LDS-fed fragments). Same products and per-accumulator order as mfma32_x6: bit-identical.
+template <int NP, int NT>
+__device__ __forceinline__ void mfma32_x6_group(const bf16x8 (&a)[3], const bf16x8 (&b)[NT][3], f32x16* acc) {
+    if constexpr (NP == 1) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[u][0], acc[u], 0, 0, 0);
+    } else {
+        constexpr int pa[6] = {2, 0, 1, 1, 0, 0}, pb[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+            for (int u = 0; u < NT; ++u)
+                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa[p]], b[u][pb[p]], acc[u], 0, 0, 0);
+    }
+}
 // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, 16-bit columns 4p..4p+3 of a
 // 4×16 block; lane i of the group receives column i of the 4 rows (row q in element q)
 __device__ __forceinline__ i16x4 lds_tr16(const char* p) {

@@ -752,7 +752,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
             ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
 #pragma unroll
-            for (int T = 0; T < 5; ++T) {
+            for (int T = 0; T < 5; ++T) {   // (interleaved tile groups as in k_dA_x6 spill here: 0.615 -> 0.637 ms)
                 const int u = (kb * 5 + T) * 3 * 64;
                 bf16x8 bp[3];
                 bp[0] = as_bf16x8(wlb.at(u));
@@ -952,15 +952,20 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
             ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
             ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+            // output tiles in groups {0, 1}, {2, 3, 4}, products interleaved within a group
+            auto group = [&](auto NTc, int T0) {
+                constexpr int NT = decltype(NTc)::value;
+                bf16x8 bp[NT][3];
 #pragma unroll
-            for (int T = 0; T < 5; ++T) {
-                const int u = (kb * 5 + T) * 3 * 64;
-                bf16x8 bp[3];
-                bp[0] = as_bf16x8(wlb.at(u));
-                bp[1] = as_bf16x8(wlb.at(u + 64));
-                bp[2] = as_bf16x8(wlb.at(u + 128));
-                acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
-            }
+                for (int v = 0; v < NT; ++v) {
+                    const int u = (kb * 5 + T0 + v) * 3 * 64;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) bp[v][p] = as_bf16x8(wlb.at(u + 64 * p));
+                }
+                mfma32_x6_group<NP, NT>(ap, bp, acc + T0);
+            };
+            group(std::integral_constant<int, 2>{}, 0);
+            group(std::integral_constant<int, 3>{}, 2);
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll

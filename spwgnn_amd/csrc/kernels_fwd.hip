@@ -1002,15 +1002,20 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                     }
                 }
             }
+            // output tiles in groups {0, 1}, {2, 3, 4}, products interleaved within a group
+            auto group = [&](auto NTc, int T0) {
+                constexpr int NT = decltype(NTc)::value;
+                bf16x8 bp[NT][3];
 #pragma unroll
-            for (int T = 0; T < 5; ++T) {
-                const int u = (kb * 5 + T) * 3 * 64;
-                bf16x8 bp[3];
-                bp[0] = as_bf16x8(wlb.at(u));
-                bp[1] = as_bf16x8(wlb.at(u + 64));
-                bp[2] = as_bf16x8(wlb.at(u + 128));
-                acc[T] = mfma32_x6<NP>(ap, bp, acc[T]);
-            }
+                for (int v = 0; v < NT; ++v) {
+                    const int u = (kb * 5 + T0 + v) * 3 * 64;
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) bp[v][q] = as_bf16x8(wlb.at(u + 64 * q));
+                }
+                mfma32_x6_group<NP, NT>(ap, bp, acc + T0);
+            };
+            group(std::integral_constant<int, 2>{}, 0);
+            group(std::integral_constant<int, 3>{}, 2);
         }
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
         const uint32_t vh = (uint32_t)vmask >> (4 * h);   // bit rho(r, 0): edge rho(r, h) is real
