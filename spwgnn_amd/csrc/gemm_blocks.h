@@ -423,6 +423,97 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
         for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6<PARTS>(a, bq[c], out[c][T]);
     }
 }
+// ---- the same product with the weight image shared by the NW waves of a workgroup through LDS.
+// Every wave of the workgroup calls the same tgemm_x6_wg sequence (no early exit: a wave with no
+// rows of its own runs on clamped rows and stores nothing), so the image streams from L2 once per
+// workgroup instead of once per wave: k-block kb's slice (NT_OUT steps × 3 parts × 1 KiB) is
+// DMA'd (global_load_lds, 1 KiB per wave-instruction, the NW waves' pieces interleaved) into LDS
+// slot kb % 3 one k-block ahead of use. One barrier per k-block, at its last step: it certifies
+// that slice kb+1 has landed (each wave's vmcnt(0) before it) and that every wave is done with
+// slot (kb−1) % 3, which then receives slice kb+2. Fragments are read one step ahead from LDS.
+// lds: kWgSlot·3 uint4 (the workgroup's only __shared__ object besides what the caller owns).
+constexpr int kWgSlot = 15 * 64;   // uint4 per slot: NT_OUT ≤ 5 steps × 3 parts × 64 lanes
+template <int NW>
+struct WgRing {
+    uint4* lds;
+    int wid;   // wave index in the workgroup (wave-uniform)
+};
+template <int NT_OUT, int NKB, int NC, int NW, int PARTS = 3, class GetB>
+__device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
+                                            int lane, const WgRing<NW>& wr) {
+    static_assert(NT_OUT * 3 * 64 <= kWgSlot, "slot size");
+    constexpr int NS = NKB * NT_OUT, NP = 4 * NC;
+    constexpr int PCS = NT_OUT * 3, PPW = (PCS + NW - 1) / NW;   // 1-KiB pieces per slice, per wave
+    auto issue = [&](int kbl) {
+#pragma unroll
+        for (int q = 0; q < PPW; ++q) {
+            const int i = min(wr.wid + NW * q, PCS - 1);   // the last pieces may be loaded twice (same bytes)
+            __builtin_amdgcn_global_load_lds(img + (kbl * PCS + i) * 64 + lane, wr.lds + ((kbl % 3) * kWgSlot + i * 64), 16, 0, 0);
+        }
+    };
+    const uint4* rl = wr.lds + lane;
+    auto frag = [&](int u, uint4 (&f)[3]) {
+        const int kb = u / NT_OUT, T = u - kb * NT_OUT;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) f[p] = rl[(kb % 3) * kWgSlot + (T * 3 + p) * 64];
+    };
+    __builtin_amdgcn_s_barrier();   // every wave is done with the previous call's slots
+    issue(0);
+    if (NKB > 1) issue(1);
+    uint32_t sp[2][NC][3][4];
+    auto split_pair = [&](int kb, int q) {
+        const int c = q >> 2, m = q & 3;
+        float v[8];
+        getb(c, kb, v);
+        split2(v[2 * m], v[2 * m + 1], sp[kb & 1][c][0][m], sp[kb & 1][c][1][m], sp[kb & 1][c][2][m]);
+    };
+#pragma unroll
+    for (int q = 0; q < NP; ++q) split_pair(0, q);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    uint4 fr[2][3];
+    frag(0, fr[0]);
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        const int kb = u / NT_OUT, T = u - kb * NT_OUT;
+        bf16x8 bq[NC][3];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                bq[c][p] = as_bf16x8(make_uint4(sp[kb & 1][c][p][0], sp[kb & 1][c][p][1], sp[kb & 1][c][p][2], sp[kb & 1][c][p][3]));
+        bf16x8 a[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = as_bf16x8(fr[u & 1][p]);
+        if (u + 1 < NS) {
+            if (T == NT_OUT - 1) {   // slice kb+1 landed, slot (kb−1)%3 free on every wave
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (kb + 2 < NKB) issue(kb + 2);
+            }
+            frag(u + 1, fr[(u + 1) & 1]);
+        }
+        if (kb + 1 < NKB) {
+#pragma unroll
+            for (int q = NP * T / NT_OUT; q < NP * (T + 1) / NT_OUT; ++q) split_pair(kb + 1, q);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6<PARTS>(a, bq[c], out[c][T]);
+    }
+}
+template <int NT_OUT, int NKB, int NT_IN, int NC, int NW, int PARTS = 3>
+__device__ __forceinline__ void tchain_x6_wg(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
+                                             const uint4* __restrict__ img, int lane, const WgRing<NW>& wr) {
+    static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");
+    tgemm_x6_wg<NT_OUT, NKB, NC, NW, PARTS>(
+        [&](int c, int kb, float (&v)[8]) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = in[c][kb >> 1][8 * (kb & 1) + e];
+        },
+        out, img, lane, wr);
+}
+
 // Chain layer: B = the C layout of the previous layer; k-block kb of tile t = kb>>1 is registers
 // 8(kb&1) .. +7 of in[c][t] (element e of lane half h = feature 16kb + 8(e>>2) + 4h + (e&3): image
 // kind X6_CHAIN).
@@ -436,6 +527,21 @@ __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 
             for (int e = 0; e < 8; ++e) v[e] = in[c][kb >> 1][8 * (kb & 1) + e];
         },
         out, img, lane);
+}
+
+// Kernels templated on the weight source: NW = 0 → each wave streams the image itself (tgemm_x6's
+// register ring, depth D), NW > 0 → the workgroup's shared LDS ring (tgemm_x6_wg).
+template <int NT_OUT, int NKB, int NC, int D, int PARTS, int NW, class GetB>
+__device__ __forceinline__ void tgemm_x6s(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img, int lane,
+                                          const WgRing<NW>& wr) {
+    if constexpr (NW > 0) tgemm_x6_wg<NT_OUT, NKB, NC, NW, PARTS>(getb, out, img, lane, wr);
+    else tgemm_x6<NT_OUT, NKB, NC, D, PARTS>(getb, out, img, lane);
+}
+template <int NT_OUT, int NKB, int NT_IN, int NC, int D, int PARTS, int NW>
+__device__ __forceinline__ void tchain_x6s(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
+                                           const uint4* __restrict__ img, int lane, const WgRing<NW>& wr) {
+    if constexpr (NW > 0) tchain_x6_wg<NT_OUT, NKB, NT_IN, NC, NW, PARTS>(in, out, img, lane, wr);
+    else tchain_x6<NT_OUT, NKB, NT_IN, NC, D, PARTS>(in, out, img, lane);
 }
 
 // Half-row operand of tgemm_x6: lane half h of column tile c holds features KH·h .. KH·h + KH-1

@@ -117,13 +117,16 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     store_cm<5>(a.G3 + bE, H, lane, valid);
 }
 
-// Node side of one backward step in split-bf16 math: the k_node_bwd chain on tgemm_x6, two 32-node
-// column tiles per wave (one wave per SIMD).
-template <int NC, int NP = 3>
+// Node side of one backward step in split-bf16 math: the k_node_bwd chain on tgemm_x6, NC 32-node
+// column tiles per wave (launched: NC = 1 at two waves per SIMD).
+// NW > 0: weight images shared by the workgroup's waves through an LDS ring (k_node_fwd_x6).
+template <int NC, int NP = 3, int NW = 0>
 __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
-    if (nb0 * 32 >= a.n_nodes) return;
+    if (NW == 0 && nb0 * 32 >= a.n_nodes) return;
+    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int nblocks = (a.n_nodes + 31) / 32;
     int nbc[NC];
     bool has[NC], valid[NC];
@@ -151,14 +154,14 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
 #pragma unroll
             for (int c = 0; c < NC; ++c) blk[c] = a.dU + bE(c);
             hr.load(blk, lane);
-            tgemm_x6<4, 10, NC, kX6Ring, NP>(hr, D, a.x_w1bt, lane);
+            tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, D, a.x_w1bt, lane, wr);
         }
         {
             HalfRows<kKhE, NC> hr;
 #pragma unroll
             for (int c = 0; c < NC; ++c) blk[c] = a.dV + bE(c);
             hr.load(blk, lane);
-            tgemm_x6<4, 10, NC, kX6Ring, NP>(hr, D, a.x_w1ct, lane);
+            tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, D, a.x_w1ct, lane, wr);
         }
     }
     if (a.tail) {  // dP0 = d/d 'propagation' (ld 100)
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
         if (has[c]) store_cm<4>(a.dx + bN(c), D[c], lane, valid[c]);
     }
     zero2(G);
-    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(D, G, a.x_wo2t, lane);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(D, G, a.x_wo2t, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 O1[4];
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // P part of omp's input → dP_s
     zero2(D);
-    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1pt, lane);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(G, D, a.x_wo1pt, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 T[4];
@@ -222,7 +225,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     // Wo1cᵀ is linear in do1 and runs once on Σ_s do1_s (k_enc_node_bwd)
     if (!a.dco_sum) {
         zero2(D);
-        tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1ct, lane);
+        tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(G, D, a.x_wo1ct, lane, wr);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             if (a.dco_accumulate) {
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // effect part → g = da ⊙ (1 - a²) → G3 = g·W3ᵀ
     zero2(D);
-    tchain_x6<4, 7, 4, NC, kX6Ring, NP>(G, D, a.x_wo1at, lane);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(G, D, a.x_wo1at, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 Aa[4];
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     f32x16 H[NC][5];
 #pragma unroll
     for (int c = 0; c < NC; ++c) zero_tiles(H[c]);
-    tchain_x6<5, 7, 4, NC, kX6Ring, NP>(D, H, a.x_w3t, lane);
+    tchain_x6s<5, 7, 4, NC, kX6Ring, NP, NW>(D, H, a.x_w3t, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
         if (has[c]) store_cm<5>(a.G3 + bE(c), H[c], lane, valid[c]);
@@ -512,16 +515,18 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     (void)h;
 }
 
-// The same backward chain in split-bf16 math: two 32-edge column tiles per wave (kernels_fwd.hip
+// The same backward chain in split-bf16 math: NC 32-edge column tiles per wave (kernels_fwd.hip
 // k_enc_edge_x6). dA rows (row-major) are loaded whole up front as half rows (lane half h: features
 // 76h .. 76h+75, image kind kh = 76), into the registers the second layer's output uses later.
 // B16 (bf16 math): dA is read and dz4..dz1 (the weight gradients' Y operands only) are stored as bf16
 // (exact, §3g).
-template <int NC, int NP = 3, bool B16 = false>
-__global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
+template <int NC, int NP = 3, bool B16 = false, int NW = 0>
+__global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
-    if (blk0 >= a.n_eblocks) return;
+    if (NW == 0 && blk0 >= a.n_eblocks) return;   // NW > 0: no early exit (tgemm_x6_wg)
+    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     f32x16 D[NC][5], E[NC][5];
     {
         float4 raw[NC][kKhE / 4];
@@ -539,20 +544,19 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
             }
             zero_tiles(D[c]);
         }
-        tgemm_x6<5, (kKhE + 7) / 8, NC, 6, NP>(
+        tgemm_x6s<5, (kKhE + 7) / 8, NC, 6, NP, NW>(
             [&](int c, int kb, float (&v)[8]) {
                 const float4 x = raw[c][2 * kb];
                 const float4 y = 2 * kb + 1 < kKhE / 4 ? raw[c][2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
                 v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
                 v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
             },
-            D, a.x_w1at, lane);   // dc_r = dA·W1aᵀ
+            D, a.x_w1at, lane, wr);   // dc_r = dA·W1aᵀ
     }
-    const bool has1 = NC > 1 && blk0 + 1 < a.n_eblocks;
     auto save = [&](float* base, const f32x16 (&Z)[NC][5]) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            if (c == 1 && !has1) break;
+            if (blk0 + c >= a.n_eblocks) break;
             if constexpr (B16) store_cm_b16<5>(reinterpret_cast<uint16_t*>(base) + (int64_t)(blk0 + c) * kCmBlk, Z[c], lane, true);
             else store_cm<5>(base + (int64_t)(blk0 + c) * kCmBlk, Z[c], lane, true);
         }
@@ -571,15 +575,15 @@ __global__ __launch_bounds__(256, 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
     bits(3, D, a.scale);   // relu + dropout of c_r
     save(a.dz4, D);
     zero2(E);
-    tchain_x6<5, 10, 5, NC, 6, NP>(D, E, a.x_rm3t, lane);
+    tchain_x6s<5, 10, 5, NC, 6, NP, NW>(D, E, a.x_rm3t, lane, wr);
     bits(2, E, 1.f);
     save(a.dz3, E);
     zero2(D);
-    tchain_x6<5, 10, 5, NC, 6, NP>(E, D, a.x_rm2t, lane);
+    tchain_x6s<5, 10, 5, NC, 6, NP, NW>(E, D, a.x_rm2t, lane, wr);
     bits(1, D, 1.f);
     save(a.dz2, D);
     zero2(E);
-    tchain_x6<5, 10, 5, NC, 6, NP>(D, E, a.x_rm1t, lane);
+    tchain_x6s<5, 10, 5, NC, 6, NP, NW>(D, E, a.x_rm1t, lane, wr);
     bits(0, E, 1.f);
     save(a.dz1, E);
     (void)h;
@@ -636,15 +640,17 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
     if (math == MATH_BF16) {
-        constexpr int NC = 2;
-        const int w2 = ((a.n_nodes + 31) / 32 + NC - 1) / NC;
-        hipLaunchKernelGGL((k_node_bwd_x6<NC, 1>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
+        const int w = (a.n_nodes + 31) / 32;
+        hipLaunchKernelGGL((k_node_bwd_x6<1, 1, 4>), dim3((w + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (math == MATH_X6) {
-        constexpr int NC = 2;
+        // one 32-node column tile per wave at two waves per SIMD, weight images shared by the
+        // workgroup's 4 waves (0.474 ms vs 0.557 for two tiles per wave at one wave per SIMD with
+        // per-wave rings, 0.630 for that with the shared ring: 393K nodes)
+        constexpr int NC = 1, NW = 4;
         const int w2 = ((a.n_nodes + 31) / 32 + NC - 1) / NC;
-        hipLaunchKernelGGL((k_node_bwd_x6<NC>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_node_bwd_x6<NC, 3, NW>), dim3((w2 + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     const int waves = (a.n_nodes + 31) / 32;
@@ -1006,16 +1012,17 @@ hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st) {
+    // one 32-edge block per wave at two waves per SIMD, weight images shared by the workgroup's 4
+    // waves (x6: 2.44 → 2.33 ms against two blocks per wave at one wave per SIMD with per-wave rings)
+    constexpr int NC = 1, NW = 4;
+    const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
     if (math == MATH_BF16) {
-        constexpr int NC = 2;
-        const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
-        if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, true>), g, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1>), g, dim3(256), 0, st, a);
+        if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, true, NW>), g, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, false, NW>), g, dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (math == MATH_X6) {
-        constexpr int NC = 2;
-        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC>), dim3((a.n_eblocks + 4 * NC - 1) / (4 * NC)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 3, false, NW>), g, dim3(256), 0, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_enc_edge_bwd, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);
@@ -1024,14 +1031,17 @@ hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st
 // The om encoder's backward in split-bf16 math: k_enc_node_bwd's two 100×100 products (Σ_s do1_s ·
 // Wo1cᵀ and om.1ᵀ) on tchain_x6 instead of the f32 matrix core (one 32-node column tile per wave, two
 // waves per SIMD, as k_enc_node_x6).
-template <int NP>
+template <int NP, int NW = 0>
 __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (nb * 32 >= a.n_nodes) return;
+    const bool has = nb * 32 < a.n_nodes;   // NW > 0: no early exit (k_enc_node_x6)
+    if (NW == 0 && !has) return;
+    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int n = nb * 32 + j;
-    const bool valid = n < a.n_nodes;
-    const int64_t bN = (int64_t)nb * kCmBlkN;   // chunk-major node block
+    const bool valid = has && n < a.n_nodes;
+    const int64_t bN = (int64_t)(has ? nb : (a.n_nodes + 31) / 32 - 1) * kCmBlkN;   // chunk-major node block
     f32x16 D[1][4], E[1][4], Z[4];
     // Σ_s do1_s in backward step order S-1..0 (the Y of the Wo1c weight gradient)
     load_cm<4>(a.do1 + (int64_t)(a.S - 1) * a.do1_step + bN, E[0], lane);
@@ -1040,17 +1050,17 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) E[0][t] += Z[t];
     }
-    store_cm<4>(a.dco + bN, E[0], lane, valid);
+    if (has) store_cm<4>(a.dco + bN, E[0], lane, valid);
     zero_tiles(D[0]);
-    tchain_x6<4, 7, 4, 1, kX6Ring, NP>(E, D, a.x_wo1ct, lane);   // dc_o = (Σ_s do1_s)·Wo1cᵀ
+    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW>(E, D, a.x_wo1ct, lane, wr);   // dc_o = (Σ_s do1_s)·Wo1cᵀ
     load_cm<4>(a.co + bN, Z, lane);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) D[0][t][r] = Z[t][r] > 0.f ? D[0][t][r] * a.scale : 0.f;
-    store_cm<4>(a.dzo2 + bN, D[0], lane, valid);
+    if (has) store_cm<4>(a.dzo2 + bN, D[0], lane, valid);
     zero_tiles(E[0]);
-    tchain_x6<4, 7, 4, 1, kX6Ring, NP>(D, E, a.x_om1t, lane);
+    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW>(D, E, a.x_om1t, lane, wr);
     if (a.zo1) {
         load_cm<4>(a.zo1 + bN, Z, lane);
     } else {   // the forward's own first-layer arithmetic (k_enc_node_x6), not a stored row
@@ -1067,14 +1077,14 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) E[0][t][r] = Z[t][r] > 0.f ? E[0][t][r] : 0.f;
-    store_cm<4>(a.dzo1 + bN, E[0], lane, valid);
+    if (has) store_cm<4>(a.dzo1 + bN, E[0], lane, valid);
 }
 
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
     if (math != MATH_F32 && a.wo1ct && a.x_wo1ct && a.x_om1t) {
-        if (math == MATH_BF16) hipLaunchKernelGGL(k_enc_node_bwd_x6<1>, dim3((waves + 3) / 4), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(k_enc_node_bwd_x6<3>, dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        if (math == MATH_BF16) hipLaunchKernelGGL((k_enc_node_bwd_x6<1, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_enc_node_bwd_x6<3, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_enc_node_bwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);
