@@ -443,19 +443,20 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
                                             int lane, const WgRing<NW>& wr) {
     static_assert(NT_OUT * 3 * 64 <= kWgSlot, "slot size");
     constexpr int NS = NKB * NT_OUT, NP = 4 * NC;
-    constexpr int PCS = NT_OUT * 3, PPW = (PCS + NW - 1) / NW;   // 1-KiB pieces per slice, per wave
+    // 1-KiB pieces per slice that are used (PARTS = 1: the h parts only, pieces 3T), per wave
+    constexpr int PCS = NT_OUT * (PARTS == 1 ? 1 : 3), PPW = (PCS + NW - 1) / NW, PST = PARTS == 1 ? 3 : 1;
     auto issue = [&](int kbl) {
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
-            const int i = min(wr.wid + NW * q, PCS - 1);   // the last pieces may be loaded twice (same bytes)
-            __builtin_amdgcn_global_load_lds(img + (kbl * PCS + i) * 64 + lane, wr.lds + ((kbl % 3) * kWgSlot + i * 64), 16, 0, 0);
+            const int i = PST * min(wr.wid + NW * q, PCS - 1);   // the last pieces may be loaded twice (same bytes)
+            __builtin_amdgcn_global_load_lds(img + (kbl * NT_OUT * 3 + i) * 64 + lane, wr.lds + ((kbl % 3) * kWgSlot + i * 64), 16, 0, 0);
         }
     };
     const uint4* rl = wr.lds + lane;
     auto frag = [&](int u, uint4 (&f)[3]) {
         const int kb = u / NT_OUT, T = u - kb * NT_OUT;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) f[p] = rl[(kb % 3) * kWgSlot + (T * 3 + p) * 64];
+        for (int p = 0; p < 3; ++p) f[p] = p < PARTS ? rl[(kb % 3) * kWgSlot + (T * 3 + p) * 64] : make_uint4(0u, 0u, 0u, 0u);
     };
     __builtin_amdgcn_s_barrier();   // every wave is done with the previous call's slots
     issue(0);
