@@ -47,15 +47,17 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 __device__ __forceinline__ float bf16_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 // (a, b) → three packed bf16 pairs h, m, l (element 0 = a in the low half)
-// The empty asm hides where h and m came from: otherwise the compiler rebuilds bf16_lo(h) as a
-// second v_cvt_pk_bf16_f32 of `a` alone plus the shift (13 VALU per pair instead of 11).
+// bf16_lo of h and m as a v_perm_b32: written as a shift, the compiler rebuilds it as a second
+// v_cvt_pk_bf16_f32 of `a` alone plus the shift (13 VALU per pair instead of 11); an empty asm
+// barrier on h and m also prevents that but costs a hazard s_nop per barrier.
+__device__ __forceinline__ float bf16_lo_perm(uint32_t p) {
+    return __uint_as_float(__builtin_amdgcn_perm(p, p, 0x01000C0Cu));   // bytes [0, 0, p0, p1]
+}
 __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
     h = pk_bf16(a, b);
-    asm("" : "+v"(h));
-    const float ra = a - bf16_lo(h), rb = b - bf16_hi(h);
+    const float ra = a - bf16_lo_perm(h), rb = b - bf16_hi(h);
     m = pk_bf16(ra, rb);
-    asm("" : "+v"(m));
-    l = pk_bf16(ra - bf16_lo(m), rb - bf16_hi(m));
+    l = pk_bf16(ra - bf16_lo_perm(m), rb - bf16_hi(m));
 }
 __device__ __forceinline__ bf16x8 as_bf16x8(i16x4 lo, i16x4 hi) {
     const i16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -160,6 +162,19 @@ __device__ __forceinline__ uint32_t writelane_imm(uint32_t val, int ln, uint32_t
 
 // The same without the wait state, for batches: every SGPR it reads must have been written several
 // instructions earlier (a group of ballots, a sched_barrier, then the group's writelanes).
+// Eight of them into one register in one statement: the compiler pads each inline asm with a
+// hazard s_nop; one pad per eight writelanes instead of one per writelane.
+__device__ __forceinline__ uint32_t writelane8_batched(uint32_t old, const uint32_t (&v)[8], const int (&ln)[8]) {
+    asm volatile(
+        "v_writelane_b32 %0, %1, %9\n\tv_writelane_b32 %0, %2, %10\n\t"
+        "v_writelane_b32 %0, %3, %11\n\tv_writelane_b32 %0, %4, %12\n\t"
+        "v_writelane_b32 %0, %5, %13\n\tv_writelane_b32 %0, %6, %14\n\t"
+        "v_writelane_b32 %0, %7, %15\n\tv_writelane_b32 %0, %8, %16"
+        : "+v"(old)
+        : "s"(v[0]), "s"(v[1]), "s"(v[2]), "s"(v[3]), "s"(v[4]), "s"(v[5]), "s"(v[6]), "s"(v[7]),
+          "i"(ln[0]), "i"(ln[1]), "i"(ln[2]), "i"(ln[3]), "i"(ln[4]), "i"(ln[5]), "i"(ln[6]), "i"(ln[7]));
+    return old;
+}
 __device__ __forceinline__ uint32_t writelane_imm_batched(uint32_t val, int ln, uint32_t old) {
     uint32_t r;
     asm volatile("v_writelane_b32 %0, %1, %2" : "=v"(r) : "s"(val), "i"(ln), "0"(old));

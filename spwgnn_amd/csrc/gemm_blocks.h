@@ -151,16 +151,20 @@ __device__ __forceinline__ int64_t cm_index(int64_t row, int f) {
 // ---- per-lane activation-sign bits of NT C-layout tiles (bit 16t + r of the lane's words), so a
 // backward pass in the same orientation reads 3 words per lane instead of the activations.
 // X must be ≥ +0 (post-relu): then X > 0 ⟺ its bit pattern is non-zero, min(bits, 1) is the bit.
+// Two VALU per bit, no compare: bits(X) + 0x7fffffff has bit 31 set ⟺ bits(X) ≠ 0, and
+// v_alignbit_b32(w, b, 31) = (w << 1) | (b >> 31) shifts it in (a word's bits walked from the top
+// index down). Written as a compare, the compiler emits v_cmp + s_nop + v_cndmask + v_or per bit.
 template <int NT>
 __device__ __forceinline__ void store_pos_bits(uint32_t* __restrict__ words, const f32x16 (&X)[NT], int lane) {
-    uint32_t w[(NT * 16 + 31) / 32] = {};
+    constexpr int NB = NT * 16;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int k = 0; k < (NB + 31) / 32; ++k) {
+        uint32_t w = 0u;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            w[(16 * t + r) >> 5] |= min(__float_as_uint(X[t][r]), 1u) << ((16 * t + r) & 31);
-#pragma unroll
-    for (int k = 0; k < (NT * 16 + 31) / 32; ++k) words[64 * k + lane] = w[k];
+        for (int idx = (32 * k + 31 < NB ? 32 * k + 31 : NB - 1); idx >= 32 * k; --idx)
+            w = __builtin_amdgcn_alignbit(w, __float_as_uint(X[idx >> 4][idx & 15]) + 0x7fffffffu, 31);
+        words[64 * k + lane] = w;
+    }
 }
 template <int NT>
 __device__ __forceinline__ void apply_pos_bits(const uint32_t* __restrict__ words, f32x16 (&X)[NT], int lane, float scale) {

@@ -1004,12 +1004,16 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                 for (int c = 0; c < 2; ++c) {
                     const int q = 2 * kb + c;
                     if (q < kKhE / 4) {
-                        uint32_t stg = 0u;
+                        uint32_t v[8];
+                        int ln[8];
 #pragma unroll
                         for (int f = 0; f < 4; ++f) {
-                            stg = writelane_imm_batched((uint32_t)bal[c][f], f, stg);
-                            stg = writelane_imm_batched((uint32_t)(bal[c][f] >> 32), 4 + f, stg);
+                            v[2 * f] = (uint32_t)bal[c][f];
+                            ln[2 * f] = f;
+                            v[2 * f + 1] = (uint32_t)(bal[c][f] >> 32);
+                            ln[2 * f + 1] = 4 + f;
                         }
+                        const uint32_t stg = writelane8_batched(0u, v, ln);
                         if (lane < 8) mrow[m1off + 4 * q] = stg;
                     }
                 }
@@ -1052,11 +1056,23 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
 #pragma unroll
                     for (int r = 0; r < 8; ++r) bal[r] = __ballot(acc[t][r0 + r] > 0.f);
                     __builtin_amdgcn_sched_barrier(0);
+                    // words m2_pos(rho(r, h), t) of ballots r = 4g..4g+3 all live in register g
+                    // (m2_pos(rho(r, h), t) >> 6 == r >> 2): one 8-writelane batch per register
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const int w0 = m2_pos(rho(r0 + r, 0), t), w1 = m2_pos(rho(r0 + r, 1), t);
-                        mw2[w0 >> 6] = writelane_imm_batched((uint32_t)bal[r], w0 & 63, mw2[w0 >> 6]);
-                        mw2[w1 >> 6] = writelane_imm_batched((uint32_t)(bal[r] >> 32), w1 & 63, mw2[w1 >> 6]);
+                    for (int g = 0; g < 2; ++g) {
+                        uint32_t v[8];
+                        int ln[8];
+                        const int reg = (r0 >> 2) + g;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int r = 4 * g + e;
+                            const int w0 = m2_pos(rho(r0 + r, 0), t), w1 = m2_pos(rho(r0 + r, 1), t);
+                            v[2 * e] = (uint32_t)bal[r];
+                            ln[2 * e] = w0 & 63;
+                            v[2 * e + 1] = (uint32_t)(bal[r] >> 32);
+                            ln[2 * e + 1] = w1 & 63;
+                        }
+                        mw2[reg] = writelane8_batched(mw2[reg], v, ln);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
