@@ -132,3 +132,27 @@ def test_bf16_math_forward_backward(N, fully):
     for k in g_ref:
         cos = float((gg[k] * g_ref[k]).sum() / (np.linalg.norm(gg[k]) * np.linalg.norm(g_ref[k]) + 1e-30))
         assert cos >= 0.99, (k, cos)
+
+
+# The chain kernels share each weight image through an LDS ring across the 4 waves of a workgroup
+# (tgemm_x6_wg): no wave may exit early, a wave past the last row block runs on the clamped block and
+# stores nothing. Row-block counts ≡ 1, 2, 3 (mod 4) for nodes and edges, forward + backward.
+@pytest.mark.parametrize("T,N", [(5, 6), (11, 6), (27, 6), (9, 9), (3, 13)])
+def test_shared_weight_ring_partial_workgroups(T, N):
+    params = O.random_params(seed=23)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(T, N, seed=T + N, fully_connected=(T % 2 == 1))
+    prop = np.random.default_rng(T).normal(0, 0.3, size=prop.shape).astype(np.float32)
+    S = 3
+    loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, S)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    print("node blocks", (batch.n_nodes + 31) // 32)
+    flat, ws, z = _gpu_forward(params, batch, S, training=True, math="x6")
+    out3, dz = E.bce(z, torch.tensor(tgt, device="cuda").reshape(-1), E.BceScratch("cuda"))
+    grads, _ = E.backward(flat, batch, E.RunConfig(S, training=True, math="x6"), ws, dz)
+    torch.cuda.synchronize()
+    ref = np.asarray(z_ref).reshape(-1)
+    assert np.all(np.abs(z.cpu().numpy().reshape(-1) - ref) <= LOGIT_ATOL + LOGIT_RTOL * np.abs(ref))
+    assert abs(float(out3[0]) - loss_ref) < 1e-5
+    got = P.from_flat(grads)
+    for name, r in g_ref.items():
+        assert np.abs(got[name] - r).max() <= 1e-5 * np.abs(r).max() + 1e-7, name
