@@ -430,41 +430,54 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
 // ---- the same product with the weight image shared by the NW waves of a workgroup through LDS.
 // Every wave of the workgroup calls the same tgemm_x6_wg sequence (no early exit: a wave with no
 // rows of its own runs on clamped rows and stores nothing), so the image streams from L2 once per
-// workgroup instead of once per wave: k-block kb's slice (NT_OUT steps × 3 parts × 1 KiB) is
-// DMA'd (global_load_lds, 1 KiB per wave-instruction, the NW waves' pieces interleaved) into LDS
-// slot kb % 3 one k-block ahead of use. One barrier per k-block, at its last step: it certifies
-// that slice kb+1 has landed (each wave's vmcnt(0) before it) and that every wave is done with
-// slot (kb−1) % 3, which then receives slice kb+2. Fragments are read one step ahead from LDS.
-// lds: kWgSlot·3 uint4 (the workgroup's only __shared__ object besides what the caller owns).
-constexpr int kWgSlot = 15 * 64;   // uint4 per slot: NT_OUT ≤ 5 steps × 3 parts × 64 lanes
+// workgroup instead of once per wave. The image is cut into slices of KPS k-blocks (all NT_OUT steps,
+// the parts the math uses: x6 one k-block × 3 parts, bf16 three k-blocks × the h part — 15 KiB
+// either way), DMA'd (global_load_lds, 1 KiB per wave-instruction, the NW waves' pieces interleaved)
+// into a ring of kWgRing LDS slots kWgRing − 2 slices ahead of use. One barrier per slice, at its
+// last step: it certifies that slice sl+1 has landed (each wave waits for its own DMAs with a vmcnt
+// that leaves the newer slices in flight) and that no wave still reads slot (sl−1) mod kWgRing, which
+// then receives slice sl + kWgRing − 1. Fragments are read one step ahead with ds_read_b128.
+// lds: kWgRing · kWgSlot uint4.
+constexpr int kWgSlot = 15 * 64;   // uint4 per slot
+constexpr int kWgRing = 4;         // slots (4 × 15 KiB per workgroup; two workgroups per CU)
 template <int NW>
 struct WgRing {
     uint4* lds;
     int wid;   // wave index in the workgroup (wave-uniform)
 };
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 template <int NT_OUT, int NKB, int NC, int NW, int PARTS = 3, class GetB>
 __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
                                             int lane, const WgRing<NW>& wr) {
-    static_assert(NT_OUT * 3 * 64 <= kWgSlot, "slot size");
-    constexpr int NS = NKB * NT_OUT, NP = 4 * NC;
-    // 1-KiB pieces per slice that are used (PARTS = 1: the h parts only, pieces 3T), per wave
-    constexpr int PCS = NT_OUT * (PARTS == 1 ? 1 : 3), PPW = (PCS + NW - 1) / NW, PST = PARTS == 1 ? 3 : 1;
-    auto issue = [&](int kbl) {
+    constexpr int LP = PARTS == 1 ? 1 : 3;    // parts held in LDS
+    constexpr int KPS = PARTS == 1 ? 3 : 1;   // k-blocks per slice
+    static_assert(KPS * NT_OUT * LP * 64 <= kWgSlot, "slot size");
+    constexpr int NS = NKB * NT_OUT, NP = 4 * NC, SST = KPS * NT_OUT;   // steps, pair-splits, steps per slice
+    constexpr int NSL = (NKB + KPS - 1) / KPS, R = kWgRing;
+    constexpr int PPW = (SST * LP + NW - 1) / NW;   // DMAs per wave per slice (short slices repeat pieces)
+    auto issue = [&](int sl) {
+        const int pc = (min(KPS, NKB - sl * KPS) * NT_OUT) * LP;   // pieces of this slice
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
-            const int i = PST * min(wr.wid + NW * q, PCS - 1);   // the last pieces may be loaded twice (same bytes)
-            __builtin_amdgcn_global_load_lds(img + (kbl * NT_OUT * 3 + i) * 64 + lane, wr.lds + ((kbl % 3) * kWgSlot + i * 64), 16, 0, 0);
+            const int i = min(wr.wid + NW * q, pc - 1);   // the last pieces may be loaded twice (same bytes)
+            const int js = i / LP, p = i - js * LP;       // step within the slice, part
+            __builtin_amdgcn_global_load_lds(img + ((sl * SST + js) * 3 + p) * 64 + lane,
+                                             wr.lds + ((sl % R) * kWgSlot + i * 64), 16, 0, 0);
         }
     };
     const uint4* rl = wr.lds + lane;
     auto frag = [&](int u, uint4 (&f)[3]) {
-        const int kb = u / NT_OUT, T = u - kb * NT_OUT;
+        const int sl = u / SST, js = u - sl * SST;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) f[p] = p < PARTS ? rl[(kb % 3) * kWgSlot + (T * 3 + p) * 64] : make_uint4(0u, 0u, 0u, 0u);
+        for (int p = 0; p < 3; ++p) f[p] = p < LP ? rl[(sl % R) * kWgSlot + (js * LP + p) * 64] : make_uint4(0u, 0u, 0u, 0u);
     };
     __builtin_amdgcn_s_barrier();   // every wave is done with the previous call's slots
-    issue(0);
-    if (NKB > 1) issue(1);
+    asm volatile("" ::: "memory");  // no memory op moves below: the vmcnt counts below see only DMAs
+#pragma unroll
+    for (int sl = 0; sl < R - 1 && sl < NSL; ++sl) issue(sl);
     uint32_t sp[2][NC][3][4];
     auto split_pair = [&](int kb, int q) {
         const int c = q >> 2, m = q & 3;
@@ -474,7 +487,7 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
     };
 #pragma unroll
     for (int q = 0; q < NP; ++q) split_pair(0, q);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_vmcnt<PPW * ((R - 2 < NSL - 1) ? R - 2 : NSL - 1)>();   // slice 0 landed (this wave's part)
     __builtin_amdgcn_s_barrier();
     uint4 fr[2][3];
     frag(0, fr[0]);
@@ -491,10 +504,15 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = as_bf16x8(fr[u & 1][p]);
         if (u + 1 < NS) {
-            if (T == NT_OUT - 1) {   // slice kb+1 landed, slot (kb−1)%3 free on every wave
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if ((u + 1) % SST == 0) {   // slice sl+1 landed, slot (sl−1) % R free on every wave
+                const int sl = u / SST;
+                // slices issued after sl+1 so far: up to min(sl + R − 2, NSL − 1)
+                const int ahead = min(sl + R - 2, NSL - 1) - (sl + 1);
+                if (ahead >= 2) wait_vmcnt<2 * PPW>();
+                else if (ahead == 1) wait_vmcnt<PPW>();
+                else wait_vmcnt<0>();
                 __builtin_amdgcn_s_barrier();
-                if (kb + 2 < NKB) issue(kb + 2);
+                if (sl + R - 1 < NSL) issue(sl + R - 1);
             }
             frag(u + 1, fr[(u + 1) & 1]);
         }

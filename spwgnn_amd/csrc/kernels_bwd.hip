@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
     if (NW == 0 && nb0 * 32 >= a.n_nodes) return;
-    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int nblocks = (a.n_nodes + 31) / 32;
     int nbc[NC];
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_bwd_x6(EncEdg
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
     if (NW == 0 && blk0 >= a.n_eblocks) return;   // NW > 0: no early exit (tgemm_x6_wg)
-    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     f32x16 D[NC][5], E[NC][5];
     {
@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool has = nb * 32 < a.n_nodes;   // NW > 0: no early exit (k_enc_node_x6)
     if (NW == 0 && !has) return;
-    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int n = nb * 32 + j;
     const bool valid = has && n < a.n_nodes;

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     const int n = nb * 32 + j;
     const bool has = nb * 32 < a.n_nodes;
     if (NW == 0 && !has) return;
-    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int nbk = has ? nb : (a.n_nodes + 31) / 32 - 1;
     const bool valid = has && n < a.n_nodes;
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_x6(EncEdgeArg
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
     if (NW == 0 && blk0 >= a.n_eblocks) return;   // NW > 0: no early exit (tgemm_x6_wg)
-    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     f32x16 X[NC][5], Y[NC][5];
     int src[NC], dst[NC];
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
     if (NW == 0 && nb0 * 32 >= a.n_nodes) return;
-    __shared__ uint4 wring[NW > 0 ? 3 * kWgSlot : 1];
+    __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int nblocks = (a.n_nodes + 31) / 32;
     int nbc[NC];
