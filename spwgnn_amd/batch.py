@@ -33,6 +33,32 @@ def default_nw_max(max_nodes: int) -> int:
 _NW_LIMIT = 32
 
 
+def upload(arrays, device) -> list:
+    """Host arrays → device tensors in ONE copy: packed (16-byte aligned) into a pinned staging
+    buffer and copied with non_blocking=True, so the host does not wait for the stream to drain (a
+    copy from pageable memory does) and can build the next batch while the GPU runs this one. The
+    caching host allocator keeps the staging block until its copy has run."""
+    dev = torch.device(device)
+    arrays = [np.ascontiguousarray(a) for a in arrays]
+    if dev.type != "cuda":
+        return [torch.from_numpy(a.copy()) for a in arrays]
+    offs, total = [], 0
+    for a in arrays:
+        offs.append(total)
+        total += (a.nbytes + 15) // 16 * 16
+    host = torch.empty(max(total, 16), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    for a, o in zip(arrays, offs):
+        hv[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+    d = host.to(dev, non_blocking=True)
+    out = []
+    for a, o in zip(arrays, offs):
+        t = d[o:o + a.nbytes].view(torch.from_numpy(a[:0].reshape(-1)).dtype) if a.nbytes else \
+            torch.empty(0, dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device=dev)
+        out.append(t.view(a.shape))
+    return out
+
+
 @dataclass
 class TowerBatch:
     n_towers: int
@@ -110,13 +136,13 @@ class TowerBatch:
         pos4 = np.zeros((Nn, 4), np.float32)
         pos4[:, :3] = np.asarray(pos, np.float32)[:, :3]
         dev = torch.device(device)
-        tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        prop_t = None
+        host = [pos4, node_tower, node_local, wtile, esrc, edst, csr]
         if prop is not None:
-            prop_t = torch.as_tensor(np.asarray(prop, np.float32).reshape(Nn, 100)).to(dev).contiguous()
+            host.append(np.asarray(prop, np.float32).reshape(Nn, 100))
+        d = upload(host, dev)
+        prop_t = d[7] if prop is not None else None
         return TowerBatch(T, Nn, tower_nodes, tower_edges, src, dst, sizes.n_wtiles, sizes.n_eblocks,
-                          sizes.nw_max, dev, tt(pos4), prop_t, tt(node_tower), tt(node_local), tt(wtile),
-                          tt(esrc), tt(edst), tt(csr), eid, node_shape)
+                          sizes.nw_max, dev, d[0], prop_t, d[1], d[2], d[3], d[4], d[5], d[6], eid, node_shape)
 
     @staticmethod
     def from_dense(objects, sender_relations, receiver_relations, propagation=None, device="cuda",

@@ -18,7 +18,7 @@ import torch
 
 from . import engine as E
 from . import params as P
-from .batch import TowerBatch
+from .batch import TowerBatch, upload
 from .network import GraphNetwork
 
 
@@ -56,13 +56,14 @@ class CompactDataset:
     def subset(self, idx: np.ndarray, device) -> TowerBatch:
         idx = np.asarray(idx)
         n = len(idx)
-        pieces_s, pieces_d = [], []
-        for k, b in enumerate(idx):
-            e0, e1 = self.edge_off[b], self.edge_off[b + 1]
-            pieces_s.append(self.src[e0:e1] + k * self.N)
-            pieces_d.append(self.dst[e0:e1] + k * self.N)
-        src = np.concatenate(pieces_s) if pieces_s else np.zeros(0, np.int32)
-        dst = np.concatenate(pieces_d) if pieces_d else np.zeros(0, np.int32)
+        # the towers' edge ranges gathered in one vectorised pass (tower k of the batch: node ids + k·N)
+        cnt = self.tower_edges[idx].astype(np.int64)
+        tot = int(cnt.sum())
+        first = np.cumsum(cnt) - cnt                         # batch position of each tower's first edge
+        gidx = np.arange(tot, dtype=np.int64) + np.repeat(self.edge_off[idx] - first, cnt)
+        shift = np.repeat(np.arange(n, dtype=np.int32) * self.N, cnt)
+        src = (self.src[gidx] + shift).astype(np.int32)
+        dst = (self.dst[gidx] + shift).astype(np.int32)
         prop = None if self.prop is None else self.prop[idx].reshape(n * self.N, 100)
         return TowerBatch.from_edges(self.objects[idx].reshape(n * self.N, 3), np.full(n, self.N, np.int32), src, dst,
                                      self.tower_edges[idx], prop, device, node_shape=(n, self.N))
@@ -138,23 +139,26 @@ class KerasModel:
         ds = CompactDataset(objects, x["sender_relations"], x["receiver_relations"], x.get("propagation"))
         rng = np.random.default_rng(seed)
         dev = self.net.device
-        tgt = torch.as_tensor(target, device=dev)
         hist = {"loss": [], "binary_accuracy": []}
         if n_val:
             hist.update({"val_loss": [], "val_binary_accuracy": []})
             vbatch = ds.subset(np.arange(n_tr, B), dev)
-            vtgt = tgt[n_tr:].reshape(-1).contiguous()
+            vtgt = torch.as_tensor(target[n_tr:], device=dev).reshape(-1).contiguous()
         for ep in range(epochs):
             order = rng.permutation(n_tr) if shuffle else np.arange(n_tr)
-            tot_l = tot_c = tot_n = 0.0
+            # (Σ loss·batch, Σ correct, Σ nodes) on the device: no host sync per batch, so the host
+            # builds the next batch while the GPU runs this one
+            tot = torch.zeros(3, dtype=torch.float64, device=dev)
+            wvec = {}   # (batch length, 1, 1) weights, one device copy per distinct length
             for b0 in range(0, n_tr, batch_size):
                 idx = order[b0:b0 + batch_size]
                 batch = ds.subset(idx, dev)
-                o3 = self.train_on_batch(batch, tgt[torch.as_tensor(idx, device=dev)].reshape(-1).contiguous())
-                l, c, n = o3.tolist()
-                tot_l += l * len(idx)
-                tot_c += c
-                tot_n += n
+                (tg,) = upload([target[idx].reshape(-1)], dev)
+                o3 = self.train_on_batch(batch, tg)
+                if len(idx) not in wvec:
+                    wvec[len(idx)] = torch.tensor([float(len(idx)), 1.0, 1.0], dtype=torch.float64, device=dev)
+                tot += o3.double() * wvec[len(idx)]
+            tot_l, tot_c, tot_n = tot.tolist()
             hist["loss"].append(tot_l / max(n_tr, 1))
             hist["binary_accuracy"].append(tot_c / max(tot_n, 1))
             if n_val:

@@ -303,3 +303,17 @@ def test_forward_hipgraph_capture_replays_identically():
                           torch.tensor(Rr, dtype=torch.float64), torch.zeros(3, 32, 100, dtype=torch.float64), 10).numpy()
     got = z.cpu().numpy().reshape(ref.shape)
     assert np.all(np.abs(got - ref) <= 1e-5 + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
+
+
+def test_batch_upload_pinned_roundtrip():
+    """batch.upload on the GPU: one pinned staging buffer, one non-blocking copy, typed views —
+    every array arrives with its dtype, shape and bytes (and the empty one stays empty)."""
+    from spwgnn_amd.batch import upload
+    rng = np.random.default_rng(0)
+    arrs = [rng.integers(-5, 5, 37).astype(np.int32), rng.normal(size=(9, 4)).astype(np.float32),
+            rng.integers(0, 255, (3, 128)).astype(np.uint8), np.zeros(0, np.int32), rng.normal(size=11).astype(np.float32)]
+    out = upload(arrs, "cuda")
+    torch.cuda.synchronize()
+    for a, t in zip(arrs, out):
+        assert t.device.type == "cuda" and t.shape == a.shape
+        assert np.array_equal(t.cpu().numpy(), a)

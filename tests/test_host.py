@@ -254,3 +254,31 @@ def test_ragged_batch_matches_per_tower_relations():
     p2, n2, s2, d2, e2 = D.edge_slice(pos, sz, s, d, te, 100, 200)
     assert np.array_equal(s2 + off[100], s[eo[100]:eo[200]]) and np.array_equal(n2, sz[100:200])
     assert len(p2) == off[200] - off[100] and s2.min() >= 0 and d2.max() < len(p2)
+
+
+def test_compact_dataset_subset_matches_per_tower_gather():
+    """keras_api.CompactDataset.subset gathers the towers' edge ranges in one vectorised pass:
+    same edge list as walking the towers one by one (node ids shifted by k·N for batch tower k)."""
+    from spwgnn_amd import data as D
+    from spwgnn_amd.keras_api import CompactDataset
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(40, 7, seed=4, fully_connected=False)
+    ds = CompactDataset(obj, Rs, Rr, prop)
+    for idx in (np.arange(40), np.random.default_rng(1).permutation(40)[:13], np.array([5])):
+        b = ds.subset(idx, "cpu")
+        ps, pd = [], []
+        for k, t in enumerate(idx):
+            e0, e1 = ds.edge_off[t], ds.edge_off[t + 1]
+            ps.append(ds.src[e0:e1] + k * ds.N)
+            pd.append(ds.dst[e0:e1] + k * ds.N)
+        assert np.array_equal(b.src, np.concatenate(ps)) and np.array_equal(b.dst, np.concatenate(pd))
+
+
+def test_batch_upload_roundtrip_cpu():
+    """batch.upload packs host arrays into one staging buffer (16-byte aligned pieces) and returns
+    one tensor per array with its dtype and shape."""
+    from spwgnn_amd.batch import upload
+    arrs = [np.arange(7, dtype=np.int32), np.ones((3, 4), np.float32) * 2.5, np.arange(5, dtype=np.uint8),
+            np.zeros(0, np.int32)]
+    out = upload(arrs, "cpu")
+    for a, t in zip(arrs, out):
+        assert t.shape == a.shape and np.array_equal(t.numpy(), a)
