@@ -431,7 +431,7 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
 // Every wave of the workgroup calls the same tgemm_x6_wg sequence (no early exit: a wave with no
 // rows of its own runs on clamped rows and stores nothing), so the image streams from L2 once per
 // workgroup instead of once per wave. The image is cut into slices of KPS k-blocks (all NT_OUT steps,
-// the parts the math uses: x6 one k-block × 3 parts, bf16 three k-blocks × the h part — 15 KiB
+// the parts the math uses: x6 one k-block × 3 parts, bf16 three k-blocks × the h part — ≤ 15 KiB
 // either way), DMA'd (global_load_lds, 1 KiB per wave-instruction, the NW waves' pieces interleaved)
 // into a ring of kWgRing LDS slots kWgRing − 2 slices ahead of use. One barrier per slice, at its
 // last step: it certifies that slice sl+1 has landed (each wave waits for its own DMAs with a vmcnt
