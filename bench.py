@@ -60,23 +60,38 @@ CONFIGS = {
     5: dict(nodes=32, towers=8192, S=10, math="x6", relations="full", mode="infer"),
 }
 
-# algorithmic FLOPs per launch of each timed kernel, as f(real edges, nodes, S)
+# algorithmic FLOPs PER STEP of each timed kernel, as f(real edges, nodes, S); the
+# launches per step are counted from the HIP events the library recorded, so a kernel family (the
+# k_wgrad_ws weight gradients: 12 launches of different shapes) reports FLOPs and time per step
+def _wgrad_ws_flops(Ne, Nn, S):
+    """the stored-operand weight gradients (k_wgrad_ws, split-bf16 maths): rm.1-3 and W1a over the
+    edges ([z | 1]ᵀ·dz, 151×150 each), W1b/W1c (100×150), W3 ([H2s | deg]ᵀ·g, 151×100), omp.0's a and
+    P parts (100×100) and omp.1 ([o1 | 1]ᵀ·dx, 101×101) over nodes × steps, omp.0's c_o part on Σ_s do1
+    and om.1 (101×100 each) over the nodes"""
+    return 2.0 * (4 * 151 * 150 * Ne + S * Nn * (2 * 100 * 150 + 151 * 100 + 2 * 100 * 100 + 101 * 101)
+                  + Nn * 2 * 101 * 100)
+
+
 KERNELS = {
-    "edge_fwd": (_lib.K_EDGE_FWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne),
-    "edge_bwd": (_lib.K_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne),
-    "node_fwd": (_lib.K_NODE_FWD, lambda Ne, Nn, S: 2.0 * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150) * Nn),
-    "node_bwd": (_lib.K_NODE_BWD, lambda Ne, Nn, S: 2.0 * (2 * 150 * 100 + 101 * 100 + 300 * 100 + 150 * 100) * Nn),
+    "edge_fwd": (_lib.K_EDGE_FWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne * S),
+    "edge_bwd": (_lib.K_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne * S),
+    "node_fwd": (_lib.K_NODE_FWD, lambda Ne, Nn, S: 2.0 * (151 * 100 + 300 * 100 + 100 * 101 + 2 * 100 * 150) * Nn * S),
+    "node_bwd": (_lib.K_NODE_BWD, lambda Ne, Nn, S: 2.0 * (2 * 150 * 100 + 101 * 100 + 300 * 100 + 150 * 100) * Nn * S),
     "wgrad_w2": (_lib.K_WGRAD_W2, lambda Ne, Nn, S: 2.0 * 151 * 150 * Ne * S),
+    "wgrad_ws": (_lib.K_WGRAD_WS, _wgrad_ws_flops),
     "dA": (_lib.K_DA, lambda Ne, Nn, S: 2.0 * 150 * 150 * Ne * S),
     "enc_edge": (_lib.K_ENC_EDGE, lambda Ne, Nn, S: 2.0 * (2 * 150 + 4 * 150 * 150) * Ne),
     "enc_edge_bwd": (_lib.K_ENC_EDGE_BWD, lambda Ne, Nn, S: 2.0 * 4 * 150 * 150 * Ne),
+    "enc_node": (_lib.K_ENC_NODE, lambda Ne, Nn, S: 2.0 * (2 * 100 + 100 * 100 + 2 * 100 * 150) * Nn),
+    "enc_node_bwd": (_lib.K_ENC_NODE_BWD, lambda Ne, Nn, S: 2.0 * 2 * 100 * 100 * Nn),
 }
-LAUNCHES_PER_STEP = {"edge_fwd": "S", "edge_bwd": "S", "node_fwd": "S", "node_bwd": "S", "wgrad_w2": 1, "dA": 1,
-                     "enc_edge": 1, "enc_edge_bwd": 1}
+INFER_KERNELS = ("edge_fwd", "node_fwd", "enc_edge", "enc_node")
+MAX_LAUNCHES = 32      # event pairs reserved per kernel per micro-batch and step (the family has 12)
 # device kernel name prefix in the rocprofv3 PMC summaries (tools/pmcsum.py)
 PMC_PREFIX = {"edge_fwd": "k_edge_fwd", "edge_bwd": "k_edge_bwd", "node_fwd": "k_node_fwd",
               "node_bwd": "k_node_bwd", "wgrad_w2": "k_w2grad", "enc_edge": "k_enc_edge", "dA": "k_dA",
-              "enc_edge_bwd": "k_enc_edge_bwd"}
+              "enc_edge_bwd": "k_enc_edge_bwd", "wgrad_ws": "k_wgrad_ws", "enc_node": "k_enc_node",
+              "enc_node_bwd": "k_enc_node_bwd"}
 
 
 def fwd_flops(Ne: int, Nn: int, S: int) -> float:
@@ -119,32 +134,43 @@ class HipEvents:
 
 
 # ------------------------------------------------------------------------------ workloads
-def make_workload(cfg: dict, rank: int, device):
-    """The synthetic batch (or micro-batches) of one rank and their targets."""
-    B, S = cfg["towers"], cfg["S"]
-    rng = np.random.default_rng(rank)
-    if isinstance(cfg["nodes"], tuple):            # config 4: ragged, micro-batched shard
-        from spwgnn_amd import shard
+def make_workload(cfg: dict, rank: int, device, world: int = 1):
+    """This rank's part of the job's synthetic global batch and its targets.
+
+    Every rank builds the same global batch of towers·world towers from one seed, cuts it with the
+    cost planner `shard.plan_shards` (contiguous tower ranges of near-equal algorithmic cost; equal
+    ranges for uniform towers) and keeps its own range, as micro-batches when the config has them.
+    Returns (batches, targets, n_global): n_global = nodes in the whole global batch, taken from the
+    plan, so the Trainer needs no per-step all-reduce of node counts."""
+    from spwgnn_amd import shard
+    B, S = cfg["towers"] * world, cfg["S"]
+    thr = D.RELATION_THRESHOLD if cfg["relations"] == "threshold" else None
+    if isinstance(cfg["nodes"], tuple):            # config 4: ragged towers
         lo, hi = cfg["nodes"]
-        pos, sizes, src, dst, te, _ = D.ragged_batch(B, lo, hi, seed=4000 + rank,
-                                                     threshold=D.RELATION_THRESHOLD if cfg["relations"] == "threshold" else None)
-        batches, targets = [], []
-        for a, b in shard.micro_batches(0, B, cfg.get("micro", B)):
-            part = D.edge_slice(pos, sizes, src, dst, te, a, b)
-            bt = TowerBatch.from_edges(*part, device=device)
-            batches.append(bt)
-            targets.append(torch.tensor(rng.integers(0, 2, size=bt.n_nodes).astype(np.float32), device=device))
-        return batches, targets
-    N = cfg["nodes"]
-    raw = D.synthetic_towers(B, N, seed=1000 + rank + 97 * N)
-    objects = (raw / D.RELATION_THRESHOLD).astype(np.float32)
-    if cfg["relations"] == "full":
-        batch = TowerBatch.fully_connected(objects, device=device)
+        pos, sizes, src, dst, te, _ = D.ragged_batch(B, lo, hi, seed=4000, threshold=thr)
     else:
-        Rs, Rr = D.relation_matrices(raw, D.RELATION_THRESHOLD)
-        batch = TowerBatch.from_dense(objects, Rs, Rr, None, device=device)
-    target = torch.tensor(rng.integers(0, 2, size=B * N).astype(np.float32), device=device)
-    return [batch], [target]
+        N = cfg["nodes"]
+        raw = D.synthetic_towers_fast(B, N, seed=1000 + 97 * N)
+        sizes = np.full(B, N, np.int32)
+        m_idx, j_idx = np.nonzero(~np.eye(N, dtype=bool))           # sender-major slots (main.py:72-81)
+        keep = np.ones((B, len(m_idx)), bool) if thr is None else \
+            np.linalg.norm(raw[:, m_idx, 0:2] - raw[:, j_idx, 0:2], axis=2) < thr
+        tt, kk = np.nonzero(keep)
+        src = (tt * N + m_idx[kk]).astype(np.int32)
+        dst = (tt * N + j_idx[kk]).astype(np.int32)
+        te = keep.sum(axis=1).astype(np.int32)
+        pos = (raw / D.RELATION_THRESHOLD).astype(np.float32).reshape(B * N, 3)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    n_global = int(off[-1])
+    target_all = np.random.default_rng(17).integers(0, 2, size=n_global).astype(np.float32)
+    a, b = shard.plan_shards(sizes, te, world, mp_steps=S)[rank]
+    batches, targets = [], []
+    for x, y in shard.micro_batches(a, b, cfg.get("micro") or max(b - a, 1)):
+        part = D.edge_slice(pos, sizes, src, dst, te, x, y)
+        bt = TowerBatch.from_edges(*part, device=device)
+        batches.append(bt)
+        targets.append(torch.tensor(target_all[off[x]:off[y]], device=device))
+    return batches, targets, n_global
 
 
 def workload_name(cfg: dict, world: int, dropout: float) -> str:
@@ -255,7 +281,7 @@ def load_pmc(config: int, kernel: str, math: str, workload: str):
             return None
         tot = cnt = 0.0
         for name, v in d.items():
-            if kernel == "enc_edge" and name.startswith("k_enc_edge_bwd"):
+            if kernel in ("enc_edge", "enc_node") and name.startswith(PMC_PREFIX[kernel] + "_bwd"):
                 continue
             if name.startswith(PMC_PREFIX[kernel]) and "hbm_read_bytes" in v and "hbm_write_bytes" in v:
                 tot += (v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["dispatches"]
@@ -294,22 +320,58 @@ def step_hbm(config: int, ms_per_step: float, math: str, workload: str):
         return None
 
 
-def roofline(kernel: str, kern_ms, Ne, Nn, S, math, config, workload):
-    """The timed kernel's roofline: algorithmic FLOPs per launch ÷ its mean HIP-event launch time,
-    against the matrix peak of the math it runs in; every timed kernel is fused GEMM work far above
-    the ridge point, so the bound is the matrix pipe. `traffic` = measured HBM bytes per
-    launch from the committed PMC summary of the same workload (null if none)."""
+def roofline(kernel: str, kern_ms, launches_per_step, Ne, Nn, S, math, config, workload):
+    """A timed kernel's roofline: its algorithmic FLOPs per step ÷ its HIP-event time per step (the
+    mean launch time × launches per step), against the matrix peak of the math it runs in; every timed
+    kernel is fused GEMM work far above the ridge point, so the bound is the matrix pipe.
+    `traffic` = measured HBM bytes per launch from the committed PMC summary of the same workload
+    (null if none)."""
     avg_ms = float(np.mean(kern_ms))
-    kflops = KERNELS[kernel][1](Ne, Nn, S)
+    fl_step = KERNELS[kernel][1](Ne, Nn, S)
+    kflops = fl_step / launches_per_step
     achieved = kflops / (avg_ms * 1e-3) / 1e12
     mpeak = MATH_PEAK[math]
     traffic = load_pmc(config, kernel, math, workload)
     h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(mpeak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / mpeak, 4), "traffic": traffic, "kernel": kernel,
-            "avg_launch_ms": round(avg_ms, 4), "launches": len(kern_ms), "flop_per_launch": kflops,
+            "avg_launch_ms": round(avg_ms, 4), "launches": len(kern_ms), "launches_per_step": launches_per_step,
+            "ms_per_step": round(avg_ms * launches_per_step, 4), "flop_per_launch": kflops,
             "hbm_gbs": round(h_gbs, 1) if h_gbs else None,
             "hbm_frac": round(h_gbs / PEAK_HBM_GBS, 4) if h_gbs else None, "peak_note": PEAK_NOTE[math]}
+
+
+def recorded_ms(ev, npairs):
+    """Launch times of the event pairs the library recorded (pairs it did not record are skipped:
+    a kernel runs fewer times than the slots reserved for it, or not at all in this math)."""
+    out = []
+    for i in range(npairs):
+        try:
+            out.append(ev.elapsed_ms(2 * i, 2 * i + 1))
+        except RuntimeError:
+            pass
+    return out
+
+
+def timed_steps(trainer, step_in, kid, n_micro, steps, slots):
+    """`steps` training steps with HIP events around every launch of kernel `kid` (at most `slots`
+    per micro-batch and step). Returns (launch ms list, launches per step, last step's out3)."""
+    ev = HipEvents(2 * slots * n_micro * steps)
+    per_step = 2 * slots * n_micro
+    out3 = None
+    for k in range(steps):
+        evs = ev.ev[per_step * k: per_step * (k + 1)]
+        if n_micro == 1:
+            trainer.prof_kernel, trainer.prof_events = kid, evs
+            out3 = trainer.step(*step_in)
+        else:
+            trainer.prof_kernel, trainer.prof_events = kid, None
+            out3 = _micro_step(trainer, *step_in, evs, slots)
+    trainer.prof_kernel, trainer.prof_events = 0, None
+    torch.cuda.synchronize()
+    ms = recorded_ms(ev, slots * n_micro * steps)
+    ev.close()
+    return ms, len(ms) // steps, out3
 
 
 # ------------------------------------------------------------------------------ main
@@ -362,59 +424,63 @@ def main():
 
 def run_train(args, cfg, world, rank, device):
     S, math = cfg["S"], cfg["math"]
-    batches, targets = make_workload(cfg, rank, device)
+    batches, targets, n_global = make_workload(cfg, rank, device, world)
     params = P.to_flat(P.glorot_uniform(0), device=device)
     if world > 1:
         dist.broadcast(params, 0)
     trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math)
-    step_in = (batches[0], targets[0]) if len(batches) == 1 else (batches, targets)
+    step_in = ((batches[0], targets[0]) if len(batches) == 1 else (batches, targets)) + (n_global,)
+    n_micro = len(batches)
     for _ in range(args.warmup):
         trainer.step(*step_in)
     torch.cuda.synchronize()
+    Ne = sum(b.n_edges for b in batches)
+    Nn = sum(b.n_nodes for b in batches)
+    B = sum(b.n_towers for b in batches)
+    wl = workload_name(cfg, world, args.dropout)
 
-    kname = args.roofline_kernel or "edge_bwd"
+    # every timed kernel's per-step time, before the timed region (untimed steps), so the roofline
+    # can name the DOMINANT kernel (largest ms per step) and time it inside the timed region
+    table = {}
+    if not args.no_kernel_table or not args.roofline_kernel:
+        table = kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, args.config, wl)
+    kname = args.roofline_kernel or (max(table, key=lambda k: table[k]["ms_per_step"]) if table else "edge_fwd")
     kid = KERNELS[kname][0]
-    per = LAUNCHES_PER_STEP[kname]
-    per_step = (S if per == "S" else per) * len(batches)
-    nl = per_step * args.steps
-    ev = HipEvents(2 * nl)
-    trainer.prof_kernel = kid
+    ev = HipEvents(2 * MAX_LAUNCHES * n_micro * args.steps)
+    per = 2 * MAX_LAUNCHES * n_micro
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        # the library fills events in launch order: one slice of the array per micro-batch launch set
-        evs = ev.ev[2 * per_step * k: 2 * per_step * (k + 1)]
-        if len(batches) == 1:
-            trainer.prof_events = evs
+        # the library fills events in launch order: one slice of the array per step (and micro-batch)
+        evs = ev.ev[per * k: per * (k + 1)]
+        if n_micro == 1:
+            trainer.prof_kernel, trainer.prof_events = kid, evs
             out3 = trainer.step(*step_in)
         else:
-            trainer.prof_events = None
-            out3 = _micro_step(trainer, batches, targets, evs, per_step // len(batches))
+            trainer.prof_kernel, trainer.prof_events = kid, None
+            out3 = _micro_step(trainer, *step_in, evs, MAX_LAUNCHES)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    trainer.prof_kernel, trainer.prof_events = 0, None
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
-    kern_ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(nl)]
+    kern_ms = recorded_ms(ev, MAX_LAUNCHES * n_micro * args.steps)
     ev.close()
-    o3 = out3 if not isinstance(out3, list) else out3[0]
-    loss = float(o3[0].item())
+    loss = float(out3[0].item())     # node-weighted mean BCE over this rank's micro-batches
 
-    Ne = sum(b.n_edges for b in batches)
-    Nn = sum(b.n_nodes for b in batches)
-    B = sum(b.n_towers for b in batches)
-    wl = workload_name(cfg, world, args.dropout)
-    # kernel FLOPs per launch: one launch covers one micro-batch
-    roof = roofline(kname, kern_ms, Ne / len(batches), Nn / len(batches), S, math, args.config, wl)
+    roof = roofline(kname, kern_ms, len(kern_ms) // args.steps, Ne, Nn, S, math, args.config, wl)
+    roof["selected"] = "--roofline-kernel" if args.roofline_kernel else \
+        "dominant: largest ms per step in this run's kernel table (measured before the timed region)"
     metric = METRIC if args.config == 0 else f"towers/sec fwd+bwd, BASELINE config {args.config}"
     out = {
         "metric": metric,
-        "value": round(world * B * args.steps / el, 1),
+        "value": round(cfg["towers"] * world * args.steps / el, 1),   # the whole global batch per step
         "unit": "towers/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -426,7 +492,8 @@ def run_train(args, cfg, world, rank, device):
         "dtype": "bf16" if math == "bf16" else "f32",
         "math": MATH_DESC[math],
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
-        "config": {"workload": wl, "baseline_config": args.config, "towers_per_gpu": B, "global_batch": B * world,
+        "config": {"workload": wl, "baseline_config": args.config, "towers_per_gpu": B, "global_batch": cfg["towers"] * world,
+                   "n_global_nodes": n_global, "shard_plan": "shard.plan_shards (cost-balanced contiguous ranges)",
                    "nodes_per_tower": list(cfg["nodes"]) if isinstance(cfg["nodes"], tuple) else cfg["nodes"],
                    "nodes_per_gpu": Nn, "edges_per_gpu": Ne, "mp_steps": S, "math": math,
                    "parallelism": f"dp{world}"},
@@ -453,8 +520,8 @@ def run_train(args, cfg, world, rank, device):
             del trm
             torch.cuda.empty_cache()
     out["hbm"] = step_hbm(args.config, out["ms_per_step"], math, wl)
-    if world == 1 and len(batches) == 1 and not args.no_kernel_table:
-        out["kernels"] = kernel_table(trainer, step_in, S, Ne, Nn, math, args.config, wl)
+    if table and not args.no_kernel_table:
+        out["kernels"] = table
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
@@ -463,38 +530,25 @@ def run_train(args, cfg, world, rank, device):
         dist.destroy_process_group()
 
 
-def kernel_table(trainer, step_in, S, Ne, Nn, math, config, wl, steps=2):
-    """Every timed kernel's roofline in the same run (after the timed region): `steps` extra training
-    steps per kernel with HIP events around each of its launches (the library's prof hook takes one
-    kernel id per call). Per kernel: mean launch ms, ms per step, achieved TFLOP/s, frac of the math's
-    matrix peak, measured HBM bytes per launch from the committed PMC summary of this workload."""
+def kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, config, wl, steps=2, names=None):
+    """Every timed kernel's roofline in the same run: `steps` extra (untimed) training steps per kernel
+    with HIP events around each of its launches (the library's prof hook takes one kernel id per call).
+    Per kernel: launches and ms per step, mean launch ms, achieved TFLOP/s, frac of the math's matrix
+    peak, measured HBM bytes per launch from the committed PMC summary of this workload."""
     table = {}
-    for name, (kid, _) in KERNELS.items():
-        per = LAUNCHES_PER_STEP[name]
-        n = (S if per == "S" else per) * steps
-        ev = HipEvents(2 * n)
-        trainer.prof_kernel = kid
-        pstep = n // steps
-        for k in range(steps):
-            trainer.prof_events = ev.ev[2 * pstep * k: 2 * pstep * (k + 1)]
-            trainer.step(*step_in)
-        torch.cuda.synchronize()
-        try:
-            ms = [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(n)]
-        except RuntimeError:   # kernel not launched by this configuration (no events recorded)
-            ms = []
-        ev.close()
+    for name in names or KERNELS:
+        kid = KERNELS[name][0]
+        ms, per_step, _ = timed_steps(trainer, step_in, kid, n_micro, steps, MAX_LAUNCHES)
         if not ms:
-            continue
-        r = roofline(name, ms, Ne, Nn, S, math, config, wl)
-        table[name] = {"avg_launch_ms": r["avg_launch_ms"], "ms_per_step": round(r["avg_launch_ms"] * pstep, 4),
-                       "tflops": r["achieved"], "frac": r["frac"], "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
-    trainer.prof_kernel = 0
-    trainer.prof_events = None
+            continue   # kernel not launched by this configuration / math
+        r = roofline(name, ms, per_step, Ne, Nn, S, math, config, wl)
+        table[name] = {"launches_per_step": per_step, "avg_launch_ms": r["avg_launch_ms"],
+                       "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
+                       "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
     return table
 
 
-def _micro_step(trainer, batches, targets, evs, per_mb):
+def _micro_step(trainer, batches, targets, n_global, evs, per_mb):
     """Trainer.step over micro-batches with the timed kernel's events handed to each micro-batch's
     launches (the library records at most prof_count pairs per call)."""
     orig = trainer.run_config
@@ -507,7 +561,7 @@ def _micro_step(trainer, batches, targets, evs, per_mb):
     trainer_kid = [trainer.prof_kernel]
     trainer.run_config = rc
     try:
-        return trainer.step(batches, targets)
+        return trainer.step(batches, targets, n_global)
     finally:
         trainer.run_config = orig
 
@@ -520,7 +574,7 @@ def run_infer(args, cfg, world, rank, device):
     over the library's launches on the capture stream) and replayed; weak scaling, replicas."""
     from spwgnn_amd import engine as E
     B, N, S, math = cfg["towers"], cfg["nodes"], cfg["S"], cfg["math"]
-    raw = D.synthetic_towers(B, N, seed=5000 + rank)
+    raw = D.synthetic_towers_fast(B, N, seed=5000 + rank)
     batch = TowerBatch.fully_connected((raw / D.RELATION_THRESHOLD).astype(np.float32), device=device)
     params = P.to_flat(P.glorot_uniform(0), device=device)
     run = E.RunConfig(S, training=False, math=math)
@@ -537,18 +591,31 @@ def run_infer(args, cfg, world, rank, device):
     for _ in range(args.warmup):
         graph.replay()
     torch.cuda.synchronize()
-    # dominant kernel timed with HIP events on un-captured passes (same stream, same launches)
-    kname = args.roofline_kernel or "edge_fwd"
-    kid = KERNELS[kname][0]
-    per = S if LAUNCHES_PER_STEP[kname] == "S" else 1
-    kern_ms = []
-    for _ in range(3):
-        ev = HipEvents(2 * per)
-        prun = E.RunConfig(S, training=False, math=math, prof_kernel=kid, prof_events=ev.ev)
-        E.forward(params, batch, prun, ws, logits=z)
+    # every forward kernel timed with HIP events on un-captured passes (same stream, same launches);
+    # the roofline names the dominant one (largest ms per forward)
+    Ne, Nn = batch.n_edges, batch.n_nodes
+    wl = workload_name(cfg, world, 0.0)
+    table, times = {}, {}
+    for name in INFER_KERNELS:
+        ev = HipEvents(2 * MAX_LAUNCHES * 3)
+        for k in range(3):
+            evs = ev.ev[2 * MAX_LAUNCHES * k: 2 * MAX_LAUNCHES * (k + 1)]
+            prun = E.RunConfig(S, training=False, math=math, prof_kernel=KERNELS[name][0], prof_events=evs)
+            E.forward(params, batch, prun, ws, logits=z)
         torch.cuda.synchronize()
-        kern_ms += [ev.elapsed_ms(2 * i, 2 * i + 1) for i in range(per)]
+        ms = recorded_ms(ev, MAX_LAUNCHES * 3)
         ev.close()
+        if not ms:
+            continue
+        r = roofline(name, ms, len(ms) // 3, Ne, Nn, S, math, 5, wl)
+        times[name] = ms
+        table[name] = {"launches_per_step": len(ms) // 3, "avg_launch_ms": r["avg_launch_ms"],
+                       "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
+                       "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
+    kname = args.roofline_kernel or max(table, key=lambda k: table[k]["ms_per_step"])
+    if kname not in times:
+        raise SystemExit(f"kernel {kname} is not launched by the inference forward")
+    kern_ms = times[kname]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -563,18 +630,19 @@ def run_infer(args, cfg, world, rank, device):
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
-    Ne, Nn = batch.n_edges, batch.n_nodes
-    wl = workload_name(cfg, world, 0.0)
     out = {
         "metric": INFER_METRIC, "value": round(world * B * args.steps / el, 1), "unit": "towers/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16" if math == "bf16" else "f32", "math": MATH_DESC[math],
         "data": "synthetic (Jenga-geometry towers, glorot weights)",
-        "config": {"workload": wl, "baseline_config": 5, "towers_per_gpu": B, "global_batch": B * world,
+        "config": {"workload": wl, "baseline_config": 5, "towers_per_gpu": B, "global_batch": cfg["towers"] * world,
                    "nodes_per_tower": N, "mp_steps": S, "math": math, "parallelism": f"replicas{world}"},
         "step_tflops": round(fwd_flops(Ne, Nn, S) * world * args.steps / el / 1e12, 2),
-        "roofline": roofline(kname, kern_ms, Ne, Nn, S, math, 5, wl),
+        "roofline": dict(roofline(kname, kern_ms, len(kern_ms) // 3, Ne, Nn, S, math, 5, wl),
+                         selected="--roofline-kernel" if args.roofline_kernel else
+                         "dominant: largest ms per forward in this run's kernel table"),
+        "kernels": table,
         "cpu_baseline": None,
     }
     out["hbm"] = step_hbm(5, out["ms_per_step"], math, wl)

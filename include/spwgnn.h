@@ -53,7 +53,7 @@ int32_t spwgnn_param_tensor(int32_t index, spwgnn_param_info* out);
 
 /* ------------------------------------------------------------- host-side input builders -- */
 /* Dense relation matrices → compact edge list. Replaces the one-hot batch_dot gathers of
- * Networks.py:27-33/:174-175 and the segment-sum of :178 at the input boundary: a column k
+ * Networks.py:27-33/:84-85 and the segment-sum of :88 at the input boundary: a column k
  * of (Rs, Rr) that is one-hot in both is edge k (sender, receiver); an all-zero column is an
  * inactive relation (it never reaches an output, Networks.py:88); a column one-hot in Rs only
  * also never reaches an output and is dropped; anything else → SPWGNN_E_RELATION.
@@ -134,6 +134,9 @@ typedef struct spwgnn_run {
 #define SPWGNN_K_ENC_EDGE_BWD 6
 #define SPWGNN_K_WGRAD_W2 7
 #define SPWGNN_K_DA 8          /* dA = Σ_s dh1pre_s rebuilt after the backward step loop (bf16 math) */
+#define SPWGNN_K_WGRAD_WS 9    /* every stored-operand weight gradient (k_wgrad_ws family, split-bf16 maths) */
+#define SPWGNN_K_ENC_NODE 10
+#define SPWGNN_K_ENC_NODE_BWD 11
 
 /* Workspace bytes for (n_nodes, n_eblocks, mp_steps, training). */
 int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training);

@@ -52,3 +52,24 @@ def object_mask(seed: int, rate: float, B: int, N: int):
     k = row_key(seed, 2, tw, np.tile(np.arange(N), B), np.full(B * N, 0xFFFF))
     scale = np.float32(1.0) / (np.float32(1.0) - np.float32(rate))
     return (keep(k, 100, rate).astype(np.float32) * scale).reshape(B, N, 100)
+
+
+def relation_mask_towers(seed: int, rate: float, tower_ids, N: int):
+    """(T, E, 150) relation masks of fully connected N-box towers with the given batch tower ids
+    (the engine keys a mask by the tower's id, so a sub-batch cut with `tower_ids` reproduces the
+    whole batch's masks for its towers)."""
+    tower_ids = np.asarray(tower_ids)
+    m_idx, j_idx = np.nonzero(~np.eye(N, dtype=bool))
+    tw = np.repeat(tower_ids, len(m_idx))
+    k = row_key(seed, 1, tw, np.tile(m_idx, len(tower_ids)), np.tile(j_idx, len(tower_ids)))
+    scale = np.float32(1.0) / (np.float32(1.0) - np.float32(rate))
+    return (keep(k, 150, rate).astype(np.float32) * scale).reshape(len(tower_ids), len(m_idx), 150)
+
+
+def object_mask_towers(seed: int, rate: float, tower_ids, N: int):
+    """(T, N, 100) object masks for the given batch tower ids."""
+    tower_ids = np.asarray(tower_ids)
+    tw = np.repeat(tower_ids, N)
+    k = row_key(seed, 2, tw, np.tile(np.arange(N), len(tower_ids)), np.full(len(tower_ids) * N, 0xFFFF))
+    scale = np.float32(1.0) / (np.float32(1.0) - np.float32(rate))
+    return (keep(k, 100, rate).astype(np.float32) * scale).reshape(len(tower_ids), N, 100)

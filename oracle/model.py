@@ -16,7 +16,7 @@ tests, and (d) committed self-generated golden vectors (``tests/golden``).
 Reference anchors (``/root/reference/src``):
   * inputs & layout ............ Networks.py:22-29 (objects, sender/receiver relations, propagation)
   * endpoint gathers ........... Networks.py:32-33  senders = Rsᵀ·objects, receivers = Rrᵀ·objects
-  * feature slicing ............ Networks.py:35-37, 148-163  d = r_pos − s_pos; o = (y, width)
+  * feature slicing ............ Networks.py:35-37, 58-71  d = r_pos − s_pos; o = (y, width)
   * MLP blocks ................. Blocks.py:20-28, 60-68  Dense(relu)…, last Dense(linear)
   * MLP sizes .................. Networks.py:46-50  rm 2→150³→150, om 2→100→100,
                                                      rmp 350→150→150→100, omp 300→100→101
@@ -40,7 +40,7 @@ MLP_SPECS: Dict[str, Tuple[int, List[int]]] = {
     "rmp": (350, [150, 150, 100]),
     "omp": (300, [100, 101]),
 }
-STATE_DIM = 100          # Networks.py:29 / :170 ('propagation' width, "100 is the layer size")
+STATE_DIM = 100          # Networks.py:29 / :80 ('propagation' width, "100 is the layer size")
 REF_MP_STEPS = 5         # Networks.py:83
 DROPOUT_RATE = 0.1       # Networks.py:77-78
 RELATION_THRESHOLD = 170.0  # main.py:71 / :91

@@ -42,6 +42,7 @@ class RunC(C.Structure):
 
 
 K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WGRAD_W2, K_DA = 1, 2, 3, 4, 5, 6, 7, 8
+K_WGRAD_WS, K_ENC_NODE, K_ENC_NODE_BWD = 9, 10, 11
 MATH_F32, MATH_X6, MATH_BF16 = 0, 1, 2
 READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 

@@ -100,9 +100,11 @@ class TowerBatch:
     # ------------------------------------------------------------------ constructors
     @staticmethod
     def from_edges(pos: np.ndarray, tower_nodes, src, dst, tower_edges, prop=None, device="cuda",
-                   nw_max: Optional[int] = None, node_shape=None) -> "TowerBatch":
+                   nw_max: Optional[int] = None, node_shape=None, tower_ids=None) -> "TowerBatch":
         """pos (Nn, >=3) objects rows (already /170); towers are consecutive node ranges;
-        edges tower-major with global node ids."""
+        edges tower-major with global node ids. `tower_ids` (T,): each tower's index in the batch it
+        was cut from (the dropout masks are keyed by it), so a shard or micro-batch of a larger batch
+        draws the masks the whole batch would; default 0..T-1."""
         L = _lib.lib()
         tower_nodes = np.ascontiguousarray(tower_nodes, dtype=np.int32)
         tower_edges = np.ascontiguousarray(tower_edges, dtype=np.int32)
@@ -130,7 +132,10 @@ class TowerBatch:
         _lib.check(L.spwgnn_plan_fill(T, _ptr(tower_nodes), _ptr(tower_edges), _ptr(src) if len(src) else None,
                                       _ptr(dst) if len(dst) else None, nw_max, C.byref(sizes), _ptr(wtile),
                                       _ptr(esrc), _ptr(edst), _ptr(eid), _ptr(csr)), "plan_fill")
-        node_tower = np.repeat(np.arange(T, dtype=np.int32), tower_nodes)
+        tid = np.arange(T, dtype=np.int32) if tower_ids is None else np.asarray(tower_ids, np.int64)
+        if len(tid) != T or (T and (tid.min() < 0 or tid.max() > np.iinfo(np.int32).max)):
+            raise ValueError("tower_ids must hold one non-negative int32 id per tower")
+        node_tower = np.repeat(tid.astype(np.int32), tower_nodes)
         starts = np.concatenate([[0], np.cumsum(tower_nodes)[:-1]]).astype(np.int64)
         node_local = (np.arange(Nn) - np.repeat(starts, tower_nodes)).astype(np.int32)
         pos4 = np.zeros((Nn, 4), np.float32)
@@ -174,7 +179,8 @@ class TowerBatch:
                                      device, nw_max, node_shape=(B, N))
 
     @staticmethod
-    def fully_connected(objects: np.ndarray, propagation=None, device="cuda", nw_max=None) -> "TowerBatch":
+    def fully_connected(objects: np.ndarray, propagation=None, device="cuda", nw_max=None,
+                        tower_ids=None) -> "TowerBatch":
         """Fast path for (B, N, 3) towers whose relations are all active (the inference relation
         set of JengaBuilder.py:309-326 and the benchmark configs)."""
         obj = np.asarray(objects, np.float32)
@@ -185,7 +191,8 @@ class TowerBatch:
         dst = (base + j_idx[None, :]).reshape(-1).astype(np.int32)
         prop = None if propagation is None else np.asarray(propagation, np.float32).reshape(B * N, 100)
         return TowerBatch.from_edges(obj.reshape(B * N, 3), np.full(B, N, np.int32), src, dst,
-                                     np.full(B, N * (N - 1), np.int32), prop, device, nw_max, node_shape=(B, N))
+                                     np.full(B, N * (N - 1), np.int32), prop, device, nw_max, node_shape=(B, N),
+                                     tower_ids=tower_ids)
 
     @staticmethod
     def ragged(objects_list, relation_threshold: Optional[float] = None, device="cuda", nw_max=None,

@@ -359,7 +359,12 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.thresh = thresh;
     en.scale = scale;
     en.seed = r->seed;
-    SPW_CHECK(launch_enc_node(en, r->math, st));
+    {
+        Prof pn{r, st};
+        SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
+        SPW_CHECK(launch_enc_node(en, r->math, st));
+        SPW_CHECK(pn.after(SPWGNN_K_ENC_NODE));
+    }
 
     EncEdgeArgs ee{};
     ee.n_eblocks = b->n_eblocks;
@@ -556,9 +561,9 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         wgs = (nst + wa.stages_per_wg - 1) / wa.stages_per_wg;
         chunks = wgs;
         const bool mask = !(g.kx_pad == 160 && g.ny_pad == 160);   // node arrays: rows ≥ count masked
-        if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
+        if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_WS));
         SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, math, st, g.b16));
-        if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
+        if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_WS));
     } else {
     // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
     const bool ws = g.recompute && math != MATH_F32 && (math == MATH_BF16 || !getenv_flag("SPWGNN_W2G_OLD"));
@@ -569,7 +574,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         bpw = (nblk + wgs - 1) / wgs;
         chunks = (nblk + bpw - 1) / bpw;
     }
-    if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
+    if (prof && g.recompute) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
     if (ws)
         SPW_CHECK(launch_w2grad_ws(a, (int)chunks, bpw, math, st));
     else if (math == MATH_BF16)
@@ -578,7 +583,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         return SPWGNN_E_ARG;
     else
         SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
-    if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
+    if (prof && g.recompute) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     }
     const ParamTable& pt = param_table();
     ReduceArgs& ra = rb.r[rb.n++];
@@ -753,7 +758,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         enb.x_wo1ct = c.x6(X6_WO1CT);
         enb.x_om1t = c.x6(X6_OM1T);
     }
+    SPW_CHECK(prof.before(SPWGNN_K_ENC_NODE_BWD));
     SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), st));
+    SPW_CHECK(prof.after(SPWGNN_K_ENC_NODE_BWD));
 
     // ---- weight gradients ----
     const int64_t RE = w.RE, RN = w.RN;
@@ -770,7 +777,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
         g.b16 = b16 ? kB16Y : 0;   // Y = dz1
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
@@ -782,12 +789,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.b0 = c.pk(PB_RM0);
         }
         g.b16 = b16 ? kB16Y : 0;   // X rebuilt from d; Y = dz2
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     const int b16xy = b16 ? (kB16X | kB16Y) : 0;
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
         // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
@@ -807,17 +814,17 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
@@ -827,28 +834,28 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.rows = nN;
             g.y_stride = 0;
         }
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)
         WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
@@ -859,7 +866,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.b0 = c.pk(PB_OM0);
         }
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
     SPW_CHECK(launch_wgrad_reduce_all(rb, st));
     return SPWGNN_OK;

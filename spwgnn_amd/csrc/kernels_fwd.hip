@@ -579,7 +579,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 //   a  = tanh([H2s | deg]·[W3; b3])              (Networks.py:88, layer 3 after the sum)
 //   o1 = relu([c_o | a | P]·Wo1 + bo1)            (Networks.py:89-90, omp layer 1)
 //   x' = o1·Wo2' + bo2'   (x' = x with the logit moved to column 100)
-//   P' = tanh(x'[0:100] + P); logit = x'[100]     (Networks.py:91, 184)
+//   P' = tanh(x'[0:100] + P); logit = x'[100]     (Networks.py:91, 94)
 //   U' = P'·W1b, V' = P'·W1c for the next step
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node_fwd(NodeFwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;

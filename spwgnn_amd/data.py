@@ -77,6 +77,120 @@ def synthetic_towers(n_towers: int, n_objects: int, seed: int = 0, remove_one: b
     return out
 
 
+def _draw(u: np.ndarray, lo: int, hi: int) -> np.ndarray:
+    """randint(lo, hi) inclusive from uniforms in [0, 1)."""
+    return lo + np.minimum(np.floor(u * (hi - lo + 1)), hi - lo).astype(np.int64)
+
+
+def draws_per_tower(n_objects: int) -> int:
+    """Upper bound on the random draws one tower of `n_objects` (+1 removed) consumes below: per box
+    a width and a gap, per layer one width, plus one x offset and the removal index."""
+    return 4 * (n_objects + 1) + 4
+
+
+def jenga_towers_from_draws(u: np.ndarray, n_objects: int, remove_one: bool = True) -> np.ndarray:
+    """Vectorised `jenga_tower` over T towers at once: (T, n_objects, 3) raw-pixel [x, y, w].
+
+    Each tower t consumes its own row u[t] of uniforms in [0, 1) strictly in order (counter c[t]),
+    in the same sequence the scalar builder draws (JengaBuilder.py:159-184: layer width, then per
+    box the gap and the next width; a one-box layer below draws the x offset, then the width), so
+    the scalar `jenga_tower` fed one row gives the same tower. All towers advance in lockstep: each
+    iteration either opens a layer or places/ends one box of the open layer."""
+    T = u.shape[0]
+    n_build = n_objects + (1 if remove_one else 0)
+    ar = np.arange(T)
+    c = np.zeros(T, np.int64)
+
+    def take(lo, hi, m):
+        v = _draw(u[ar[m], c[m]], lo, hi)
+        c[m] += 1
+        return v
+
+    out = np.zeros((T, n_build, 3))
+    placed = np.zeros(T, np.int64)
+    layer = np.full(T, -1, np.int64)
+    in_layer = np.zeros(T, bool)               # a multi-box layer is open
+    cnt = np.zeros(T, np.int64)                # boxes in the open layer
+    prev_min = np.zeros(T)
+    prev_max = np.zeros(T)
+    cur_min = np.full(T, np.inf)
+    cur_max = np.full(T, -np.inf)
+    left = np.zeros(T)
+    right = np.zeros(T)
+    w = np.zeros(T)
+    y = np.zeros(T)
+
+    def place(m, x, yy, ww):
+        i = np.nonzero(m)[0]
+        out[i, placed[i], 0] = x
+        out[i, placed[i], 1] = yy
+        out[i, placed[i], 2] = ww
+        placed[i] += 1
+        cur_min[i] = np.minimum(cur_min[i], x)
+        cur_max[i] = np.maximum(cur_max[i], x)
+
+    while True:
+        todo = placed < n_build
+        if not todo.any():
+            break
+        # ---- open a layer
+        op = todo & ~in_layer
+        if op.any():
+            layer[op] += 1
+            first = op & (layer == 0)
+            later = op & (layer > 0)
+            prev_min[later], prev_max[later] = cur_min[later], cur_max[later]
+            right[first], left[first] = RIGHT_MOST, LEFT_MOST
+            right[later], left[later] = prev_max[later], prev_min[later]
+            cur_min[op], cur_max[op] = np.inf, -np.inf
+            y[op] = BOTTOM_EDGE + RECT_HEIGHT / 2 + RECT_HEIGHT * layer[op]
+            single = op & (right == left)
+            if single.any():                   # JengaBuilder.py:159-167
+                xs = left[single]
+                x = (np.floor(xs - RECT_WIDTH_MIN / 2) + take(0, RECT_WIDTH_MIN, single)).astype(np.float64)
+                ww = take(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE, single).astype(np.float64)
+                place(single, x, BOTTOM_EDGE + int(RECT_HEIGHT / 2) + RECT_HEIGHT * layer[single], ww)
+                # the layer is complete (stays closed): next iteration opens the next one
+            multi = op & ~single
+            if multi.any():                    # JengaBuilder.py:171-173
+                left[multi] -= (layer[multi] > 0) * int(RECT_WIDTH_AVERAGE / 2)
+                w[multi] = take(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE, multi)
+                left[multi] += w[multi]
+                in_layer[multi] = True
+                cnt[multi] = 0
+            continue
+        # ---- one step of the open layers: place a box or close the layer (JengaBuilder.py:174-184)
+        go = todo & in_layer & (left - w / 2 < right)
+        if go.any():
+            place(go, left[go] - w[go] / 2, y[go], w[go].copy())
+            cnt[go] += 1
+            # the scalar loop draws the gap and the next width even after its last box
+            left[go] += take(0, MAX_SPACE_RECTS, go)
+            w[go] = take(RECT_WIDTH_MIN, RECT_WIDTH_MIN + RECT_WIDTH_RANGE, go)
+            left[go] += w[go]
+            in_layer[go & (placed >= n_build)] = False
+        stop = todo & in_layer & ~go
+        if stop.any():
+            empty = stop & (cnt == 0)
+            if empty.any():                    # first box wider than the narrow layer below
+                place(empty, (left[empty] - w[empty] + right[empty]) / 2, y[empty], w[empty].copy())
+            in_layer[stop] = False
+    if not remove_one:
+        return out
+    r = take(0, n_build - 1, np.ones(T, bool))
+    keep = np.ones((T, n_build), bool)
+    keep[ar, r] = False
+    return out[keep].reshape(T, n_objects, 3)
+
+
+def synthetic_towers_fast(n_towers: int, n_objects: int, seed: int = 0, remove_one: bool = True) -> np.ndarray:
+    """`synthetic_towers`' geometry for large batches: (B, N, 3) raw-pixel towers from a numpy
+    uniform table, built by the vectorised lockstep builder (≈ 100× faster than the per-tower loop;
+    a different random stream, the same distribution)."""
+    u = np.random.default_rng(seed).random((n_towers, draws_per_tower(n_objects)))
+    return jenga_towers_from_draws(u, n_objects, remove_one)
+
+
 def relation_matrices(boxes_raw: np.ndarray, threshold: Optional[float] = RELATION_THRESHOLD):
     """Dense sender/receiver one-hot matrices (B, N, E), E = N(N-1), exactly as main.py:66-81
     (threshold on raw-pixel frame-0 distance) — vectorised over towers and slots.
@@ -148,7 +262,8 @@ def ragged_batch(n_towers: int, n_min: int, n_max: int, seed: int = 0,
 
     Returns the compact edge form `TowerBatch.from_edges` takes: (pos (Nn, 3) f32, tower_nodes (T,),
     src (Ne,), dst (Ne,), tower_edges (T,), raw (list of (N_t, 3) pixel arrays)). Edges are tower-major
-    and sender-major inside a tower (the slot order of main.py:72-81). Vectorised per tower size."""
+    and sender-major inside a tower (the slot order of main.py:72-81). Vectorised per tower size
+    (geometry from `synthetic_towers_fast`: 2^20 towers build in seconds)."""
     rng = np.random.default_rng(seed)
     sizes = rng.integers(n_min, n_max + 1, size=n_towers).astype(np.int32)
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
@@ -159,7 +274,7 @@ def ragged_batch(n_towers: int, n_min: int, n_max: int, seed: int = 0,
         idx = np.nonzero(sizes == n)[0]
         if len(idx) == 0:
             continue
-        raw = synthetic_towers(len(idx), n, seed=seed * 1000 + n)
+        raw = synthetic_towers_fast(len(idx), n, seed=seed * 1000 + n)
         rows = off[idx][:, None] + np.arange(n)[None, :]
         pos[rows.reshape(-1)] = (raw / RELATION_THRESHOLD).reshape(-1, 3)
         for j, t in enumerate(idx):

@@ -6,6 +6,7 @@ arithmetic happens in libspwgnn_hip.so. Nothing here falls back to CPU.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -65,11 +66,20 @@ class Workspace:
         self.device = torch.device(device)
         self.buf: Optional[torch.Tensor] = None
         self.fwd_key: Optional[tuple] = None   # what the last forward on this workspace stored
+        self.fwd_batch = None                  # weakref to the batch that forward ran on
 
     @staticmethod
     def key(batch: TowerBatch, run: "RunConfig") -> tuple:
+        # sizes and run fields, plus the device arrays the stored activations were computed from:
+        # two same-shape batches (equal micro-batches under one seed) must not pass for each other
         return (run.math, int(run.mp_steps), bool(run.training), float(run.dropout), int(run.seed),
-                batch.n_nodes, batch.n_eblocks, batch.n_wtiles)
+                batch.n_nodes, batch.n_eblocks, batch.n_wtiles, batch.pos.data_ptr(), batch.edge_src.data_ptr(),
+                batch.prop.data_ptr() if batch.prop is not None else 0)
+
+    def holds(self, batch: TowerBatch, run: "RunConfig") -> bool:
+        """True when the last forward on this workspace ran `batch` (the same object) with `run`."""
+        return (self.buf is not None and self.fwd_batch is not None and self.fwd_batch() is batch
+                and self.fwd_key == Workspace.key(batch, run))
 
     def get(self, nbytes: int) -> torch.Tensor:
         if self.buf is None or self.buf.numel() < nbytes:
@@ -99,6 +109,7 @@ def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Wo
     st = _lib.lib().spwgnn_forward(flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(),
                                    logits.data_ptr(), _stream(batch.device))
     ws.fwd_key = Workspace.key(batch, run) if st == 0 else None
+    ws.fwd_batch = weakref.ref(batch) if st == 0 else None
     _lib.check(st, "spwgnn_forward")
     return logits
 
@@ -107,7 +118,7 @@ def backward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: W
              grads: Optional[torch.Tensor] = None, want_dprop: bool = False):
     if not run.training:
         raise _lib.SpwgnnError("backward needs a training forward on the same workspace")
-    if ws.buf is None or ws.fwd_key != Workspace.key(batch, run):
+    if not ws.holds(batch, run):
         # the backward reads what the forward stored (masks, activations, packed weights); the split-
         # bf16 maths do not store z1/zo1 at all, so a mismatched math or step count reads garbage
         raise _lib.SpwgnnError("backward needs the training forward of the same batch and RunConfig "

@@ -2,7 +2,7 @@
 
 Mirrors the reference call sites one-to-one so a driver written against the reference drops in:
   * PropagationNetwork().getModel(n_objects, object_dim=3, relation_dim=1)  — Networks.py:12-104
-    (one model per n_objects, cached; all models share rm/om/rmp/omp weights, :107-108, :130-146)
+    (one model per n_objects, cached at Networks.py:17-18,103; all models share rm/om/rmp/omp weights, :40-56)
   * model.fit(x_dict, {'target': y}, batch_size=32, epochs=10, validation_split=0.2, shuffle=True,
     verbose=1)                                                            — main.py:92-98
   * model.predict(x_dict) → (B, N, 1) probabilities                       — JengaBuilder.py:328-329

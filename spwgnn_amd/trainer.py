@@ -29,6 +29,27 @@ from . import engine as E
 from .batch import TowerBatch
 
 
+_M64 = (1 << 64) - 1
+
+
+def splitmix64(x: int) -> int:
+    """One splitmix64 output step (Steele et al.): a bijective 64-bit mix."""
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def dropout_key(seed: int, iteration: int, rank: int, micro: int) -> int:
+    """The run's 64-bit dropout key for (seed, optimizer step, rank, micro-batch): each field is
+    folded through splitmix64 in turn, so no field overflows into the next (a packed
+    ((seed·P + it)·R + rank)·M + micro key collides once rank ≥ R or micro ≥ M)."""
+    h = splitmix64(seed & _M64)
+    for v in (iteration, rank, micro):
+        h = splitmix64(h ^ (v & _M64))
+    return h
+
+
 class HipEngine:
     def __init__(self, device):
         self.device = torch.device(device)
@@ -74,13 +95,15 @@ class Trainer:
 
     def run_config(self, micro: int = 0) -> E.RunConfig:
         # distinct dropout keys per step, per rank and per micro-batch (different towers)
-        key = ((self.seed * 1_000_003 + self.iterations) * 4099 + self.rank) * 257 + micro
+        key = dropout_key(self.seed, self.iterations, self.rank, micro)
         return E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, seed=key, math=self.math,
                            prof_kernel=self.prof_kernel, prof_events=self.prof_events)
 
     def step(self, batch, target, n_global: Optional[int] = None):
         """One optimizer step. `batch`/`target` may be lists (micro-batches of this rank's shard);
-        `n_global` = nodes in the whole global batch (all ranks, all micro-batches)."""
+        `n_global` = nodes in the whole global batch (all ranks, all micro-batches). Returns one
+        [loss, correct, n] device tensor for this rank's shard: the node-weighted mean BCE over its
+        micro-batches, the binary_accuracy numerator and the node count."""
         batches = batch if isinstance(batch, (list, tuple)) else [batch]
         targets = target if isinstance(target, (list, tuple)) else [target]
         if len(batches) != len(targets) or not batches:
@@ -95,13 +118,16 @@ class Trainer:
                 n_global = int(t.item())
         run = self.run_config()
         acc = None
-        outs = []
+        tot3 = None
         for i, (b, tg) in enumerate(zip(batches, targets)):
             if i:
                 run = self.run_config(micro=i)
             z = self.engine.forward(self.params, b, run)
             out3, dz = self.engine.loss(z, tg)
-            outs.append(out3)
+            # [loss, correct, n] of this micro-batch, folded in before the engine reuses its buffer:
+            # Σ loss_i·n_i, Σ correct_i, Σ n_i (the engine's out3 is one persistent tensor)
+            w3 = out3.double() * out3.new_tensor([float(b.n_nodes), 1.0, 1.0], dtype=torch.float64)
+            tot3 = w3 if tot3 is None else tot3 + w3
             g = self.engine.backward(self.params, b, run, dz)
             w = b.n_nodes / n_global
             if len(batches) == 1:
@@ -117,4 +143,5 @@ class Trainer:
         self.iterations += 1
         self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
                          self.l2, 1.0)
-        return outs[0] if len(outs) == 1 else outs
+        # node-weighted mean loss of this rank's shard, total correct, total nodes (device, fp32)
+        return torch.stack([tot3[0] / tot3[2], tot3[1], tot3[2]]).float()

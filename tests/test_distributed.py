@@ -212,3 +212,64 @@ def test_plan_shards_balances_cost():
     n2 = np.array([16] * 100 + [4] * 100)
     r = plan_shards(n2, n2 * (n2 - 1), 2)
     assert r[0][1] < 100
+
+
+# ---------------------------------------------------------------- the bench's own DP workload path
+def _bench_cfg():
+    import bench
+    # BASELINE config 4 (ragged 4-16, thresholded, S=5, micro-batched) scaled to 5 towers per rank,
+    # micro-batches of 2: the same make_workload → plan_shards → micro_batches → Trainer path
+    cfg = dict(bench.CONFIGS[4], towers=5, micro=2, S=2)
+    return bench, cfg
+
+
+def _bench_worker(rank, world, port, steps, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench, cfg = _bench_cfg()
+    batches, targets, n_global = bench.make_workload(cfg, rank, "cpu", world)
+    params = P.to_flat(O.random_params(11), dtype=torch.float64)
+    tr = Trainer(params, engine=OracleEngine(), mp_steps=cfg["S"], dropout=0.0)
+    tr.m = torch.zeros_like(params)
+    tr.v = torch.zeros_like(params)
+    for _ in range(steps):
+        out3 = tr.step([b for b in batches], [t.double() for t in targets], n_global)
+    assert abs(float(out3[2]) - sum(b.n_nodes for b in batches)) < 1e-9
+    np.save(out + f".{rank}.npy", params.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_workload_dp_gloo_world2_equals_single_process(tmp_path):
+    """bench.make_workload at world 2: both ranks build the same global ragged batch (one seed), cut it
+    with shard.plan_shards and take n_global from the plan (no node-count all-reduce); the DP step over
+    the two shards' micro-batches equals the single-process step on the whole global batch."""
+    out = str(tmp_path / "p")
+    mp.start_processes(_bench_worker, args=(2, _free_port(), 2, out), nprocs=2, join=True, start_method="spawn")
+    bench, cfg = _bench_cfg()
+    single = dict(cfg, towers=10)                 # the same 10-tower global batch in one process
+    batches, targets, n_global = bench.make_workload(single, 0, "cpu", 1)
+    assert n_global == sum(b.n_nodes for b in batches)
+    params = P.to_flat(O.random_params(11), dtype=torch.float64)
+    tr = Trainer(params, engine=OracleEngine(), mp_steps=cfg["S"], dropout=0.0)
+    tr.m = torch.zeros_like(params)
+    tr.v = torch.zeros_like(params)
+    for _ in range(2):
+        tr.step(batches, [t.double() for t in targets], n_global)
+    for r in range(2):
+        assert np.abs(np.load(out + f".{r}.npy") - params.numpy()).max() < 1e-9
+    # and the plan really split the global batch: both ranks hold towers
+    w0 = bench.make_workload(cfg, 0, "cpu", 2)
+    w1 = bench.make_workload(cfg, 1, "cpu", 2)
+    assert sum(b.n_towers for b in w0[0]) + sum(b.n_towers for b in w1[0]) == 10
+    assert min(sum(b.n_towers for b in w[0]) for w in (w0, w1)) >= 1 and w0[2] == w1[2] == n_global
+
+
+def test_dropout_key_fields_do_not_collide():
+    """Trainer dropout keys: distinct for every (step, rank, micro) combination, including ranks and
+    micro indices past the field widths of the old packed key (4099 ranks, 257 micro-batches)."""
+    from spwgnn_amd.trainer import dropout_key
+    keys = {dropout_key(7, it, rank, micro) for it in (0, 1) for rank in (0, 1, 4098, 4099, 4100)
+            for micro in (0, 1, 256, 257, 258)}
+    assert len(keys) == 2 * 5 * 5
+    assert dropout_key(7, 0, 0, 257) != dropout_key(7, 0, 1, 0)

@@ -228,13 +228,16 @@ def test_plan_rejects_cross_tower_edge_inside_one_packed_tile():
     assert ok.n_wtiles == 1
 
 
-@pytest.mark.parametrize("B,v", [(7, 0.2), (13, 0.2), (10, 0.2), (96, 0.25), (5, 0.0), (3, 0.5)])
-def test_keras_validation_split_matches_keras2(B, v):
+# (B, validation_split) → training samples, worked by hand from Keras 2.x's
+# split_at = int(num_train_samples * (1. - validation_split)):
+#   7·0.8 = 5.6 → 5; 13·0.8 = 10.4 → 10; 10·0.8 = 8.000000000000002 → 8; 96·0.75 = 72;
+#   5, v = 0 → 5 (no split); 3·0.5 = 1.5 → 1; 1000·0.8 = 800; 9·(1 − 0.1) = 8.1 → 8; 4·0.8 = 3.2 → 3
+@pytest.mark.parametrize("B,v,want", [(7, 0.2, 5), (13, 0.2, 10), (10, 0.2, 8), (96, 0.25, 72), (5, 0.0, 5),
+                                      (3, 0.5, 1), (1000, 0.2, 800), (9, 0.1, 8), (4, 0.2, 3)])
+def test_keras_validation_split_matches_keras2(B, v, want):
     """Keras 2.x fit: split_at = int(B·(1 − v)) training samples, the rest is validation (main.py:96)."""
     from spwgnn_amd.keras_api import keras_split_at
-    assert keras_split_at(B, v) == (int(int(B) * (1.0 - v)) if v else B)
-    if (B, v) == (7, 0.2):
-        assert keras_split_at(B, v) == 5
+    assert keras_split_at(B, v) == want
 
 
 def test_ragged_batch_matches_per_tower_relations():
@@ -282,3 +285,33 @@ def test_batch_upload_roundtrip_cpu():
     out = upload(arrs, "cpu")
     for a, t in zip(arrs, out):
         assert t.shape == a.shape and np.array_equal(t.numpy(), a)
+
+
+class _UniformRandint:
+    """random.Random stand-in for `jenga_tower`: randint(a, b) from a row of uniforms, in order."""
+
+    def __init__(self, row):
+        self.row, self.k = row, 0
+
+    def randint(self, a, b):
+        v = a + min(int(np.floor(self.row[self.k] * (b - a + 1))), b - a)
+        self.k += 1
+        return v
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 6, 9, 12, 16, 32])
+def test_vectorised_jenga_builder_equals_scalar(n):
+    """data.jenga_towers_from_draws (the lockstep builder the benchmark's large batches use) gives,
+    tower for tower, what the scalar JengaBuilder.create_world restatement `jenga_tower` gives on the
+    same draws (JengaBuilder.py:150-184), including the removed box (JengaBuilder.py:223-233)."""
+    T = 300
+    u = np.random.default_rng(n).random((T, D.draws_per_tower(n)))
+    vec = D.jenga_towers_from_draws(u, n)
+    for t in range(T):
+        r = _UniformRandint(u[t])
+        tower = D.jenga_tower(n + 1, r)
+        tower = np.delete(tower, r.randint(0, len(tower) - 1), axis=0)
+        assert r.k <= u.shape[1]
+        np.testing.assert_array_equal(vec[t], tower)
+    fast = D.synthetic_towers_fast(64, n, seed=3)
+    assert fast.shape == (64, n, 3) and np.all(fast[..., 2] >= D.RECT_WIDTH_MIN)
