@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 from spwgnn_amd import _lib, params as P  # noqa: E402
 from spwgnn_amd import data as D  # noqa: E402
-from spwgnn_amd.batch import TowerBatch  # noqa: E402
+from spwgnn_amd.batch import HostPlan, TowerBatch  # noqa: E402
 from spwgnn_amd.trainer import Trainer  # noqa: E402
 
 METRIC = "towers/sec fwd+bwd, 6-block batch=65k, 1/2/4/8 MI355X; achieved HBM GB/s"
@@ -53,7 +53,7 @@ MATH_DESC = {"x6": "x6: each fp32 matrix product as 6 bf16 MFMA products of 3-wa
 # BASELINE.json configs (index = position + 1; 0 = the headline metric's configuration)
 CONFIGS = {
     0: dict(nodes=6, towers=65536, S=5, math="x6", relations="full", mode="train"),
-    1: dict(nodes=6, towers=32, S=1, math="x6", relations="threshold", mode="train"),
+    1: dict(nodes=6, towers=32, S=1, math="x6", relations="threshold", mode="train", replay=True),
     2: dict(nodes=6, towers=4096, S=3, math="x6", relations="threshold", mode="train"),
     3: dict(nodes=12, towers=65536, S=5, math="bf16", relations="full", mode="train"),
     4: dict(nodes=(4, 16), towers=131072, S=5, math="bf16", relations="threshold", mode="train", micro=65536),
@@ -122,9 +122,12 @@ class HipEvents:
 
     def elapsed_ms(self, a, b) -> float:
         ms = C.c_float()
-        self.hip.hipEventSynchronize(C.c_void_p(self.ev[b]))
+        s1 = self.hip.hipEventSynchronize(C.c_void_p(self.ev[b]))
         st = self.hip.hipEventElapsedTime(C.byref(ms), C.c_void_p(self.ev[a]), C.c_void_p(self.ev[b]))
-        if st != 0:
+        if st != 0 or s1 != 0:
+            # a pair the library did not record: HIP keeps the failure as the thread's last error,
+            # which the library's next launch check (hipGetLastError) would report as its own — clear it
+            self.hip.hipGetLastError()
             raise RuntimeError(f"hipEventElapsedTime failed ({st})")
         return ms.value
 
@@ -134,14 +137,15 @@ class HipEvents:
 
 
 # ------------------------------------------------------------------------------ workloads
-def make_workload(cfg: dict, rank: int, device, world: int = 1):
+def make_workload(cfg: dict, rank: int, device, world: int = 1, plans: bool = False):
     """This rank's part of the job's synthetic global batch and its targets.
 
     Every rank builds the same global batch of towers·world towers from one seed, cuts it with the
     cost planner `shard.plan_shards` (contiguous tower ranges of near-equal algorithmic cost; equal
     ranges for uniform towers) and keeps its own range, as micro-batches when the config has them.
     Returns (batches, targets, n_global): n_global = nodes in the whole global batch, taken from the
-    plan, so the Trainer needs no per-step all-reduce of node counts."""
+    plan, so the Trainer needs no per-step all-reduce of node counts. `plans`: host plans sized for
+    every relation slot (replayed steps, spwgnn_amd/replay.py) and host targets instead."""
     from spwgnn_amd import shard
     B, S = cfg["towers"] * world, cfg["S"]
     thr = D.RELATION_THRESHOLD if cfg["relations"] == "threshold" else None
@@ -167,6 +171,10 @@ def make_workload(cfg: dict, rank: int, device, world: int = 1):
     batches, targets = [], []
     for x, y in shard.micro_batches(a, b, cfg.get("micro") or max(b - a, 1)):
         part = D.edge_slice(pos, sizes, src, dst, te, x, y)
+        if plans:
+            batches.append(HostPlan.build(*part, edge_cap=part[1] * (part[1] - 1)))
+            targets.append(target_all[off[x]:off[y]])
+            continue
         bt = TowerBatch.from_edges(*part, device=device)
         batches.append(bt)
         targets.append(torch.tensor(target_all[off[x]:off[y]], device=device))
@@ -444,8 +452,10 @@ def run_train(args, cfg, world, rank, device):
     table = {}
     if not args.no_kernel_table or not args.roofline_kernel:
         table = kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, args.config, wl)
-    kname = args.roofline_kernel or (max(table, key=lambda k: table[k]["ms_per_step"]) if table else "edge_fwd")
+    kname = args.roofline_kernel or dominant(table)
     kid = KERNELS[kname][0]
+    if cfg.get("replay") and world == 1 and n_micro == 1:
+        return run_replay(args, cfg, trainer, rank, device, kname, table, wl)
     ev = HipEvents(2 * MAX_LAUNCHES * n_micro * args.steps)
     per = 2 * MAX_LAUNCHES * n_micro
     if world > 1:
@@ -530,6 +540,63 @@ def run_train(args, cfg, world, rank, device):
         dist.destroy_process_group()
 
 
+def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
+    """A launch-bound config (config 1: the reference's own 32-tower batch) timed as it should run:
+    each step one replayed hipGraph (spwgnn_amd/replay.py) after one pinned copy of the step's batch
+    arrays into the graph's static buffers. The batch is planned with every relation slot (N(N−1)
+    per tower); the kernel table and roofline come from eager steps of the same trainer (HIP events
+    cannot time launches inside a replayed graph)."""
+    from spwgnn_amd.replay import ReplayStep
+    S, math = cfg["S"], cfg["math"]
+    plans, tg_np, n_global = make_workload(cfg, rank, device, 1, plans=True)
+    plan, tgt = plans[0], tg_np[0]
+    rs = ReplayStep(plan, device, trainer.replay_body(plan.n_nodes, n_global))
+    for _ in range(args.warmup + 1):             # the first call runs eagerly and captures
+        rs(plan, tgt)
+        trainer.iterations += 1
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rs(plan, tgt)
+        trainer.iterations += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    loss = float(rs.bce.out3[0].item())
+    Ne, Nn = len(plan.src), plan.n_nodes
+    k = table.get(kname)
+    roof = None
+    if k:
+        roof = roofline(kname, [k["avg_launch_ms"]], k["launches_per_step"], Ne, Nn, S, math, args.config, wl)
+        roof["selected"] = "dominant kernel of this run's kernel table (eager steps of the same batch)"
+    out = {
+        "metric": f"towers/sec fwd+bwd, BASELINE config {args.config}", "value": round(cfg["towers"] * args.steps / el, 1),
+        "unit": "towers/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if math == "bf16" else "f32", "math": MATH_DESC[math],
+        "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
+        "config": {"workload": wl + "; each step a replayed hipGraph (batch arrays copied in per step)",
+                   "baseline_config": args.config, "towers_per_gpu": cfg["towers"], "global_batch": cfg["towers"],
+                   "nodes_per_tower": cfg["nodes"], "nodes_per_gpu": Nn, "edges_per_gpu": Ne, "mp_steps": S,
+                   "math": math, "parallelism": "dp1", "replays": rs.replays, "eblocks_planned": plan.n_eblocks},
+        "step_tflops": round(step_flops(Ne, Nn, S) * args.steps / el / 1e12, 4),
+        "loss": round(loss, 5), "roofline": roof, "kernels": table, "cpu_baseline": None,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+# kernel families: one SPWGNN_K_* id over several kernels of different shapes (listed in the table,
+# never named as "the dominant kernel" — a roofline belongs to one kernel)
+FAMILIES = ("wgrad_ws",)
+
+
+def dominant(table) -> str:
+    """The single kernel with the largest time per step in this run's kernel table."""
+    single = {k: v for k, v in table.items() if k not in FAMILIES}
+    return max(single, key=lambda k: single[k]["ms_per_step"]) if single else "edge_fwd"
+
+
 def kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, config, wl, steps=2, names=None):
     """Every timed kernel's roofline in the same run: `steps` extra (untimed) training steps per kernel
     with HIP events around each of its launches (the library's prof hook takes one kernel id per call).
@@ -545,6 +612,8 @@ def kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, config, wl, steps=2
         table[name] = {"launches_per_step": per_step, "avg_launch_ms": r["avg_launch_ms"],
                        "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
                        "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
+        if name in FAMILIES:
+            table[name]["family"] = "several kernels of different shapes under one id; frac over the family"
     return table
 
 
@@ -612,7 +681,7 @@ def run_infer(args, cfg, world, rank, device):
         table[name] = {"launches_per_step": len(ms) // 3, "avg_launch_ms": r["avg_launch_ms"],
                        "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
                        "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
-    kname = args.roofline_kernel or max(table, key=lambda k: table[k]["ms_per_step"])
+    kname = args.roofline_kernel or dominant(table)
     if kname not in times:
         raise SystemExit(f"kernel {kname} is not launched by the inference forward")
     kern_ms = times[kname]

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 1
+#define SPWGNN_ABI_VERSION 2
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -82,6 +82,16 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
                          int32_t* edge_src /* [n_eblocks*32] */, int32_t* edge_dst,
                          int32_t* edge_id /* [n_eblocks*32] original edge index or -1 */,
                          uint8_t* blk_csr /* [n_eblocks][128] */);
+/* The same plan with each tower's blocks sized for tower_edge_cap[t] >= tower_edges[t] edges
+ * (e.g. N(N-1), every relation slot): the wave-tiles and block counts then depend only on the
+ * tower sizes and capacities, so batches of the same shape share one plan geometry and one
+ * captured hipGraph (the unused capacity is padding, index -1, which matches no node). */
+int32_t spwgnn_plan_size_cap(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edge_cap,
+                             int32_t nw_max, spwgnn_plan_sizes* out);
+int32_t spwgnn_plan_fill_cap(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                             const int32_t* tower_edge_cap, const int32_t* src, const int32_t* dst, int32_t nw_max,
+                             const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src, int32_t* edge_dst,
+                             int32_t* edge_id, uint8_t* blk_csr);
 
 /* ------------------------------------------------------------------- device batch ------- */
 typedef struct spwgnn_batch {
@@ -113,6 +123,10 @@ typedef struct spwgnn_run {
     int32_t prof_kernel;
     int32_t prof_count;
     void** prof_events;
+    /* Replayable steps (hipGraph): when non-NULL the dropout key is read from this device word at
+     * run time instead of `seed`, so a captured step draws new masks on every replay once
+     * spwgnn_step_advance has moved the key on. NULL = use `seed`. */
+    const uint64_t* seed_dev;
 } spwgnn_run;
 
 /* Matrix-product arithmetic. F32 and X6 give fp32-class results:
@@ -167,6 +181,24 @@ int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* 
 int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64_t n, int32_t step,
                     float lr, float beta1, float beta2, float eps, float l2, float grad_scale,
                     spwgnn_stream_t stream);
+
+/* Replayable (hipGraph-captured) training steps: the per-step scalars live on the device.
+ * spwgnn_step_advance (one thread, stream-ordered) starts a step: *step_dev += 1 and the dropout
+ * key *key_dev becomes, for mode
+ *   SPWGNN_STEP_KEY_COUNTER   *key_dev + 1  (the Keras front end's per-step seed counter), or
+ *   SPWGNN_STEP_KEY_SPLITMIX  splitmix64 chain of (seed, step before the increment, rank, 0)
+ *                             (spwgnn_amd.trainer.dropout_key — the Trainer's key).
+ * spwgnn_adam_dev is spwgnn_adam with the step read from *step_dev and lr_t = lr_table[step]
+ * (table_len entries, clamped), the table filled on the host by spwgnn_adam_lr_table with the
+ * expression spwgnn_adam evaluates, so replayed and eager steps agree bit for bit. */
+#define SPWGNN_STEP_KEY_COUNTER 0
+#define SPWGNN_STEP_KEY_SPLITMIX 1
+int32_t spwgnn_step_advance(uint64_t* key_dev, int32_t* step_dev, int32_t mode, uint64_t seed, int32_t rank,
+                            spwgnn_stream_t stream);
+int32_t spwgnn_adam_lr_table(float lr, float beta1, float beta2, int32_t n, float* out_host);
+int32_t spwgnn_adam_dev(float* params, const float* grads, float* m, float* v, int64_t n, const int32_t* step_dev,
+                        const float* lr_table, int32_t table_len, float beta1, float beta2, float eps, float l2,
+                        float grad_scale, spwgnn_stream_t stream);
 
 /* Sigmoid readout (Networks.py:93-96) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream);

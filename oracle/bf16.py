@@ -36,6 +36,19 @@ from . import model as O
 
 
 ROUND = True   # False: the same factored graph without rounding (checked against model.forward_gather)
+KBLOCK = 0     # > 0: every product accumulated as a running sum of k-blocks of this size (an fp32
+               # accumulator walking the contraction in MFMA-like blocks); 0: one library matmul
+
+
+def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b, accumulated in KBLOCK-sized k-blocks in order when KBLOCK > 0."""
+    k = a.shape[1]
+    if KBLOCK <= 0 or k <= KBLOCK:
+        return a @ b
+    acc = a[:, 0:KBLOCK] @ b[0:KBLOCK]
+    for s in range(KBLOCK, k, KBLOCK):
+        acc = acc + a[:, s:s + KBLOCK] @ b[s:s + KBLOCK]
+    return acc
 
 
 def b16(x: torch.Tensor) -> torch.Tensor:
@@ -52,13 +65,13 @@ class _MM(torch.autograd.Function):
     def forward(ctx, x, w):
         xb, wb = b16(x), b16(w)
         ctx.save_for_backward(xb, wb)
-        return xb @ wb
+        return mm(xb, wb)
 
     @staticmethod
     def backward(ctx, g):
         xb, wb = ctx.saved_tensors
         gb = b16(g)
-        return gb @ wb.T, xb.T @ gb
+        return mm(gb, wb.T), mm(xb.T, gb)
 
 
 class _Bias(torch.autograd.Function):
@@ -167,12 +180,57 @@ def forward(p: Dict[str, torch.Tensor], pos, src, dst, prop, mp_steps: int = O.R
 
 
 def loss_and_grads(params: Dict[str, np.ndarray], pos, src, dst, prop, target, mp_steps: int = O.REF_MP_STEPS,
-                   drop_r=None, drop_o=None, training: bool = True):
-    """(loss, logits, grads) of the Keras BCE (Networks.py:102) on the bf16-operand emulation."""
-    tp = O.to_torch(params, dtype=torch.float64, requires_grad=True)
-    t = lambda a: None if a is None else torch.as_tensor(np.asarray(a), dtype=torch.float64)
-    z = forward(tp, t(pos), torch.as_tensor(np.asarray(src), dtype=torch.long),
-                torch.as_tensor(np.asarray(dst), dtype=torch.long), t(prop), mp_steps, t(drop_r), t(drop_o), training)
-    loss = O.keras_bce_from_logits(z, t(target).reshape(z.shape))
-    loss.backward()
-    return float(loss.detach()), z.detach().numpy(), {k: v.grad.detach().numpy().copy() for k, v in tp.items()}
+                   drop_r=None, drop_o=None, training: bool = True, dtype=torch.float64, kblock: int = 0):
+    """(loss, logits, grads) of the Keras BCE (Networks.py:102) on the bf16-operand emulation.
+
+    `dtype` is the accumulation type (float64: the emulator proper; float32 with `kblock` > 0: another
+    valid implementation of the same bf16 definition, summing each product in k-blocks of that size)."""
+    global KBLOCK
+    tp = O.to_torch(params, dtype=dtype, requires_grad=True)
+    t = lambda a: None if a is None else torch.as_tensor(np.ascontiguousarray(a), dtype=dtype)
+    old, KBLOCK = KBLOCK, kblock
+    try:
+        z = forward(tp, t(pos), torch.as_tensor(np.asarray(src), dtype=torch.long),
+                    torch.as_tensor(np.asarray(dst), dtype=torch.long), t(prop), mp_steps, t(drop_r), t(drop_o),
+                    training)
+        loss = O.keras_bce_from_logits(z, t(target).reshape(z.shape))
+        loss.backward()
+    finally:
+        KBLOCK = old
+    return (float(loss.detach()), z.detach().double().numpy(),
+            {k: v.grad.detach().double().numpy().copy() for k, v in tp.items()})
+
+
+NOISE_KBLOCKS = (0, 16, 32, 64)   # 0: one library matmul per product
+
+
+def noise_band(params: Dict[str, np.ndarray], pos, src, dst, prop, target, mp_steps: int = O.REF_MP_STEPS,
+               drop_r=None, drop_o=None, training: bool = True, ref=None):
+    """How far valid implementations of the SAME bf16-operand arithmetic land apart on this batch.
+
+    bf16 rounding is discontinuous: an operand that fp32 accumulation order moves across a bf16
+    rounding boundary changes by one bf16 ulp (2⁻⁸ relative), which perturbs everything downstream in
+    its tower by far more than the fp32 difference that caused it, and the perturbed values cross
+    further boundaries (measured: this emulator in fp32 vs fp64 on 64 six-block towers, S = 5 — about
+    1 operand in 10⁵ flips in the first layer, yet a third of the logits move, by up to 4.6e-3, and
+    the rm.0 kernel gradient by 1.7 % of its norm). No fp32 implementation can therefore match the
+    emulator element for element; the engine is held to landing no further from it than other valid
+    implementations do. Returns (ref, band): ref = the fp64 emulator's (loss, logits, grads); band =
+    per quantity the largest distance from ref over the alternative implementations (fp32 accumulation
+    in k-blocks of NOISE_KBLOCKS, like an MFMA k loop, or in one library matmul): {"z_rms", "z_max", "g": {name: relative L2}}."""
+    if ref is None:
+        ref = loss_and_grads(params, pos, src, dst, prop, target, mp_steps, drop_r, drop_o, training)
+    band = {"z_rms": 0.0, "z_max": 0.0, "g": {k: 0.0 for k in ref[2]}}
+    for kb in NOISE_KBLOCKS:
+        alt = loss_and_grads(params, pos, src, dst, prop, target, mp_steps, drop_r, drop_o, training,
+                             dtype=torch.float32, kblock=kb)
+        dz = alt[1] - ref[1]
+        band["z_rms"] = max(band["z_rms"], float(np.sqrt(np.mean(dz ** 2))))
+        band["z_max"] = max(band["z_max"], float(np.abs(dz).max()))
+        for k, r in ref[2].items():
+            band["g"][k] = max(band["g"][k], rel_l2(alt[2][k], r))
+    return ref, band
+
+
+def rel_l2(a, ref) -> float:
+    return float(np.linalg.norm(np.asarray(a, np.float64) - ref) / (np.linalg.norm(ref) + 1e-30))

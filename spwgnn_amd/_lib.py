@@ -38,12 +38,14 @@ class BatchC(C.Structure):
 class RunC(C.Structure):
     _fields_ = [("mp_steps", C.c_int32), ("training", C.c_int32), ("dropout", C.c_float), ("math", C.c_int32),
                 ("seed", C.c_uint64), ("prof_kernel", C.c_int32), ("prof_count", C.c_int32),
-                ("prof_events", C.c_void_p)]
+                ("prof_events", C.c_void_p), ("seed_dev", C.c_void_p)]
 
 
 K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WGRAD_W2, K_DA = 1, 2, 3, 4, 5, 6, 7, 8
 K_WGRAD_WS, K_ENC_NODE, K_ENC_NODE_BWD = 9, 10, 11
 MATH_F32, MATH_X6, MATH_BF16 = 0, 1, 2
+STEP_KEY_COUNTER, STEP_KEY_SPLITMIX = 0, 1
+ABI_VERSION = 2        # SPWGNN_ABI_VERSION this binding's structs follow
 READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 
 
@@ -59,12 +61,17 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_dense_to_edges": (i32, [vp, vp, i32, i32, vp, vp, vp, i64, C.POINTER(i64), vp]),
         "spwgnn_plan_size": (i32, [i32, vp, vp, i32, C.POINTER(PlanSizes)]),
         "spwgnn_plan_fill": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
+        "spwgnn_plan_size_cap": (i32, [i32, vp, vp, i32, C.POINTER(PlanSizes)]),
+        "spwgnn_plan_fill_cap": (i32, [i32, vp, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
         "spwgnn_workspace_bytes": (i64, [i32, i32, i32, i32]),
         "spwgnn_forward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp]),
         "spwgnn_backward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp, vp, vp]),
         "spwgnn_bce_scratch_bytes": (i64, [i64]),
         "spwgnn_bce": (i32, [vp, vp, i64, vp, vp, vp, vp]),
         "spwgnn_adam": (i32, [vp, vp, vp, vp, i64, i32, f32, f32, f32, f32, f32, f32, vp]),
+        "spwgnn_adam_dev": (i32, [vp, vp, vp, vp, i64, vp, vp, i32, f32, f32, f32, f32, f32, vp]),
+        "spwgnn_adam_lr_table": (i32, [f32, f32, f32, i32, vp]),
+        "spwgnn_step_advance": (i32, [vp, vp, i32, C.c_uint64, i32, vp]),
         "spwgnn_sigmoid": (i32, [vp, vp, i64, vp]),
         "spwgnn_tower_readout": (i32, [vp, vp, i32, i32, vp, vp]),
     }
@@ -82,8 +89,12 @@ def lib() -> C.CDLL:
         if not path.exists():
             raise SpwgnnError(f"{path} not found — build it with `python -m spwgnn_amd.build` "
                               "(the HIP path has no CPU fallback)")
-        _lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
-        _declare(_lib)
+        lib_ = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+        _declare(lib_)
+        if lib_.spwgnn_version() != ABI_VERSION:
+            raise SpwgnnError(f"{path} implements ABI {lib_.spwgnn_version()}, this binding expects {ABI_VERSION}: "
+                              "rebuild with `python -m spwgnn_amd.build`")
+        _lib = lib_
     return _lib
 
 

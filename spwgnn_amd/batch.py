@@ -60,6 +60,89 @@ def upload(arrays, device) -> list:
 
 
 @dataclass
+class HostPlan:
+    """A batch's host-side arrays in upload order (pos4, node_tower, node_local, wtile, edge_src,
+    edge_dst, blk_csr[, prop]) plus the sizes the kernels are launched with."""
+    n_towers: int
+    n_nodes: int
+    tower_nodes: np.ndarray
+    tower_edges: np.ndarray
+    src: np.ndarray
+    dst: np.ndarray
+    n_wtiles: int
+    n_eblocks: int
+    nw_max: int
+    edge_id: np.ndarray
+    node_shape: Optional[tuple]
+    has_prop: bool
+    arrays: list
+
+    @property
+    def geometry(self) -> tuple:
+        """What a captured step bakes in: sizes and every array's shape."""
+        return (self.n_towers, self.n_nodes, self.n_wtiles, self.n_eblocks, self.nw_max, self.has_prop,
+                tuple(a.shape for a in self.arrays))
+
+    @staticmethod
+    def build(pos, tower_nodes, src, dst, tower_edges, prop=None, nw_max=None, node_shape=None, tower_ids=None,
+              edge_cap=None) -> "HostPlan":
+        L = _lib.lib()
+        tower_nodes = np.ascontiguousarray(tower_nodes, dtype=np.int32)
+        tower_edges = np.ascontiguousarray(tower_edges, dtype=np.int32)
+        src = np.ascontiguousarray(src, dtype=np.int32)
+        dst = np.ascontiguousarray(dst, dtype=np.int32)
+        T = len(tower_nodes)
+        Nn = int(tower_nodes.sum())
+        if T == 0:
+            raise ValueError("empty batch: at least one tower is needed")
+        if pos.shape[0] != Nn:
+            raise ValueError(f"pos has {pos.shape[0]} rows, towers hold {Nn} nodes")
+        if int(tower_edges.sum()) != len(src) or len(src) != len(dst):
+            raise ValueError("edge counts do not match the edge list")
+        if nw_max is None:
+            nw_max = default_nw_max(int(tower_nodes.max()) if T else 1)
+        if T and int(tower_nodes.max()) > _NW_LIMIT:
+            raise ValueError(f"towers of more than {_NW_LIMIT} nodes are not supported by this build")
+        cap = None
+        if edge_cap is not None:
+            cap = np.ascontiguousarray(np.broadcast_to(np.asarray(edge_cap, np.int32), (T,)), dtype=np.int32)
+            if np.any(cap < tower_edges):
+                raise ValueError("edge_cap must be >= every tower's edge count")
+        sizes = _lib.PlanSizes()
+        if cap is None:
+            _lib.check(L.spwgnn_plan_size(T, _ptr(tower_nodes), _ptr(tower_edges), nw_max, C.byref(sizes)), "plan_size")
+        else:
+            _lib.check(L.spwgnn_plan_size_cap(T, _ptr(tower_nodes), _ptr(cap), nw_max, C.byref(sizes)), "plan_size_cap")
+        wtile = np.zeros((sizes.n_wtiles, 4), np.int32)
+        esrc = np.zeros(sizes.n_eblocks * 32, np.int32)
+        edst = np.zeros(sizes.n_eblocks * 32, np.int32)
+        eid = np.zeros(sizes.n_eblocks * 32, np.int32)
+        csr = np.zeros((sizes.n_eblocks, 128), np.uint8)
+        sp = _ptr(src) if len(src) else None
+        dp = _ptr(dst) if len(dst) else None
+        if cap is None:
+            _lib.check(L.spwgnn_plan_fill(T, _ptr(tower_nodes), _ptr(tower_edges), sp, dp, nw_max, C.byref(sizes),
+                                          _ptr(wtile), _ptr(esrc), _ptr(edst), _ptr(eid), _ptr(csr)), "plan_fill")
+        else:
+            _lib.check(L.spwgnn_plan_fill_cap(T, _ptr(tower_nodes), _ptr(tower_edges), _ptr(cap), sp, dp, nw_max,
+                                              C.byref(sizes), _ptr(wtile), _ptr(esrc), _ptr(edst), _ptr(eid),
+                                              _ptr(csr)), "plan_fill_cap")
+        tid = np.arange(T, dtype=np.int32) if tower_ids is None else np.asarray(tower_ids, np.int64)
+        if len(tid) != T or (T and (tid.min() < 0 or tid.max() > np.iinfo(np.int32).max)):
+            raise ValueError("tower_ids must hold one non-negative int32 id per tower")
+        node_tower = np.repeat(tid.astype(np.int32), tower_nodes)
+        starts = np.concatenate([[0], np.cumsum(tower_nodes)[:-1]]).astype(np.int64)
+        node_local = (np.arange(Nn) - np.repeat(starts, tower_nodes)).astype(np.int32)
+        pos4 = np.zeros((Nn, 4), np.float32)
+        pos4[:, :3] = np.asarray(pos, np.float32)[:, :3]
+        host = [pos4, node_tower, node_local, wtile, esrc, edst, csr]
+        if prop is not None:
+            host.append(np.asarray(prop, np.float32).reshape(Nn, 100))
+        return HostPlan(T, Nn, tower_nodes, tower_edges, src, dst, sizes.n_wtiles, sizes.n_eblocks, sizes.nw_max,
+                        eid, node_shape, prop is not None, host)
+
+
+@dataclass
 class TowerBatch:
     n_towers: int
     n_nodes: int
@@ -100,54 +183,26 @@ class TowerBatch:
     # ------------------------------------------------------------------ constructors
     @staticmethod
     def from_edges(pos: np.ndarray, tower_nodes, src, dst, tower_edges, prop=None, device="cuda",
-                   nw_max: Optional[int] = None, node_shape=None, tower_ids=None) -> "TowerBatch":
+                   nw_max: Optional[int] = None, node_shape=None, tower_ids=None, edge_cap=None) -> "TowerBatch":
         """pos (Nn, >=3) objects rows (already /170); towers are consecutive node ranges;
         edges tower-major with global node ids. `tower_ids` (T,): each tower's index in the batch it
         was cut from (the dropout masks are keyed by it), so a shard or micro-batch of a larger batch
-        draws the masks the whole batch would; default 0..T-1."""
-        L = _lib.lib()
-        tower_nodes = np.ascontiguousarray(tower_nodes, dtype=np.int32)
-        tower_edges = np.ascontiguousarray(tower_edges, dtype=np.int32)
-        src = np.ascontiguousarray(src, dtype=np.int32)
-        dst = np.ascontiguousarray(dst, dtype=np.int32)
-        T = len(tower_nodes)
-        Nn = int(tower_nodes.sum())
-        if T == 0:
-            raise ValueError("empty batch: at least one tower is needed")
-        if pos.shape[0] != Nn:
-            raise ValueError(f"pos has {pos.shape[0]} rows, towers hold {Nn} nodes")
-        if int(tower_edges.sum()) != len(src) or len(src) != len(dst):
-            raise ValueError("edge counts do not match the edge list")
-        if nw_max is None:
-            nw_max = default_nw_max(int(tower_nodes.max()) if T else 1)
-        if T and int(tower_nodes.max()) > _NW_LIMIT:
-            raise ValueError(f"towers of more than {_NW_LIMIT} nodes are not supported by this build")
-        sizes = _lib.PlanSizes()
-        _lib.check(L.spwgnn_plan_size(T, _ptr(tower_nodes), _ptr(tower_edges), nw_max, C.byref(sizes)), "plan_size")
-        wtile = np.zeros((sizes.n_wtiles, 4), np.int32)
-        esrc = np.zeros(sizes.n_eblocks * 32, np.int32)
-        edst = np.zeros(sizes.n_eblocks * 32, np.int32)
-        eid = np.zeros(sizes.n_eblocks * 32, np.int32)
-        csr = np.zeros((sizes.n_eblocks, 128), np.uint8)
-        _lib.check(L.spwgnn_plan_fill(T, _ptr(tower_nodes), _ptr(tower_edges), _ptr(src) if len(src) else None,
-                                      _ptr(dst) if len(dst) else None, nw_max, C.byref(sizes), _ptr(wtile),
-                                      _ptr(esrc), _ptr(edst), _ptr(eid), _ptr(csr)), "plan_fill")
-        tid = np.arange(T, dtype=np.int32) if tower_ids is None else np.asarray(tower_ids, np.int64)
-        if len(tid) != T or (T and (tid.min() < 0 or tid.max() > np.iinfo(np.int32).max)):
-            raise ValueError("tower_ids must hold one non-negative int32 id per tower")
-        node_tower = np.repeat(tid.astype(np.int32), tower_nodes)
-        starts = np.concatenate([[0], np.cumsum(tower_nodes)[:-1]]).astype(np.int64)
-        node_local = (np.arange(Nn) - np.repeat(starts, tower_nodes)).astype(np.int32)
-        pos4 = np.zeros((Nn, 4), np.float32)
-        pos4[:, :3] = np.asarray(pos, np.float32)[:, :3]
+        draws the masks the whole batch would; default 0..T-1. `edge_cap` (T,) ≥ tower_edges: size
+        each tower's blocks for that many edges (spwgnn_plan_fill_cap) so same-shape batches share
+        one plan geometry (replayed hipGraph steps); default: the actual edge counts."""
+        plan = HostPlan.build(pos, tower_nodes, src, dst, tower_edges, prop, nw_max, node_shape, tower_ids, edge_cap)
+        return TowerBatch.from_plan(plan, device)
+
+    @staticmethod
+    def from_plan(plan: "HostPlan", device, dev_arrays: Optional[list] = None) -> "TowerBatch":
+        """A device batch from a host plan: its arrays uploaded in one copy, or `dev_arrays` (device
+        tensors of the plan's array shapes, e.g. a replayed step's static buffers) used as they are."""
         dev = torch.device(device)
-        host = [pos4, node_tower, node_local, wtile, esrc, edst, csr]
-        if prop is not None:
-            host.append(np.asarray(prop, np.float32).reshape(Nn, 100))
-        d = upload(host, dev)
-        prop_t = d[7] if prop is not None else None
-        return TowerBatch(T, Nn, tower_nodes, tower_edges, src, dst, sizes.n_wtiles, sizes.n_eblocks,
-                          sizes.nw_max, dev, d[0], prop_t, d[1], d[2], d[3], d[4], d[5], d[6], eid, node_shape)
+        d = dev_arrays if dev_arrays is not None else upload(plan.arrays, dev)
+        m = plan
+        prop_t = d[7] if m.has_prop else None
+        return TowerBatch(m.n_towers, m.n_nodes, m.tower_nodes, m.tower_edges, m.src, m.dst, m.n_wtiles, m.n_eblocks,
+                          m.nw_max, dev, d[0], prop_t, d[1], d[2], d[3], d[4], d[5], d[6], m.edge_id, m.node_shape)
 
     @staticmethod
     def from_dense(objects, sender_relations, receiver_relations, propagation=None, device="cuda",

@@ -359,6 +359,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.thresh = thresh;
     en.scale = scale;
     en.seed = r->seed;
+    en.seed_dev = r->seed_dev;
     {
         Prof pn{r, st};
         SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
@@ -401,6 +402,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.thresh = thresh;
     ee.scale = scale;
     ee.seed = r->seed;
+    ee.seed_dev = r->seed_dev;
     {
         Prof p0{r, st};
         SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
@@ -927,6 +929,46 @@ int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* 
     return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
 }
 
+static float adam_lr_t(float lr, float beta1, float beta2, double t) {
+    return (float)(lr * std::sqrt(1.0 - std::pow((double)beta2, t)) / (1.0 - std::pow((double)beta1, t)));
+}
+
+int32_t spwgnn_adam_lr_table(float lr, float beta1, float beta2, int32_t n, float* out) {
+    if (!out || n < 2) return SPWGNN_E_ARG;
+    out[0] = 0.f;   // step 0 never runs (steps count from 1)
+    for (int32_t t = 1; t < n; ++t) out[t] = adam_lr_t(lr, beta1, beta2, (double)t);
+    return SPWGNN_OK;
+}
+
+int32_t spwgnn_adam_dev(float* params, const float* grads, float* m, float* v, int64_t n, const int32_t* step_dev,
+                        const float* lr_table, int32_t table_len, float beta1, float beta2, float eps, float l2,
+                        float grad_scale, spwgnn_stream_t stream) {
+    if (!params || !grads || !m || !v || n < 1 || !step_dev || !lr_table || table_len < 2) return SPWGNN_E_ARG;
+    AdamArgs a{};
+    a.p = params;
+    a.g = grads;
+    a.m = m;
+    a.v = v;
+    a.n = n;
+    a.step_dev = step_dev;
+    a.lr_table = lr_table;
+    a.table_len = table_len;
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.l2 = l2;
+    a.gscale = grad_scale;
+    hipError_t e = launch_adam(a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
+int32_t spwgnn_step_advance(uint64_t* key_dev, int32_t* step_dev, int32_t mode, uint64_t seed, int32_t rank,
+                            spwgnn_stream_t stream) {
+    if (!key_dev || !step_dev || mode < SPWGNN_STEP_KEY_COUNTER || mode > SPWGNN_STEP_KEY_SPLITMIX) return SPWGNN_E_ARG;
+    hipError_t e = launch_step_advance(key_dev, step_dev, mode, seed, rank, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
 int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64_t n, int32_t step, float lr,
                     float beta1, float beta2, float eps, float l2, float grad_scale, spwgnn_stream_t stream) {
     if (!params || !grads || !m || !v || n < 1 || step < 1) return SPWGNN_E_ARG;
@@ -937,7 +979,7 @@ int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64
     a.v = v;
     a.n = n;
     const double t = step;
-    a.lr_t = (float)(lr * std::sqrt(1.0 - std::pow((double)beta2, t)) / (1.0 - std::pow((double)beta1, t)));
+    a.lr_t = adam_lr_t(lr, beta1, beta2, t);
     a.b1 = beta1;
     a.b2 = beta2;
     a.eps = eps;

@@ -127,10 +127,12 @@ int32_t spwgnn_dense_to_edges(const float* Rs, const float* Rr, int32_t B, int32
     return SPWGNN_OK;
 }
 
-static int32_t plan_pack(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+// Towers → wave-tiles of whole towers (≤ nw_max nodes each, in order) and 32-edge blocks per tile;
+// a tile's block count follows the edge counts in `blk_edges` (actual counts, or capacities).
+static int32_t plan_pack(int32_t n_towers, const int32_t* tower_nodes, const int32_t* blk_edges,
                          int32_t nw_max, std::vector<int32_t>* tile_first_tower, int32_t* n_blocks_out,
                          int32_t* nw_used) {
-    if (n_towers < 0 || !tower_nodes || !tower_edges || nw_max < 1 || nw_max > kNwMaxLimit) return SPWGNN_E_ARG;
+    if (n_towers < 0 || !tower_nodes || !blk_edges || nw_max < 1 || nw_max > kNwMaxLimit) return SPWGNN_E_ARG;
     int32_t nb = 0, used = 0;
     int32_t t = 0;
     while (t < n_towers) {
@@ -138,7 +140,7 @@ static int32_t plan_pack(int32_t n_towers, const int32_t* tower_nodes, const int
         int32_t nodes = 0, edges = 0, t0 = t;
         while (t < n_towers && nodes + tower_nodes[t] <= nw_max) {
             nodes += tower_nodes[t];
-            edges += tower_edges[t];
+            edges += blk_edges[t];
             ++t;
         }
         if (tile_first_tower) tile_first_tower->push_back(t0);
@@ -151,12 +153,12 @@ static int32_t plan_pack(int32_t n_towers, const int32_t* tower_nodes, const int
     return SPWGNN_OK;
 }
 
-int32_t spwgnn_plan_size(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
-                         int32_t nw_max, spwgnn_plan_sizes* out) {
+static int32_t plan_size_impl(int32_t n_towers, const int32_t* tower_nodes, const int32_t* blk_edges,
+                              int32_t nw_max, spwgnn_plan_sizes* out) {
     if (!out) return SPWGNN_E_ARG;
     std::vector<int32_t> first;
     int32_t nb = 0, used = 0;
-    int32_t st = plan_pack(n_towers, tower_nodes, tower_edges, nw_max, &first, &nb, &used);
+    int32_t st = plan_pack(n_towers, tower_nodes, blk_edges, nw_max, &first, &nb, &used);
     if (st) return st;
     out->n_wtiles = (int32_t)first.size() - 1;
     out->n_eblocks = nb;
@@ -164,22 +166,24 @@ int32_t spwgnn_plan_size(int32_t n_towers, const int32_t* tower_nodes, const int
     return SPWGNN_OK;
 }
 
-int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
-                         const int32_t* src, const int32_t* dst, int32_t nw_max,
-                         const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src,
-                         int32_t* edge_dst, int32_t* edge_id, uint8_t* blk_csr) {
-    if (!sizes || !wtile || !edge_src || !edge_dst || !blk_csr) return SPWGNN_E_ARG;
+static int32_t plan_fill_impl(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                              const int32_t* blk_edges, const int32_t* src, const int32_t* dst, int32_t nw_max,
+                              const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src,
+                              int32_t* edge_dst, int32_t* edge_id, uint8_t* blk_csr) {
+    if (!sizes || !wtile || !edge_src || !edge_dst || !blk_csr || !tower_edges) return SPWGNN_E_ARG;
     std::vector<int32_t> first;
     int32_t nb = 0, used = 0;
-    int32_t st = plan_pack(n_towers, tower_nodes, tower_edges, nw_max, &first, &nb, &used);
+    int32_t st = plan_pack(n_towers, tower_nodes, blk_edges, nw_max, &first, &nb, &used);
     if (st) return st;
     const int32_t ntiles = (int32_t)first.size() - 1;
     if (ntiles != sizes->n_wtiles || nb != sizes->n_eblocks) return SPWGNN_E_ARG;
-    // prefix sums of nodes and edges per tower
-    std::vector<int64_t> node_off(n_towers + 1, 0), edge_off(n_towers + 1, 0);
+    // prefix sums of nodes, edges and block-sizing edges per tower
+    std::vector<int64_t> node_off(n_towers + 1, 0), edge_off(n_towers + 1, 0), cap_off(n_towers + 1, 0);
     for (int32_t t = 0; t < n_towers; ++t) {
+        if (tower_edges[t] < 0 || tower_edges[t] > blk_edges[t]) return SPWGNN_E_ARG;
         node_off[t + 1] = node_off[t] + tower_nodes[t];
         edge_off[t + 1] = edge_off[t] + tower_edges[t];
+        cap_off[t + 1] = cap_off[t] + blk_edges[t];
     }
     if (edge_off[n_towers] > 0 && (!src || !dst)) return SPWGNN_E_ARG;   // no list needed without edges
     int32_t blk = 0;
@@ -187,8 +191,7 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
         const int32_t t0 = first[w], t1 = first[w + 1];
         const int64_t n0 = node_off[t0], n1 = node_off[t1];
         const int64_t e0 = edge_off[t0], e1 = edge_off[t1];
-        const int32_t ne = (int32_t)(e1 - e0);
-        const int32_t nblk = std::max(1, (ne + 31) / 32);
+        const int32_t nblk = std::max<int32_t>(1, (int32_t)((cap_off[t1] - cap_off[t0] + 31) / 32));
         wtile[4 * w + 0] = blk;
         wtile[4 * w + 1] = nblk;
         wtile[4 * w + 2] = (int32_t)n0;
@@ -235,6 +238,32 @@ int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int
         }
     }
     return SPWGNN_OK;
+}
+
+int32_t spwgnn_plan_size(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                         int32_t nw_max, spwgnn_plan_sizes* out) {
+    return plan_size_impl(n_towers, tower_nodes, tower_edges, nw_max, out);
+}
+
+int32_t spwgnn_plan_fill(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                         const int32_t* src, const int32_t* dst, int32_t nw_max,
+                         const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src,
+                         int32_t* edge_dst, int32_t* edge_id, uint8_t* blk_csr) {
+    return plan_fill_impl(n_towers, tower_nodes, tower_edges, tower_edges, src, dst, nw_max, sizes, wtile, edge_src,
+                          edge_dst, edge_id, blk_csr);
+}
+
+int32_t spwgnn_plan_size_cap(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edge_cap,
+                             int32_t nw_max, spwgnn_plan_sizes* out) {
+    return plan_size_impl(n_towers, tower_nodes, tower_edge_cap, nw_max, out);
+}
+
+int32_t spwgnn_plan_fill_cap(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                             const int32_t* tower_edge_cap, const int32_t* src, const int32_t* dst, int32_t nw_max,
+                             const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src, int32_t* edge_dst,
+                             int32_t* edge_id, uint8_t* blk_csr) {
+    return plan_fill_impl(n_towers, tower_nodes, tower_edges, tower_edge_cap, src, dst, nw_max, sizes, wtile,
+                          edge_src, edge_dst, edge_id, blk_csr);
 }
 
 }  // extern "C"

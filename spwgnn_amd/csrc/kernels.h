@@ -75,6 +75,7 @@ struct EncNodeArgs {
     uint32_t thresh;
     float scale;
     uint64_t seed;
+    const uint64_t* seed_dev;   // non-null: the dropout key is read from device memory (replayable steps)
 };
 
 struct EncEdgeArgs {
@@ -91,7 +92,15 @@ struct EncEdgeArgs {
     uint32_t thresh;
     float scale;
     uint64_t seed;
+    const uint64_t* seed_dev;   // non-null: the dropout key is read from device memory (replayable steps)
 };
+
+// The run's dropout key: a kernel argument, or (graph-replayed training steps) a device word the
+// step-advance kernel rewrites before each replay.
+template <class Args>
+__device__ __forceinline__ uint64_t run_seed(const Args& a) {
+    return a.seed_dev ? *a.seed_dev : a.seed;
+}
 
 struct EdgeFwdArgs {
     int n_wtiles, nw_max, wpg;
@@ -259,6 +268,9 @@ struct AdamArgs {
     const float* g;
     int64_t n;
     float lr_t, b1, b2, eps, l2, gscale;
+    const int32_t* step_dev;   // non-null: lr_t = lr_table[min(*step_dev, table_len - 1)]
+    const float* lr_table;
+    int32_t table_len;
 };
 
 // Host launchers (defined next to their kernels; each returns hipGetLastError()).
@@ -282,6 +294,7 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
+hipError_t launch_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);
 hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers, int mode, float* out, hipStream_t st);
 

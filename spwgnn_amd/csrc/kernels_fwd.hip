@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     tchain_acc<4, 4, 4, kLdN>(Z, C, a.w_om1, lane);
     bias_act_rho<4, true>(C, a.b_om1, h);  // relu(om(.)) — Networks.py:76
     if (a.dropout_on) {                    // Networks.py:78
-        const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
+        const uint32_t key = drop_row_key(run_seed(a), 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW>(Z, C, a.x_om1, lane, wr);
     bias_act_rho<4, true>(C[0], a.b_om1, h);  // relu(om(.)) — Networks.py:76
     if (a.dropout_on) {                       // Networks.py:78
-        const uint32_t key = drop_row_key(a.seed, 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
+        const uint32_t key = drop_row_key(run_seed(a), 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     bias_act_rho<5, true>(Y, a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:75
     if (a.dropout_on && valid) {           // Networks.py:77
         const uint32_t tw = (uint32_t)a.node_tower[s];
-        const uint32_t key = drop_row_key(a.seed, 1u, tw, (uint32_t)a.node_local[s], (uint32_t)a.node_local[d]);
+        const uint32_t key = drop_row_key(run_seed(a), 1u, tw, (uint32_t)a.node_local[s], (uint32_t)a.node_local[d]);
 #pragma unroll
         for (int t = 0; t < 5; ++t)
 #pragma unroll
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_x6(EncEdgeArg
         bias_act_rho<5, true>(Y[c], a.b_rm3, h);  // rm's last Dense is linear; relu from Networks.py:75
         if (a.dropout_on && src[c] >= 0) {         // Networks.py:77
             const uint32_t tw = (uint32_t)a.node_tower[src[c]];
-            const uint32_t key = drop_row_key(a.seed, 1u, tw, (uint32_t)a.node_local[src[c]], (uint32_t)a.node_local[dst[c]]);
+            const uint32_t key = drop_row_key(run_seed(a), 1u, tw, (uint32_t)a.node_local[src[c]], (uint32_t)a.node_local[dst[c]]);
 #pragma unroll
             for (int t = 0; t < 5; ++t)
 #pragma unroll

@@ -1015,6 +1015,9 @@ __global__ void k_bce_final(BceArgs a) {
 }
 
 __global__ void k_adam(AdamArgs a) {
+    // replayable steps: the step count lives on the device; lr_t comes from the host-built table
+    // (spwgnn_adam_lr_table: the same expression spwgnn_adam evaluates, so both paths agree bitwise)
+    if (a.step_dev) a.lr_t = a.lr_table[min(max(*a.step_dev, 0), a.table_len - 1)];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
         const float p = a.p[i];
         const float g = a.gscale * a.g[i] + 2.f * a.l2 * p;
@@ -1024,6 +1027,31 @@ __global__ void k_adam(AdamArgs a) {
         a.v[i] = v;
         a.p[i] = p - a.lr_t * m / (sqrtf(v) + a.eps);
     }
+}
+
+// Start of a replayable training step (one thread): the optimizer step count moves on and the
+// dropout key is derived for the new step — mode 0: key + 1 (the Keras front end's per-step seed
+// counter); mode 1: splitmix64 chain of (seed, iteration, rank, micro 0), Trainer.run_config's key.
+__device__ __forceinline__ uint64_t splitmix64_dev(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__global__ void k_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank) {
+    if (threadIdx.x != 0) return;
+    const int32_t it = *step;
+    uint64_t k;
+    if (mode == 0) {
+        k = *key + 1ull;
+    } else {
+        k = splitmix64_dev(seed);
+        k = splitmix64_dev(k ^ (uint64_t)(int64_t)it);
+        k = splitmix64_dev(k ^ (uint64_t)(int64_t)rank);
+        k = splitmix64_dev(k ^ 0ull);
+    }
+    *key = k;
+    *step = it + 1;
 }
 
 __global__ void k_sigmoid(const float* z, float* p, int64_t n) {
@@ -1166,6 +1194,10 @@ hipError_t launch_bce(const BceArgs& a, hipStream_t st) {
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
     const int64_t blocks = std::min<int64_t>((a.n + 255) / 256, 2048);
     hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank, hipStream_t st) {
+    hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(64), 0, st, key, step, mode, seed, rank);
     return hipGetLastError();
 }
 hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers, int mode, float* out, hipStream_t st) {

@@ -40,6 +40,7 @@ class RunConfig:
     math: str = "x6"                     # "x6" split-bf16 matrix products | "f32" f32 MFMA (spwgnn.h)
     prof_kernel: int = 0                 # SPWGNN_K_* to bracket with HIP events (bench only)
     prof_events: Optional[list] = None   # raw hipEvent_t handles, 2 per launch
+    seed_dev: Optional[torch.Tensor] = None   # (1,) int64 device word holding the dropout key (replayable steps)
 
     def cstruct(self) -> _lib.RunC:
         r = _lib.RunC()
@@ -56,6 +57,10 @@ class RunConfig:
             r.prof_kernel = int(self.prof_kernel)
             r.prof_count = len(self.prof_events) // 2
             r.prof_events = C.cast(arr, C.c_void_p)
+        if self.seed_dev is not None:
+            if self.seed_dev.device.type != "cuda" or self.seed_dev.dtype != torch.int64:
+                raise ValueError("seed_dev must be a (1,) int64 device tensor")
+            r.seed_dev = self.seed_dev.data_ptr()
         return r
 
 
@@ -73,7 +78,7 @@ class Workspace:
         # sizes and run fields, plus the device arrays the stored activations were computed from:
         # two same-shape batches (equal micro-batches under one seed) must not pass for each other
         return (run.math, int(run.mp_steps), bool(run.training), float(run.dropout), int(run.seed),
-                batch.n_nodes, batch.n_eblocks, batch.n_wtiles, batch.pos.data_ptr(), batch.edge_src.data_ptr(),
+                run.seed_dev.data_ptr() if run.seed_dev is not None else 0, batch.n_nodes, batch.n_eblocks, batch.n_wtiles, batch.pos.data_ptr(), batch.edge_src.data_ptr(),
                 batch.prop.data_ptr() if batch.prop is not None else 0)
 
     def holds(self, batch: TowerBatch, run: "RunConfig") -> bool:
@@ -162,6 +167,32 @@ def adam(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v: torch.Te
     st = _lib.lib().spwgnn_adam(params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), params.numel(),
                                 int(step), lr, beta1, beta2, eps, l2, grad_scale, _stream(params.device))
     _lib.check(st, "spwgnn_adam")
+
+
+def adam_dev(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step_dev: torch.Tensor,
+             lr_table: torch.Tensor, beta1=0.9, beta2=0.999, eps=1e-7, l2=0.0, grad_scale=1.0):
+    """Adam with the step count read from the device word `step_dev` ((1,) int32) and lr_t from
+    `lr_table` (device fp32, built by `adam_lr_table`): capturable into a replayed hipGraph."""
+    st = _lib.lib().spwgnn_adam_dev(params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), params.numel(),
+                                    step_dev.data_ptr(), lr_table.data_ptr(), lr_table.numel(), beta1, beta2, eps, l2,
+                                    grad_scale, _stream(params.device))
+    _lib.check(st, "spwgnn_adam_dev")
+
+
+def adam_lr_table(n: int, lr=5e-4, beta1=0.9, beta2=0.999, device="cuda") -> torch.Tensor:
+    """lr_t of steps 0..n-1 (host-built with spwgnn_adam's own expression), on the device."""
+    import numpy as np
+    out = np.zeros(int(n), np.float32)
+    _lib.check(_lib.lib().spwgnn_adam_lr_table(lr, beta1, beta2, int(n), out.ctypes.data), "spwgnn_adam_lr_table")
+    return torch.from_numpy(out).to(device)
+
+
+def step_advance(key_dev: torch.Tensor, step_dev: torch.Tensor, mode: int = _lib.STEP_KEY_COUNTER, seed: int = 0,
+                 rank: int = 0):
+    """Start a replayable step on the device: step += 1, dropout key moved on (spwgnn.h)."""
+    st = _lib.lib().spwgnn_step_advance(key_dev.data_ptr(), step_dev.data_ptr(), int(mode),
+                                        int(seed) & 0xFFFFFFFFFFFFFFFF, int(rank), _stream(key_dev.device))
+    _lib.check(st, "spwgnn_step_advance")
 
 
 def sigmoid(logits: torch.Tensor) -> torch.Tensor:

@@ -16,10 +16,12 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from . import _lib
 from . import engine as E
 from . import params as P
-from .batch import TowerBatch, upload
+from .batch import HostPlan, TowerBatch
 from .network import GraphNetwork
+from .replay import DeviceCounters, ReplayCache
 
 
 class CompactDataset:
@@ -54,6 +56,11 @@ class CompactDataset:
             np.asarray(propagation, np.float32)
 
     def subset(self, idx: np.ndarray, device) -> TowerBatch:
+        return TowerBatch.from_plan(self.subset_plan(idx), device)
+
+    def subset_plan(self, idx: np.ndarray, edge_cap: bool = False) -> HostPlan:
+        """Host plan of the towers `idx`; `edge_cap`: blocks sized for all N(N−1) relation slots
+        per tower, so every batch of len(idx) towers has one geometry (replayed steps)."""
         idx = np.asarray(idx)
         n = len(idx)
         # the towers' edge ranges gathered in one vectorised pass (tower k of the batch: node ids + k·N)
@@ -65,8 +72,9 @@ class CompactDataset:
         src = (self.src[gidx] + shift).astype(np.int32)
         dst = (self.dst[gidx] + shift).astype(np.int32)
         prop = None if self.prop is None else self.prop[idx].reshape(n * self.N, 100)
-        return TowerBatch.from_edges(self.objects[idx].reshape(n * self.N, 3), np.full(n, self.N, np.int32), src, dst,
-                                     self.tower_edges[idx], prop, device, node_shape=(n, self.N))
+        return HostPlan.build(self.objects[idx].reshape(n * self.N, 3), np.full(n, self.N, np.int32), src, dst,
+                              self.tower_edges[idx], prop, node_shape=(n, self.N),
+                              edge_cap=self.N * (self.N - 1) if edge_cap else None)
 
 
 class KerasModel:
@@ -90,6 +98,12 @@ class KerasModel:
         self._bce = E.BceScratch(dev)
         self._grads = torch.empty_like(net.flat.data)
         self.history: Dict[str, List[float]] = {}
+        # replayed fit steps (spwgnn_amd/replay.py): device step words, per-geometry graphs, epoch sums
+        self._ctr: Optional[DeviceCounters] = None
+        self._replays: Optional[ReplayCache] = None
+        self._replay_graph: Optional[bool] = None
+        self._tot = torch.zeros(3, dtype=torch.float64, device=dev)
+        self._w3: Dict[int, torch.Tensor] = {}
 
     # ---------------------------------------------------------------- inference
     def predict(self, x: Dict[str, np.ndarray], batch_size: int = 32768) -> np.ndarray:
@@ -123,6 +137,24 @@ class KerasModel:
                self.eps, self.l2)
         return out3
 
+    def _replay_body(self):
+        """One fit step's launches for a replayed geometry: the same sequence as train_on_batch
+        (key + 1, forward, BCE, backward, Adam at the incremented step) with the per-step scalars
+        read from the device, and the epoch sums accumulated on the device."""
+        net, ctr = self.net, self._ctr
+
+        def body(batch, target, ws, bce, z, dz):
+            w3 = self._w3[batch.n_towers]        # created before the first (eager) run of a geometry
+            E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_COUNTER)
+            run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key)
+            E.forward(net.flat.data, batch, run, ws, logits=z)
+            out3, _ = E.bce(z, target, bce, dlogits=dz)
+            self._tot.add_(out3.double() * w3)
+            E.backward(net.flat.data, batch, run, ws, dz, grads=self._grads)
+            E.adam_dev(net.flat.data, self._grads, self.m, self.v, ctr.step, ctr.lr_table, self.beta1, self.beta2,
+                       self.eps, self.l2)
+        return body
+
     def evaluate_batch(self, batch: TowerBatch, target: torch.Tensor):
         run = E.RunConfig(self.net.mp_steps, training=False)
         z = E.forward(self.net.flat.data, batch, run, self._ws)
@@ -130,7 +162,11 @@ class KerasModel:
         return out3
 
     def fit(self, x: Dict[str, np.ndarray], y: Dict[str, np.ndarray], batch_size: int = 32, epochs: int = 10,
-            validation_split: float = 0.0, shuffle: bool = True, verbose: int = 1, seed: int = 0):
+            validation_split: float = 0.0, shuffle: bool = True, verbose: int = 1, seed: int = 0,
+            graph: bool = True):
+        """Keras fit (main.py:92-98). Each training step is a replayed hipGraph of forward, BCE,
+        backward and Adam per batch geometry (`graph=False`: the identical launches issued eagerly,
+        bit-identical results); batches are planned with N(N−1) relation slots per tower."""
         objects = np.asarray(x["objects"], np.float32)
         target = np.asarray(y["target"], np.float32).reshape(objects.shape[0], -1)
         B = objects.shape[0]
@@ -144,21 +180,29 @@ class KerasModel:
             hist.update({"val_loss": [], "val_binary_accuracy": []})
             vbatch = ds.subset(np.arange(n_tr, B), dev)
             vtgt = torch.as_tensor(target[n_tr:], device=dev).reshape(-1).contiguous()
+        # every step runs as a replayed hipGraph per batch geometry (graph=False: the same launches
+        # eagerly); the device words start from the host counters and the host mirrors each step
+        if self._ctr is None:
+            self._ctr = DeviceCounters(dev, self.net._step_seed, self.iterations, self.lr, self.beta1,
+                                       self.beta2)
+        else:
+            self._ctr.set(key=self.net._step_seed, step=self.iterations)
+        if self._replays is None or self._replay_graph != graph:
+            self._replays = ReplayCache(dev, self._replay_body, graph=graph)
+            self._replay_graph = graph
         for ep in range(epochs):
             order = rng.permutation(n_tr) if shuffle else np.arange(n_tr)
             # (Σ loss·batch, Σ correct, Σ nodes) on the device: no host sync per batch, so the host
             # builds the next batch while the GPU runs this one
-            tot = torch.zeros(3, dtype=torch.float64, device=dev)
-            wvec = {}   # (batch length, 1, 1) weights, one device copy per distinct length
+            self._tot.zero_()
             for b0 in range(0, n_tr, batch_size):
                 idx = order[b0:b0 + batch_size]
-                batch = ds.subset(idx, dev)
-                (tg,) = upload([target[idx].reshape(-1)], dev)
-                o3 = self.train_on_batch(batch, tg)
-                if len(idx) not in wvec:
-                    wvec[len(idx)] = torch.tensor([float(len(idx)), 1.0, 1.0], dtype=torch.float64, device=dev)
-                tot += o3.double() * wvec[len(idx)]
-            tot_l, tot_c, tot_n = tot.tolist()
+                if len(idx) not in self._w3:
+                    self._w3[len(idx)] = torch.tensor([float(len(idx)), 1.0, 1.0], dtype=torch.float64, device=dev)
+                self._replays(ds.subset_plan(idx, edge_cap=True), target[idx])
+                self.net._step_seed += 1
+                self.iterations += 1
+            tot_l, tot_c, tot_n = self._tot.tolist()
             hist["loss"].append(tot_l / max(n_tr, 1))
             hist["binary_accuracy"].append(tot_c / max(tot_n, 1))
             if n_val:

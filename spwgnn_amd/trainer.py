@@ -25,7 +25,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from . import engine as E
+from . import _lib, engine as E
 from .batch import TowerBatch
 
 
@@ -98,6 +98,36 @@ class Trainer:
         key = dropout_key(self.seed, self.iterations, self.rank, micro)
         return E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, seed=key, math=self.math,
                            prof_kernel=self.prof_kernel, prof_events=self.prof_events)
+
+    def replay_body(self, n_nodes: int, n_global: Optional[int] = None):
+        """The launches of one single-batch `step` for spwgnn_amd.replay.ReplayStep (hipGraph
+        replay): the dropout key and Adam step are device words (spwgnn_step_advance in the
+        Trainer's splitmix key mode, spwgnn_adam_dev), so every replay is the next optimizer step
+        with the masks `step` would draw. Single process only (no all-reduce inside a graph)."""
+        from .replay import DeviceCounters
+        if self.world > 1:
+            raise ValueError("replayed steps are single-process; DP steps use step()")
+        if not isinstance(self.engine, HipEngine):
+            raise ValueError("replayed steps need the HIP engine")
+        if getattr(self, "_ctr", None) is None:
+            self._ctr = DeviceCounters(self.params.device, 0, self.iterations, self.lr, self.b1, self.b2)
+        else:
+            self._ctr.set(step=self.iterations)
+        ctr = self._ctr
+        w = n_nodes / (n_global or n_nodes)
+        grads = torch.empty_like(self.params)
+
+        def body(batch, target, ws, bce, z, dz):
+            E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_SPLITMIX, self.seed, self.rank)
+            run = E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, math=self.math, seed_dev=ctr.key)
+            E.forward(self.params, batch, run, ws, logits=z)
+            out3, _ = E.bce(z, target, bce, dlogits=dz)
+            E.backward(self.params, batch, run, ws, dz, grads=grads)
+            if w != 1.0:
+                grads.mul_(w)
+            E.adam_dev(self.params, grads, self.m, self.v, ctr.step, ctr.lr_table, self.b1, self.b2, self.eps,
+                       self.l2)
+        return body
 
     def step(self, batch, target, n_global: Optional[int] = None):
         """One optimizer step. `batch`/`target` may be lists (micro-batches of this rank's shard);

@@ -139,15 +139,11 @@ def test_config5_full_size_inference_hipgraph():
 # ---------------------------------------------------------------------------------------------
 # Config 2 (N = 6, B = 4,096, S = 3, fp32 training) and configs 3–4 in bf16 arithmetic
 # (BASELINE.json names bf16 for them; SPWGNN_MATH_BF16 = operands rounded to bf16, one MFMA product,
-# fp32 accumulation). bf16 tolerances as test_gpu_parity.test_bf16_math_forward_backward:
-# logits |Δ| ≤ 0.05, each gradient tensor's cosine with the fp64 oracle's ≥ 0.99.
+# fp32 accumulation). Here: full-size properties (linearity, Adam) and the distance of sampled logits
+# from the fp64 oracle (|Δ| ≤ 0.05: the bf16 arithmetic's own error, measured ≤ 1.5e-2); the
+# arithmetic itself is checked against the bf16-operand emulator in tests/test_gpu_fullsize.py.
 # ---------------------------------------------------------------------------------------------
 BF16_LOGIT_ATOL = 0.05
-BF16_COS = 0.99
-
-
-def _cos(a, b):
-    return float((a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
 
 
 def _train_grads(flat, batch, tgt, S, math, dropout=0.0):
@@ -231,8 +227,8 @@ def test_config3_bf16_full_size():
     """Config 3 in its BASELINE arithmetic (bf16): 65,536 fully connected 12-block towers, S = 5,
     training forward + backward at full size. Sampled towers' logits are within the bf16 tolerance of
     the fp64 oracle; the full-batch gradients equal the mean of its two halves' gradients (linearity
-    of the node-mean BCE; fp32 accumulation, 1e-4 of each tensor's max); the gradients of a sampled
-    16-tower sub-batch have cosine ≥ 0.99 with the oracle's."""
+    of the node-mean BCE; fp32 accumulation, 1e-4 of each tensor's max). A sampled sub-batch's
+    gradients against the bf16 emulator: test_gpu_fullsize.test_config3_bf16_full_size_against_emulator."""
     B, N, S = 65536, 12, 5
     params = O.random_params(43)
     raw = D.synthetic_towers(B, N, seed=13)
@@ -249,12 +245,6 @@ def test_config3_bf16_full_size():
     for k in g:
         comb = (hg[0][k] + hg[1][k]) / 2
         assert np.abs(comb - g[k]).max() <= 1e-4 * np.abs(g[k]).max() + 1e-9, k
-    # the sampled sub-batch's gradients vs the oracle (bf16 tolerance)
-    Rs, Rr = O.relation_matrices(raw[pick], None)
-    _, _, gs = _train_grads(flat, TowerBatch.fully_connected(obj[pick], device="cuda"), tgt[pick], S, "bf16")
-    _, _, g_ref = O.loss_and_grads(params, obj[pick], Rs, Rr, np.zeros((len(pick), N, 100), np.float32), tgt[pick], S)
-    for k in g_ref:
-        assert _cos(gs[k], g_ref[k]) >= BF16_COS, (k, _cos(gs[k], g_ref[k]))
 
 
 def test_config4_bf16_shard_training():

@@ -9,10 +9,11 @@ training forward + BCE + backward exactly as a bench step runs it. Checked throu
     oracle run with those masks restated by oracle/dropout.py — fp32 tolerance (logits 1e-5 abs +
     1e-5 rel, gradients 1e-5 of each tensor's max), and the full batch's logits of those towers.
 bf16 (SPWGNN_MATH_BF16): logits and every gradient tensor against oracle/bf16.py, which restates the
-engine's arithmetic definition (operands rounded to bf16 RNE, fp32 accumulation) on the reference graph:
-logits |Δ| ≤ 1e-3 + 1e-3·|z|, gradients ≤ 1e-3 of each tensor's max (vs the bf16 rounding itself,
-≈ 4e-3 relative per operand; the fp64 oracle differs from bf16 arithmetic by up to ≈ 0.1 of a tensor's
-max on these batches).
+engine's arithmetic definition (operands rounded to bf16 RNE, fp32 accumulation) on the reference graph.
+bf16 rounding is discontinuous, so two valid implementations of it that only sum in different orders
+land apart by a batch-dependent amount (OB.noise_band: fp32 k-blocked variants of the emulator); the
+engine must land no further from the fp64 emulator than 2.5× that band, per logit statistic and per
+gradient tensor (relative L2), with the median gradient ratio ≤ 1.5.
 """
 import numpy as np
 import pytest
@@ -25,7 +26,7 @@ from spwgnn_amd import TowerBatch, data as D, engine as E, params as P
 
 pytestmark = pytest.mark.gpu
 
-BF16_TOL = 1e-3
+BAND_FACTOR = 2.5   # engine distance ≤ 2.5 × the band of valid implementations (calibration ≤ 1.6)
 
 
 def _train(flat, batch, tgt, S, math, dropout=0.0, seed=0):
@@ -91,22 +92,33 @@ def test_headline_training_step_full_size():
 
 
 # ------------------------------------------------------------------------------- bf16 emulation
-def _bf16_check(got_z, got_g, ref_z, ref_g, what):
-    err_z = np.abs(got_z - ref_z)
-    assert np.all(err_z <= BF16_TOL + BF16_TOL * np.abs(ref_z)), (what, float(err_z.max()))
-    worst = {}
-    for k, r in ref_g.items():
-        e = np.abs(got_g[k] - r).max() / (np.abs(r).max() + 1e-30)
-        worst[k] = e
-        assert e <= BF16_TOL, (what, k, e)
-    print(f"{what}: logits max|Δ| {err_z.max():.2e}, worst gradient {max(worst.values()):.2e} "
-          f"({max(worst, key=worst.get)})")
+def _bf16_check(got_z, got_g, ref, band, what, loss=None):
+    """The engine's distance from the fp64 emulator must stay inside the band other valid
+    implementations of the same bf16 arithmetic span on this batch (oracle/bf16.py noise_band; the
+    calibration in tests/test_oracle.py measures ratios ≤ 1.6 between independent implementations)."""
+    _, z_e, g_e = ref
+    dz = np.asarray(got_z, np.float64).reshape(-1) - z_e
+    rms, mx = float(np.sqrt(np.mean(dz ** 2))), float(np.abs(dz).max())
+    assert rms <= BAND_FACTOR * band["z_rms"] + 1e-6, (what, "logit rms", rms, band["z_rms"])
+    assert mx <= BAND_FACTOR * band["z_max"] + 1e-5, (what, "logit max", mx, band["z_max"])
+    err = {k: OB.rel_l2(got_g[k], r) for k, r in g_e.items()}
+    ratio = {k: err[k] / (band["g"][k] + 1e-12) for k in err}
+    med = float(np.median(list(ratio.values())))
+    print(f"{what}: logits rms {rms:.2e} (band {band['z_rms']:.2e}), max {mx:.2e} (band {band['z_max']:.2e}); "
+          f"gradient rel-L2 / band: worst {max(ratio.values()):.2f} ({max(ratio, key=ratio.get)}), median {med:.2f}; "
+          + " ".join(f"{k}={err[k]:.1e}/{band['g'][k]:.1e}" for k in err))
+    for k in err:
+        assert err[k] <= BAND_FACTOR * band["g"][k] + 1e-5, (what, k, err[k], band["g"][k])
+    assert med <= 1.5, (what, "median gradient ratio", med)
+    if loss is not None:
+        assert abs(loss - ref[0]) <= 1e-3 * max(1.0, abs(ref[0])), (what, loss, ref[0])
 
 
 @pytest.mark.parametrize("N,fully,dropout", [(6, True, 0.0), (9, False, 0.0), (6, False, 0.1), (12, True, 0.1)])
 def test_bf16_math_against_bf16_emulator(N, fully, dropout):
-    """SPWGNN_MATH_BF16 on a 64-tower batch: logits, loss and every gradient equal the bf16-operand
-    emulator (oracle/bf16.py) at 1e-3, with and without dropout (the engine's masks, restated)."""
+    """SPWGNN_MATH_BF16 on a 64-tower batch: logits, loss and every gradient against the bf16-operand
+    emulator (oracle/bf16.py), inside the band of valid bf16 implementations, with and without
+    dropout (the engine's masks, restated)."""
     params = O.random_params(5)
     obj, Rs, Rr, prop, tgt = D.synthetic_batch(64, N, seed=2, fully_connected=fully)
     batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
@@ -119,16 +131,15 @@ def test_bf16_math_against_bf16_emulator(N, fully, dropout):
         full_r = DR.relation_mask_towers(seed, dropout, np.arange(64), N)   # slot order, all E slots
         dr = full_r[e[:, 0], e[:, 1]]
         do = DR.object_mask_towers(seed, dropout, np.arange(64), N).reshape(-1, 100)
-    loss_e, z_e, g_e = OB.loss_and_grads(params, obj.reshape(-1, 3), src, dst, prop.reshape(-1, 100),
-                                         tgt.reshape(-1), 5, drop_r=dr, drop_o=do)
-    _bf16_check(z.reshape(-1), g, z_e, g_e, f"bf16 N={N} fully={fully} dropout={dropout}")
-    assert abs(loss - loss_e) <= 1e-4
+    ref, band = OB.noise_band(params, obj.reshape(-1, 3), src, dst, prop.reshape(-1, 100), tgt.reshape(-1), 5,
+                              drop_r=dr, drop_o=do)
+    _bf16_check(z.reshape(-1), g, ref, band, f"bf16 N={N} fully={fully} dropout={dropout}", loss)
 
 
 def test_config3_bf16_full_size_against_emulator():
-    """Config 3 in bf16 (65,536 fully connected 12-block towers, S = 5, training): sampled towers'
-    logits of the full batch and a sampled 16-tower sub-batch's gradients equal the bf16 emulator
-    at 1e-3."""
+    """Config 3 in bf16 (65,536 fully connected 12-block towers, S = 5, training): a sampled 16-tower
+    sub-batch's logits and gradients, and the full batch's logits of those towers, against the bf16
+    emulator inside the band of valid implementations."""
     B, N, S = 65536, 12, 5
     params = O.random_params(43)
     raw = D.synthetic_towers_fast(B, N, seed=13)
@@ -138,17 +149,22 @@ def test_config3_bf16_full_size_against_emulator():
     z, _, _ = _train(flat, TowerBatch.fully_connected(obj, device="cuda"), tgt, S, "bf16")
     z = z.reshape(B, N)
     pick = np.sort(np.random.default_rng(8).choice(B, 16, replace=False))
-    zs, _, gs = _train(flat, TowerBatch.fully_connected(obj[pick], device="cuda"), tgt[pick], S, "bf16")
+    zs, loss_s, gs = _train(flat, TowerBatch.fully_connected(obj[pick], device="cuda"), tgt[pick], S, "bf16")
     src, dst = _edges_full(len(pick), N)
-    _, z_e, g_e = OB.loss_and_grads(params, obj[pick].reshape(-1, 3), src, dst, np.zeros((len(pick) * N, 100)),
-                                    tgt[pick].reshape(-1), S)
-    _bf16_check(zs.reshape(-1), gs, z_e, g_e, "config 3 sub-batch")
-    assert np.all(np.abs(z[pick].reshape(-1) - z_e) <= BF16_TOL + BF16_TOL * np.abs(z_e))
+    ref, band = OB.noise_band(params, obj[pick].reshape(-1, 3), src, dst, np.zeros((len(pick) * N, 100)),
+                              tgt[pick].reshape(-1), S)
+    _bf16_check(zs.reshape(-1), gs, ref, band, "config 3 sub-batch", loss_s)
+    # the same towers inside the full batch: each tower's arithmetic does not depend on its position
+    # beyond the receiver-sum grouping, so the full batch's logits sit in the same band
+    dzf = z[pick].reshape(-1) - ref[1]
+    assert np.sqrt(np.mean(dzf ** 2)) <= BAND_FACTOR * band["z_rms"] + 1e-6
+    assert np.abs(dzf).max() <= BAND_FACTOR * band["z_max"] + 1e-5
 
 
 def test_config4_bf16_shard_against_emulator():
-    """Config 4's shard in bf16 (131,072 ragged 4–16-block towers, thresholded relations): sampled
-    towers' logits equal the bf16 emulator run on each tower alone, at 1e-3."""
+    """Config 4's shard in bf16 (131,072 ragged 4–16-block towers, thresholded relations, training
+    forward): 24 sampled towers' logits against the bf16 emulator run on those towers alone, inside
+    the band of valid implementations."""
     B, S = 131072, 5
     params = O.random_params(44)
     pos, sizes, src, dst, te, raws = D.ragged_batch(B, 4, 16, seed=9)
@@ -157,11 +173,19 @@ def test_config4_bf16_shard_against_emulator():
                      np.zeros(int(sizes.sum()), np.float32), S, "bf16")
     off = np.concatenate([[0], np.cumsum(sizes)])
     eoff = np.concatenate([[0], np.cumsum(te)])
-    for t in np.sort(np.random.default_rng(11).choice(B, 12, replace=False)):
+    pick = np.sort(np.random.default_rng(11).choice(B, 24, replace=False))
+    p_pos, p_src, p_dst, got, base = [], [], [], [], 0
+    for t in pick:
         n = int(sizes[t])
-        s_t, d_t = src[eoff[t]:eoff[t + 1]] - off[t], dst[eoff[t]:eoff[t + 1]] - off[t]
-        ze = OB.forward(O.to_torch(params), torch.tensor(pos[off[t]:off[t + 1]], dtype=torch.float64),
-                        torch.as_tensor(s_t, dtype=torch.long), torch.as_tensor(d_t, dtype=torch.long),
-                        torch.zeros(n, 100, dtype=torch.float64), S).numpy()
-        got = z[off[t]:off[t + 1]]
-        assert np.all(np.abs(got - ze) <= BF16_TOL + BF16_TOL * np.abs(ze)), (int(t), np.abs(got - ze).max())
+        p_pos.append(pos[off[t]:off[t + 1]])
+        p_src.append(src[eoff[t]:eoff[t + 1]] - off[t] + base)
+        p_dst.append(dst[eoff[t]:eoff[t + 1]] - off[t] + base)
+        got.append(z[off[t]:off[t + 1]])
+        base += n
+    p_pos = np.concatenate(p_pos)
+    ref, band = OB.noise_band(params, p_pos, np.concatenate(p_src), np.concatenate(p_dst), np.zeros((base, 100)),
+                              np.zeros(base), S)
+    dz = np.concatenate(got) - ref[1]
+    rms = float(np.sqrt(np.mean(dz ** 2)))
+    assert rms <= BAND_FACTOR * band["z_rms"] + 1e-6, (rms, band["z_rms"])
+    assert np.abs(dz).max() <= BAND_FACTOR * band["z_max"] + 1e-5, (np.abs(dz).max(), band["z_max"])

@@ -1,0 +1,98 @@
+"""GPU: replayed (hipGraph-captured) training steps — spwgnn_amd/replay.py.
+
+A replayed step must be the step the eager path runs: same dropout masks (the key read from a
+device word that spwgnn_step_advance moves on), same Adam step (lr_t from the host-built table),
+same batch arrays (refilled in place before each replay). Checked bit for bit:
+  * Keras fit with graph=True against graph=False (the same launches issued eagerly), and against
+    train_on_batch (host-side key and step, spwgnn_adam) on the same capacity-planned batches;
+  * Trainer.replay_body replays against Trainer.step on changing batches.
+Reference: the training loop of src/main.py:92-98 (batch 32) and Networks.py:101-102 (Adam, BCE).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model as O
+from spwgnn_amd import data as D, params as P
+from spwgnn_amd.batch import HostPlan, TowerBatch
+from spwgnn_amd.keras_api import CompactDataset, PropagationNetwork
+from spwgnn_amd.replay import ReplayStep
+from spwgnn_amd.trainer import Trainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _xy(n, seed):
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(n, 6, seed=seed, fully_connected=False)
+    return ({"objects": obj, "sender_relations": Rs, "receiver_relations": Rr, "propagation": prop},
+            {"target": tgt.reshape(n, 6, 1)})
+
+
+def test_fit_replayed_equals_eager_bitwise():
+    """model.fit with every step a replayed hipGraph == the same fit issued eagerly: per-epoch
+    losses/accuracies and the final weights, bit for bit (batch 32 plus a partial last batch: two
+    captured geometries), and a second fit call continues from the device counters."""
+    x, y = _xy(150, 7)
+    res = []
+    for graph in (True, False):
+        model = PropagationNetwork(seed=0).getModel(6)
+        h1 = model.fit(x, y, batch_size=32, epochs=3, validation_split=0.2, verbose=0, graph=graph)
+        h2 = model.fit(x, y, batch_size=32, epochs=1, validation_split=0.2, verbose=0, graph=graph, seed=5)
+        torch.cuda.synchronize()
+        res.append((h1, h2, model.net.flat.detach().cpu().numpy().copy(), model.iterations, model.net._step_seed,
+                    model._replays))
+    (ha, ha2, wa, ia, ka, ra), (hb, hb2, wb, ib, kb, rb) = res
+    assert ha == hb and ha2 == hb2
+    assert np.array_equal(wa, wb)
+    assert ia == ib == 4 * 4 and ka == kb                    # 120 training towers → 4 steps per epoch
+    assert sum(s.replays for s in ra.steps.values()) == 16 - len(ra.steps)   # first call of a geometry is eager
+    assert all(s.graph is None for s in rb.steps.values())
+    assert ha["loss"][-1] < ha["loss"][0]
+
+
+def test_fit_steps_equal_train_on_batch():
+    """The replayed step's device-side key and Adam step reproduce the host-side path
+    (train_on_batch: key from net._step_seed, spwgnn_adam at model.iterations) bit for bit."""
+    x, y = _xy(64, 9)
+    ma = PropagationNetwork(seed=3).getModel(6)
+    ma.fit(x, y, batch_size=32, epochs=1, validation_split=0.0, shuffle=False, verbose=0)
+    mb = PropagationNetwork(seed=3).getModel(6)
+    ds = CompactDataset(x["objects"], x["sender_relations"], x["receiver_relations"], x["propagation"])
+    tgt = y["target"].reshape(64, 6)
+    for b0 in (0, 32):
+        idx = np.arange(b0, b0 + 32)
+        batch = TowerBatch.from_plan(ds.subset_plan(idx, edge_cap=True), "cuda")
+        mb.train_on_batch(batch, torch.as_tensor(tgt[idx].reshape(-1), device="cuda"))
+    torch.cuda.synchronize()
+    assert np.array_equal(ma.net.flat.detach().cpu().numpy(), mb.net.flat.detach().cpu().numpy())
+    assert ma.iterations == mb.iterations == 2 and ma.net._step_seed == mb.net._step_seed
+
+
+def test_trainer_replay_equals_step():
+    """Trainer.replay_body (splitmix key mode, x6 math, dropout 0.1) replayed over three different
+    batches of one geometry == Trainer.step on the same batches, bit for bit (parameters and both
+    Adam moments)."""
+    params = O.random_params(12)
+    plans, tgts = [], []
+    for seed in (1, 2, 3):
+        raw = D.synthetic_towers(32, 6, seed=seed)
+        obj = (raw / D.RELATION_THRESHOLD).astype(np.float32)
+        Rs, Rr = D.relation_matrices(raw, D.RELATION_THRESHOLD)
+        e = np.array(O.dense_to_edges(Rs, Rr), np.int64).reshape(-1, 4)
+        te = np.bincount(e[:, 0], minlength=32).astype(np.int32)
+        plans.append(HostPlan.build(obj.reshape(-1, 3), np.full(32, 6, np.int32), e[:, 0] * 6 + e[:, 2],
+                                    e[:, 0] * 6 + e[:, 3], te, edge_cap=30))
+        tgts.append(np.random.default_rng(seed).integers(0, 2, 192).astype(np.float32))
+    assert len({p.geometry for p in plans}) == 1
+    ta = Trainer(P.to_flat(params, device="cuda"), mp_steps=5, dropout=0.1, seed=11, math="x6")
+    for p, t in zip(plans, tgts):
+        ta.step(TowerBatch.from_plan(p, "cuda"), torch.as_tensor(t, device="cuda"))
+    tb = Trainer(P.to_flat(params, device="cuda"), mp_steps=5, dropout=0.1, seed=11, math="x6")
+    rs = ReplayStep(plans[0], "cuda", tb.replay_body(plans[0].n_nodes))
+    for p, t in zip(plans, tgts):
+        rs(p, t)
+        tb.iterations += 1
+    torch.cuda.synchronize()
+    assert rs.replays == 2
+    assert torch.equal(ta.params, tb.params) and torch.equal(ta.m, tb.m) and torch.equal(ta.v, tb.v)
+    assert int(tb._ctr.step.item()) == 3

@@ -23,7 +23,10 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.lib()
     for name in sorted(declared):
         assert hasattr(lib, name), name
-    assert lib.spwgnn_version() == 1
+    ver = int(re.search(r"#define SPWGNN_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.spwgnn_version() == ver == _lib.ABI_VERSION
+    # the ctypes run struct ends with the field the header declares last
+    assert _lib.RunC._fields_[-1][0] == re.search(r"(\w+);\s*\} spwgnn_run;", hdr).group(1)
     assert b"workspace" in lib.spwgnn_strerror(-4)
 
 
@@ -315,3 +318,48 @@ def test_vectorised_jenga_builder_equals_scalar(n):
         np.testing.assert_array_equal(vec[t], tower)
     fast = D.synthetic_towers_fast(64, n, seed=3)
     assert fast.shape == (64, n, 3) and np.all(fast[..., 2] >= D.RECT_WIDTH_MIN)
+
+
+def test_capacity_plan_shares_geometry_and_edge_layout():
+    """spwgnn_plan_fill_cap: blocks sized for N(N-1) edges per tower, so two batches of 6-block
+    towers with different relation sets get the same wave-tiles and block counts (one captured
+    graph); each real edge sits where the actual-count plan puts it, the rest is padding (-1)."""
+    from spwgnn_amd.batch import HostPlan
+    geo = set()
+    for seed in (1, 2, 3):
+        obj, Rs, Rr, prop, _ = D.synthetic_batch(32, 6, seed=seed, fully_connected=False)
+        e = np.array(O.dense_to_edges(Rs, Rr), np.int64).reshape(-1, 4)
+        src, dst = (e[:, 0] * 6 + e[:, 2]).astype(np.int32), (e[:, 0] * 6 + e[:, 3]).astype(np.int32)
+        te = np.bincount(e[:, 0], minlength=32).astype(np.int32)
+        nodes = np.full(32, 6, np.int32)
+        plain = HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te)
+        cap = HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te, edge_cap=30)
+        geo.add(cap.geometry)
+        assert cap.n_wtiles == plain.n_wtiles == 16 and cap.n_eblocks == 32 >= plain.n_eblocks
+        wp, wc = plain.arrays[3], cap.arrays[3]
+        assert np.array_equal(wp[:, [2, 3]], wc[:, [2, 3]])           # same towers per wave-tile
+        for t in range(16):
+            a, n = wp[t, 0], wp[t, 1]
+            b, m = wc[t, 0], wc[t, 1]
+            assert m == 2 and n <= m
+            for arr in (4, 5):
+                got = cap.arrays[arr][32 * b: 32 * (b + m)]
+                want = plain.arrays[arr][32 * a: 32 * (a + n)]
+                assert np.array_equal(got[:len(want)], want) and np.all(got[len(want):] == -1)
+            assert np.array_equal(cap.arrays[6][b: b + n], plain.arrays[6][a: a + n])
+    assert len(geo) == 1
+    with pytest.raises(ValueError):
+        HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te, edge_cap=1)
+
+
+def test_adam_lr_table_is_keras_adam_lr_t():
+    """spwgnn_adam_lr_table (host, the table replayed steps read lr_t from) = Keras-2.x Adam's
+    lr_t = lr·sqrt(1−β2^t)/(1−β1^t) (Networks.py:101), rounded to fp32 once."""
+    out = np.zeros(5000, np.float32)
+    assert _lib.lib().spwgnn_adam_lr_table(5e-4, 0.9, 0.999, len(out), out.ctypes.data) == 0
+    t = np.arange(1, len(out), dtype=np.float64)
+    want = (np.float32(5e-4).astype(np.float64) * np.sqrt(1 - np.float32(0.999).astype(np.float64) ** t)
+            / (1 - np.float32(0.9).astype(np.float64) ** t)).astype(np.float32)
+    assert out[0] == 0.0
+    assert np.array_equal(out[1:], want)
+    assert _lib.lib().spwgnn_adam_lr_table(5e-4, 0.9, 0.999, 1, out.ctypes.data) != 0
