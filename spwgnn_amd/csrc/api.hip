@@ -539,6 +539,10 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.RN = w.RN;
         a.S = (int)(g.rows / w.RE);
         a.a_b16 = (g.b16 & kB16A) != 0;
+        a.wtile = b->wtile;
+        a.n_wtiles = b->n_wtiles;
+        a.nw_max = b->nw_max;
+        a.w2_tile = !getenv_flag("SPWGNN_W2G_GATHER");   // A/B switch: the per-edge gather kernel
     }
     // stored chunk-major operands in x6 math: the warp-specialized kernel, one workgroup per CU
     if (math != MATH_F32 && g.xmode == XM_CM && (g.ymode == YM_CM || g.ymode == YM_ROW) &&

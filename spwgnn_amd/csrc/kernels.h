@@ -225,6 +225,9 @@ struct WgradArgs {
     int64_t RE, RN;
     int S;                         // steps (XM_H1 / YM_DH2 walk rows as (edge block, step) stages)
     int a_b16;                     // bf16 math: A stored as bf16 (k_w2grad_ws)
+    const int32_t* wtile;          // the batch plan's wave-tiles (k_w2grad_tile walks whole tiles)
+    int n_wtiles, nw_max;
+    int w2_tile;                   // 1: the W2 gradient with LDS-staged node rows (bf16 math)
     float* slab;           // [chunks][kx_pad][ny_pad]
 };
 struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 32-row blocks

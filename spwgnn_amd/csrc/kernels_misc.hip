@@ -718,6 +718,259 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
     __syncthreads();   // the matrix waves' last stage
 }
 
+// W2 gradient with the node rows staged in LDS per (wave-tile, step) — bf16 math. The per-edge
+// gathers of U[src], V[dst], G3[dst] bound k_w2grad_ws there: diagnosis builds at config 3 (65,536
+// fully connected 12-block towers) ran 8.4 ms with the gathers, 7.2 ms with every gather hitting the
+// cache, 2.5 ms without them — the vector-memory instruction stream, not HBM. Here a workgroup walks
+// whole wave-tiles (tile-major, then step, then 32-edge block): for each (tile, step) group the ≤ 16
+// node rows of U, V and G3 are loaded once with coalesced loads (one group ahead, into registers) and
+// written to an LDS node buffer (double-buffered by group parity); each edge then reads its rows
+// from LDS. A rows and the h2 > 0 words stay per-stage global loads (contiguous per block). Matrix
+// waves, images, products and the per-workgroup slab are k_w2grad_ws's; stages differ only in order,
+// so the gradient is the same sum in a different fixed order (deterministic).
+constexpr int kW2tNodes = 16;                          // ≤ 16-node wave-tiles (default plan for N ≤ 16)
+constexpr int kW2tChunks = kRowE / 4;                  // 38 float4 chunks per 152-feature row
+constexpr int kW2tUnits = 3 * kW2tNodes * kW2tChunks;  // U, V, G3 chunks of one group: 1824
+constexpr int kW2tPf = (kW2tUnits + 255) / 256;        // per staging thread: 8
+
+struct W2tSet {
+    uint2 ah[5];
+    float4 a[5];
+    uint32_t m[5];
+    int src, dst;
+};
+struct W2tIt {   // stage iterator (wave-uniform): tile ti, step s, block bb of the tile
+    int ti, s, bb;
+    int4 info;   // wtile[ti]: first block, blocks, first node, nodes
+};
+
+// DBG (diagnosis builds, SPWGNN_W2G_DBG with SPWGNN_DIAG; wrong results): 1 no node-row LDS reads,
+// 2 no per-stage global loads (A, h2 words, indices), 4 no node-row loads/stores, 8 no staging
+// stores (nor the arithmetic feeding them), 16 no MFMAs
+template <int NP, bool AB16, int DBG = 0>
+__global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_w2grad_tile(WgradArgs a, int64_t blk_per_wg) {
+    using IM = X6Img<160>;
+    constexpr int IMG = NP * IM::PART;
+    __shared__ __attribute__((aligned(16))) char buf[2][2 * IMG];            // [stage parity][X | Y]
+    __shared__ __attribute__((aligned(16))) float4 nodes[2][kW2tUnits];      // [group parity][arr][node][chunk]
+    const int tid = threadIdx.x;
+    const int S = a.S;
+    const int nt = a.n_wtiles;
+    const int4* wt = reinterpret_cast<const int4*>(a.wtile);
+    const int64_t nblk = a.RE >> 5;
+    // this workgroup's wave-tiles: those whose first block lies in [w·bpw, (w+1)·bpw)
+    auto lower = [&](int64_t blk) {
+        int lo = 0, hi = nt;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (wt[mid].x < blk) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    };
+    const int tlo = lower((int64_t)blockIdx.x * blk_per_wg);
+    const int thi = lower((int64_t)(blockIdx.x + 1) * blk_per_wg);
+    const int64_t blo = tlo < nt ? wt[tlo].x : nblk, bhi = thi < nt ? wt[thi].x : nblk;
+    const int T = (int)(bhi - blo) * S;
+    if (tid < 256) {
+        // ---------------- matrix waves (as k_w2grad_ws) ----------------
+        const int lane = tid & 63, c16 = lane & 15, kq = lane >> 4;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int wx = wave >> 1, wy = wave & 1;
+        f32x4 acc[5][5];
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+#pragma unroll
+            for (int y = 0; y < 5; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int ox[5], oy[5];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) ox[x] = IM::roff(lane, 5 * wx + x);
+#pragma unroll
+        for (int y = 0; y < 5; ++y) oy[y] = IM::roff(lane, 5 * wy + y);
+        __syncthreads();   // group 0's node rows in LDS (the staging waves' prologue barrier)
+        __syncthreads();   // stage 0 staged
+        for (int t = 0; t < T; ++t) {
+            const char* Xs = buf[t & 1];
+            const char* Ys = Xs + IMG;
+            if constexpr ((DBG & 16) != 0) { __syncthreads(); continue; }
+            bf16x8 yb[5][3], xa[2][3];
+            IM::template get<NP>(Xs, ox[0], xa[0]);
+            IM::template get<NP>(Ys, oy[0], yb[0]);
+#pragma unroll
+            for (int y = 0; y < 5; ++y) {
+                if (y < 4) IM::template get<NP>(Ys, oy[y + 1], yb[y + 1]);
+                else IM::template get<NP>(Xs, ox[1], xa[1]);
+                __builtin_amdgcn_sched_barrier(0);
+                acc[0][y] = mfma16_x6<NP>(xa[0], yb[y], acc[0][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int x = 1; x < 5; ++x) {
+                if (x < 4) IM::template get<NP>(Xs, ox[x + 1], xa[(x + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int y = 0; y < 5; ++y) acc[x][y] = mfma16_x6<NP>(xa[x & 1], yb[y], acc[x][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+        }
+        float* out = a.slab + (int64_t)blockIdx.x * 160 * 160;
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+#pragma unroll
+            for (int y = 0; y < 5; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    out[(int64_t)(16 * (5 * wx + x) + 4 * kq + r) * 160 + 16 * (5 * wy + y) + c16] = acc[x][y][r];
+        return;
+    }
+    // ---------------- staging waves ----------------
+    const int st = tid - 256, rr = st & 31, c0 = st >> 5;
+    const bool k4ok = __builtin_amdgcn_readfirstlane(st >> 6) < 3;   // c0 < 6: chunk c0 + 32 < 38
+    int off[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) off[k] = (k < 4 || k4ok) ? cm_offk<kKhE>(0, 4 * (c0 + 8 * k)) : 0;
+    const int64_t nstep_n = a.RN * kRowE;
+    if (T == 0) {   // the matrix waves' two barriers (they write a zero slab)
+        __syncthreads();
+        __syncthreads();
+        return;
+    }
+    auto tile_info = [&](int ti) { return wt[ti < thi ? ti : thi - 1]; };
+    auto advance = [&](W2tIt& it) {
+        if (++it.bb >= it.info.y) {
+            it.bb = 0;
+            if (++it.s >= S) {
+                it.s = 0;
+                ++it.ti;
+                it.info = tile_info(it.ti);
+            }
+        }
+    };
+    auto fetch = [&](const W2tIt& it, W2tSet& R) {
+        if constexpr ((DBG & 2) != 0) {
+            R.src = R.dst = rr;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) { R.ah[k] = make_uint2(0x3f803f80u, 0u); R.a[k] = f4zero(); R.m[k] = ~0u; }
+            return;
+        }
+        const int64_t b = (int64_t)it.info.x + it.bb;
+        R.src = a.esrc[32 * b + rr];
+        R.dst = a.edst[32 * b + rr];
+        const int64_t ia = b * kCmBlk + rr * 4;
+        load_m2(a.mask2 + ((int64_t)it.s * nblk + b) * kM2Blk, rr, R.m);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + ia + off[k]);
+            else R.a[k] = *reinterpret_cast<const float4*>(a.A + ia + off[k]);
+        }
+    };
+    // one group's node rows: unit u = (arr·38 + chunk)·16 + node (node fastest: coalesced per chunk)
+    float4 pf[kW2tPf];
+    auto node_fetch = [&](int ti, int s) {
+        if constexpr ((DBG & 4) != 0) return;
+        const int4 inf = tile_info(ti);
+        const int64_t ns = (int64_t)s * nstep_n;
+#pragma unroll
+        for (int j = 0; j < kW2tPf; ++j) {
+            const int u = st + 256 * j;
+            const int arr = u / (kW2tChunks * kW2tNodes), rem = u - arr * (kW2tChunks * kW2tNodes);
+            const int q = rem >> 4, nd = rem & 15;
+            pf[j] = f4zero();
+            if (u < kW2tUnits && nd < inf.w) {
+                const float* base = arr == 0 ? a.U : (arr == 1 ? a.V : a.G3);
+                pf[j] = *reinterpret_cast<const float4*>(base + ns + cm_index<kKhE>(inf.z + nd, 4 * q));
+            }
+        }
+    };
+    auto node_store = [&](int par) {
+        if constexpr ((DBG & 4) != 0) return;
+#pragma unroll
+        for (int j = 0; j < kW2tPf; ++j) {
+            const int u = st + 256 * j;
+            const int arr = u / (kW2tChunks * kW2tNodes), rem = u - arr * (kW2tChunks * kW2tNodes);
+            const int q = rem >> 4, nd = rem & 15;
+            if (u < kW2tUnits) nodes[par][(arr * kW2tNodes + nd) * kW2tChunks + q] = pf[j];
+        }
+    };
+    int gpar = 0;   // node buffer of the group being built
+    auto build = [&](const W2tIt& it, const W2tSet& R, char* Xs) {
+        if (it.bb == 0) {   // first stage of its group: fetch the next group's rows
+            const bool more_steps = it.s + 1 < S;
+            node_fetch(more_steps ? it.ti : it.ti + 1, more_steps ? it.s + 1 : 0);
+        }
+        char* Ys = Xs + IMG;
+        const float4* nb = nodes[gpar];
+        const bool in = R.src >= 0;
+        const int sl = in ? R.src - it.info.z : 0, dl = in ? R.dst - it.info.z : 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k == 4 && !k4ok) break;
+            const int cg = c0 + 8 * k;
+            const float4 u = (DBG & 1) ? make_float4(0.1f, 0.2f, 0.3f, 0.4f) : nb[sl * kW2tChunks + cg];
+            const float4 v = (DBG & 1) ? make_float4(0.1f, 0.2f, 0.3f, 0.4f) : nb[(kW2tNodes + dl) * kW2tChunks + cg];
+            const float4 gv = (DBG & 1) ? make_float4(0.1f, 0.2f, 0.3f, 0.4f) : nb[(2 * kW2tNodes + dl) * kW2tChunks + cg];
+            float4 x = f4relu(f4add3(AB16 ? unpack4_bf16(R.ah[k]) : R.a[k], u, v));
+            if (k == 4 && c0 == 5) x.z = 1.f;   // feature 150: the b2 ones column
+            const int w = (int)(in ? R.m[k] : 0u);
+            const float4 y = make_float4(
+                __int_as_float(__float_as_int(gv.x) & __builtin_amdgcn_sbfe(w, 4 * c0, 1)),
+                __int_as_float(__float_as_int(gv.y) & __builtin_amdgcn_sbfe(w, 4 * c0 + 1, 1)),
+                __int_as_float(__float_as_int(gv.z) & __builtin_amdgcn_sbfe(w, 4 * c0 + 2, 1)),
+                __int_as_float(__float_as_int(gv.w) & __builtin_amdgcn_sbfe(w, 4 * c0 + 3, 1)));
+            if constexpr ((DBG & 8) == 0) {
+                IM::template put<NP>(Xs, rr, cg, x);
+                IM::template put<NP>(Ys, rr, cg, y);
+            }
+        }
+        if (it.bb == it.info.y - 1) {   // last stage of its group: the next group's rows → LDS
+            node_store(gpar ^ 1);
+            gpar ^= 1;
+        }
+    };
+    if (!k4ok) {   // padding columns 152..159 of both operands in both buffers stay zero
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            IM::template put<NP>(buf[p], rr, c0 + 32, f4zero());
+            IM::template put<NP>(buf[p] + IMG, rr, c0 + 32, f4zero());
+        }
+    }
+    // prologue: group 0's rows, stages 0 and 1 fetched, stage 0 built
+    W2tIt ib{tlo, 0, 0, tile_info(tlo)};
+    node_fetch(ib.ti, 0);
+    node_store(0);
+    __syncthreads();   // group 0's node rows visible to every staging wave
+    W2tIt i1 = ib;
+    advance(i1);
+    W2tIt i2 = i1;
+    advance(i2);
+    W2tSet R0, R1;
+    fetch(ib, R0);
+    fetch(i1, R1);
+    build(ib, R0, buf[0]);
+    __syncthreads();   // stage 0 staged
+    // iteration t: fetch stage t+2 into the set stage t used, build stage t+1, barrier
+    int t = 0;
+    for (; t + 2 < T; t += 2) {
+        fetch(i2, R0);
+        build(i1, R1, buf[1]);
+        __syncthreads();
+        i1 = i2;
+        advance(i2);
+        fetch(i2, R1);
+        build(i1, R0, buf[0]);
+        __syncthreads();
+        i1 = i2;
+        advance(i2);
+    }
+    if (t + 1 < T) {   // t even: build stage t+1 from set 1
+        build(i1, R1, buf[1]);
+        __syncthreads();
+        ++t;
+    }
+    __syncthreads();   // the matrix waves' last stage
+}
+
 // Stored-operand weight gradients (x6), warp-specialized like k_w2grad_ws: dW[k][n] =
 // Σ_rows X[row][k]·Y[row][n] with X chunk-major and Y chunk-major (YROW = 0) or row-major
 // (YROW = 1, stride 160: the dA rows). Stages are 32-row blocks t = (step s, block nb) of a
@@ -1115,6 +1368,36 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
 #endif
     const dim3 g(wgs), b(kW2gThreads);
     if (math == MATH_BF16) {
+#ifdef SPWGNN_DIAG
+        if (a.a_b16 && dbg && dbg < 100) {
+            switch (dbg) {
+                case 1: hipLaunchKernelGGL((k_w2grad_ws<1, 1, true>), g, b, 0, st, a, blk_per_wg); break;
+                case 2: hipLaunchKernelGGL((k_w2grad_ws<2, 1, true>), g, b, 0, st, a, blk_per_wg); break;
+                case 4: hipLaunchKernelGGL((k_w2grad_ws<4, 1, true>), g, b, 0, st, a, blk_per_wg); break;
+                case 32: hipLaunchKernelGGL((k_w2grad_ws<32, 1, true>), g, b, 0, st, a, blk_per_wg); break;
+                case 33: hipLaunchKernelGGL((k_w2grad_ws<33, 1, true>), g, b, 0, st, a, blk_per_wg); break;
+                case 36: hipLaunchKernelGGL((k_w2grad_ws<36, 1, true>), g, b, 0, st, a, blk_per_wg); break;
+                default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
+#endif
+        if (a.w2_tile && a.nw_max <= kW2tNodes) {   // node rows via LDS (k_w2grad_tile)
+#ifdef SPWGNN_DIAG
+            if (a.a_b16 && dbg >= 100) {   // the tile kernel's diagnosis variants: SPWGNN_W2G_DBG = 100 + bits
+                switch (dbg - 100) {
+#define W2T_CASE(d) case d: hipLaunchKernelGGL((k_w2grad_tile<1, true, d>), g, b, 0, st, a, blk_per_wg); break;
+                    W2T_CASE(1) W2T_CASE(2) W2T_CASE(4) W2T_CASE(8) W2T_CASE(16) W2T_CASE(3) W2T_CASE(6) W2T_CASE(7)
+#undef W2T_CASE
+                    default: return hipErrorInvalidValue;
+                }
+                return hipGetLastError();
+            }
+#endif
+            if (a.a_b16) hipLaunchKernelGGL((k_w2grad_tile<1, true>), g, b, 0, st, a, blk_per_wg);
+            else hipLaunchKernelGGL((k_w2grad_tile<1, false>), g, b, 0, st, a, blk_per_wg);
+            return hipGetLastError();
+        }
         if (a.a_b16) hipLaunchKernelGGL((k_w2grad_ws<0, 1, true>), g, b, 0, st, a, blk_per_wg);
         else hipLaunchKernelGGL((k_w2grad_ws<0, 1>), g, b, 0, st, a, blk_per_wg);
         return hipGetLastError();
