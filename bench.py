@@ -574,13 +574,14 @@ def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
         "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16" if math == "bf16" else "f32", "math": MATH_DESC[math],
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
-        "config": {"workload": wl + "; each step a replayed hipGraph (batch arrays copied in per step)",
+        "config": {"workload": wl, "step_mode": "each step one replayed hipGraph (batch arrays copied in per step)",
                    "baseline_config": args.config, "towers_per_gpu": cfg["towers"], "global_batch": cfg["towers"],
                    "nodes_per_tower": cfg["nodes"], "nodes_per_gpu": Nn, "edges_per_gpu": Ne, "mp_steps": S,
                    "math": math, "parallelism": "dp1", "replays": rs.replays, "eblocks_planned": plan.n_eblocks},
         "step_tflops": round(step_flops(Ne, Nn, S) * args.steps / el / 1e12, 4),
         "loss": round(loss, 5), "roofline": roof, "kernels": table, "cpu_baseline": None,
     }
+    out["hbm"] = step_hbm(args.config, out["ms_per_step"], math, wl)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     print(json.dumps(out), flush=True)
