@@ -2,8 +2,10 @@
 replayed for every later batch of the same geometry.
 
 The reference trains with Keras fit at batch 32 (src/main.py:92-98). At that size a step is ~50
-small kernel launches and the host's launch latency, not the GPU, sets the rate. A replayed step
-issues the whole sequence as one graph launch. What a capture bakes in, and how it stays valid:
+small kernel launches; a replayed step issues the whole sequence as one graph launch, so the host
+only prepares the next batch (measured on MI355X, BASELINE config 1: the replayed step is the
+kernels' own 0.40 ms — the small-batch kernels' latency, not launch overhead, is what remains;
+DESIGN.md §3k). What a capture bakes in, and how it stays valid:
 
 * sizes — the batch is planned with per-tower block capacity N(N−1) (spwgnn_plan_fill_cap), so
   every batch of B towers of N boxes has the same wave-tiles and blocks whatever its relations
@@ -29,7 +31,9 @@ import torch
 from . import _lib, engine as E
 from .batch import HostPlan, TowerBatch
 
-LR_TABLE_LEN = 1 << 20      # Adam steps covered by one lr table (4 MiB); a longer run rebuilds
+# Adam steps covered by one lr table (4 MiB); later steps read the last entry, which is exact: lr_t
+# = lr·sqrt(1−β2^t)/(1−β1^t) equals lr in fp32 from t ≈ 2·10^4 on (β2 = 0.999)
+LR_TABLE_LEN = 1 << 20
 
 
 def _i64(x: int) -> int:
@@ -76,13 +80,24 @@ class StaticBatch:
             views.append(self.buf[o:o + a.nbytes].view(dt).view(a.shape))
         self.target = self.buf[self.t_off:self.t_off + 4 * plan.n_nodes].view(torch.float32)
         self.batch = TowerBatch.from_plan(plan, self.device, dev_arrays=views)
+        # pinned staging ring: a slot is refilled only after the copy that last read it has run
+        # (its event), so the host never waits on the step in flight and never allocates per step
+        self.ring = [torch.empty(self.total, dtype=torch.uint8, pin_memory=True) for _ in range(self.RING)]
+        self.ring_ev = [None] * self.RING
+        self.loads = 0
+
+    RING = 3
 
     def load(self, plan: HostPlan, target: np.ndarray):
-        """This step's plan arrays and targets → the static buffers (pinned staging, non-blocking
-        copy; the caching host allocator keeps the staging block until the copy has run)."""
+        """This step's plan arrays and targets → the static buffers (one pinned staging slot, one
+        non-blocking copy on the current stream)."""
         if plan.geometry != self.geometry:
             raise ValueError("batch geometry differs from the captured one")
-        host = torch.empty(self.total, dtype=torch.uint8, pin_memory=True)
+        slot = self.loads % self.RING
+        self.loads += 1
+        if self.ring_ev[slot] is not None:
+            self.ring_ev[slot].synchronize()
+        host = self.ring[slot]
         hv = host.numpy()
         for a, o in zip(plan.arrays, self.offsets):
             hv[o:o + a.nbytes] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
@@ -91,6 +106,9 @@ class StaticBatch:
             raise ValueError("one target per node")
         hv[self.t_off:self.t_off + t.nbytes] = t.view(np.uint8)
         self.buf.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.ring_ev[slot] = ev
         # host-side copies the wrappers keep for reporting (edge ids, counts) follow the new batch
         b = self.batch
         b.tower_edges, b.src, b.dst, b.edge_id = plan.tower_edges, plan.src, plan.dst, plan.edge_id
