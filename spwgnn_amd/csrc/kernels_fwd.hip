@@ -909,9 +909,11 @@ __global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_pe
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? SPWGNN_EFWD_PF : 5;
     static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
-    __shared__ uint4 wl[50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
-    for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
-    __syncthreads();
+    __shared__ uint4 wl[DBG == 2 ? 64 : 50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
+    if constexpr (DBG != 2) {
+        for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int4* wtiles = reinterpret_cast<const int4*>(a.wtile);
@@ -1026,7 +1028,8 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                 for (int v = 0; v < NT; ++v) {
                     const int u = (kb * 5 + T0 + v) * 3 * 64;
 #pragma unroll
-                    for (int q = 0; q < NP; ++q) bp[v][q] = as_bf16x8(wlb.at(u + 64 * q));
+                    for (int q = 0; q < NP; ++q)   // DBG 2 (diagnosis): the image streamed from L2, LDS left free
+                        bp[v][q] = as_bf16x8(DBG == 2 ? a.x_w2[u + 64 * q + lane] : wlb.at(u + 64 * q));
                 }
                 mfma32_x6_group<NP, NT>(ap, bp, acc + T0);
             };
@@ -1166,6 +1169,10 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
 #endif
         if (a.nw_max <= 16 && dbg == 1)   // diagnosis: A rows from 8 cached blocks
             hipLaunchKernelGGL((k_edge_fwd_x6<true, 1>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+#ifdef SPWGNN_DIAG
+        else if (a.nw_max <= 16 && dbg == 2)   // diagnosis: W2 image from L2 instead of LDS
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 2>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+#endif
         else if (a.nw_max <= 16)
             hipLaunchKernelGGL(k_edge_fwd_x6<true>, dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         else
