@@ -666,9 +666,15 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 #ifndef SPWGNN_EBWD_PF
 #define SPWGNN_EBWD_PF 2
 #endif
-template <bool ACCUM, bool NODA = false, int NP = 3>
+#ifndef SPWGNN_EBWD_PF_B16
+#define SPWGNN_EBWD_PF_B16 5
+#endif
+#ifndef SPWGNN_DA_PF_B16
+#define SPWGNN_DA_PF_B16 5
+#endif
+template <bool ACCUM, bool NODA = false, int NP = 3, int DBG = 0>   // DBG 3 (diagnosis): G3 rows of the tile's first node
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
-    constexpr int PF = SPWGNN_EBWD_PF, kWaves = 8;
+    constexpr int PF = NP == 1 ? SPWGNN_EBWD_PF_B16 : SPWGNN_EBWD_PF, kWaves = 8;   // bf16: see k_dA_x6
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
     for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2t[idx];
     __syncthreads();
@@ -687,7 +693,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         return p;
     };
     auto g_of = [&](int d, int n0) {
-        return reinterpret_cast<const float4*>(a.G3 + cm_index<kKhE>(d >= 0 ? d : n0, 0) + h * 128);
+        return reinterpret_cast<const float4*>(a.G3 + cm_index<kKhE>(DBG == 3 ? n0 : (d >= 0 ? d : n0), 0) + h * 128);
     };
     struct KB { float4 g[2]; };
     auto ld = [&](const float4* G4, int kb, KB& r) {
@@ -841,6 +847,13 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
         // no_dA: dA = Σ_s dh1pre_s is rebuilt once after the step loop by k_dA_x6 (launch_dA)
         if (a.no_dA) {
+#ifdef SPWGNN_DIAG
+            static const int edbg = getenv("SPWGNN_EBWD_DBG") ? atoi(getenv("SPWGNN_EBWD_DBG")) : 0;
+            if (math == MATH_BF16 && edbg == 3) {
+                hipLaunchKernelGGL((k_edge_bwd_x6<false, true, 1, 3>), g, b, 0, st, a);
+                return hipGetLastError();
+            }
+#endif
             if (math == MATH_BF16) hipLaunchKernelGGL((k_edge_bwd_x6<false, true, 1>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_edge_bwd_x6<false, true>), g, b, 0, st, a);
             return hipGetLastError();
@@ -882,7 +895,8 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
 // W2ᵀ (x6 image) is the LDS B operand; blocks are independent (no tile structure needed).
 template <int NP = 3, bool B16 = false>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_dA_x6(DaArgs a) {
-    constexpr int kWaves = 8, PF = 2;
+    // bf16 math (NP = 1): a k-block is 5 MFMAs, so the G3 rows run further ahead to cover HBM latency
+    constexpr int kWaves = 8, PF = NP == 1 ? SPWGNN_DA_PF_B16 : 2;
     static_assert(10 % PF == 0, "ring slots carry over between (block, step) pairs");
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
     for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2t[idx];

@@ -904,10 +904,14 @@ struct NodeSum16X6 {
 #ifndef SPWGNN_EFWD_PF
 #define SPWGNN_EFWD_PF 1
 #endif
+#ifndef SPWGNN_EFWD_PF_B16
+#define SPWGNN_EFWD_PF_B16 2
+#endif
 template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false>   // AB16: A stored as bf16 (§3g)
 __global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
-    constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? SPWGNN_EFWD_PF : 5;
+    // bf16 math (NP = 1): a k-block is 5 MFMAs, too short to cover a load one k-block ahead
+    constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? (NP == 1 ? SPWGNN_EFWD_PF_B16 : SPWGNN_EFWD_PF) : 5;
     static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
     __shared__ uint4 wl[DBG == 2 ? 64 : 50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
     if constexpr (DBG != 2) {
@@ -923,7 +927,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     // a block's h1 operand sources: A rows and the gathered U[s], V[r] rows (chunk q at +256q / +64q)
     struct Src { int64_t ai; const float4 *U, *V; };   // ai: element index of the A rows
     auto src_of = [&](int blk, int2 sd, int n0) {
-        const int sc = sd.x >= 0 ? sd.x : n0, dc = sd.x >= 0 ? sd.y : n0;
+        const int sc = DBG == 3 ? n0 : (sd.x >= 0 ? sd.x : n0), dc = DBG == 3 ? n0 : (sd.x >= 0 ? sd.y : n0);
         return Src{(int64_t)(DBG == 1 ? (blk & 7) : blk) * kCmBlk + h * 128 + i * 4,
                    reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128),
                    reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128)};
@@ -1151,6 +1155,17 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
     if (math == MATH_BF16) {
+#ifdef SPWGNN_DIAG   // 1: A rows from 8 cached blocks; 3: U, V rows of the tile's first node (wrong results)
+        static const int bdbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;
+        if (a.nw_max <= 16 && a.a_b16 && bdbg == 1) {
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 1, 1, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+            return hipGetLastError();
+        }
+        if (a.nw_max <= 16 && a.a_b16 && bdbg == 3) {
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 3, 1, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+            return hipGetLastError();
+        }
+#endif
         if (a.nw_max <= 16 && a.a_b16)
             hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         else if (a.a_b16)
