@@ -127,17 +127,6 @@ typedef struct spwgnn_run {
      * run time instead of `seed`, so a captured step draws new masks on every replay once
      * spwgnn_step_advance has moved the key on. NULL = use `seed`. */
     const uint64_t* seed_dev;
-    /* Optional concurrency for small batches: with n_aux > 0 auxiliary streams (caller-created, and
-     * n_events >= 2·n_aux + 4 caller-created hipEvent_t, timing disabled) the launches that do not
-     * depend on each other — the object encoder beside the relation encoder, and after the backward
-     * step loop the object-encoder backward and the weight gradients — are forked onto them and
-     * joined back into `stream` before the call returns (stream-ordered, hipGraph-capturable). At
-     * small batches each launch occupies a few CUs and the kernels' latencies add up; overlapping
-     * them shortens the step. Results are identical (every launch writes its own outputs). */
-    int32_t n_aux;
-    int32_t n_events;
-    void** aux_streams;
-    void** events;
 } spwgnn_run;
 
 /* Matrix-product arithmetic. F32 and X6 give fp32-class results:

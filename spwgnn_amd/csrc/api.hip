@@ -275,64 +275,6 @@ struct Prof {
     }
 };
 
-// Fork/join of independent launches onto the caller's auxiliary streams (spwgnn_run.n_aux; none:
-// every stream() is the main stream and fork/join are no-ops). Events are taken from the caller's
-// pool in order; a recorded event is only waited on after its record (host order), so reuse across
-// calls is safe.
-struct Aux {
-    hipStream_t main;
-    int n = 0, n_ev = 0, next = 0;
-    hipStream_t* aux = nullptr;
-    hipEvent_t* ev = nullptr;
-    bool used[8] = {};
-    Aux(const spwgnn_run* r, hipStream_t st) : main(st) {
-        if (r->n_aux > 0 && r->aux_streams && r->events && r->n_events >= 2 * r->n_aux + 4) {
-            n = r->n_aux < 8 ? r->n_aux : 8;
-            n_ev = r->n_events;
-            aux = reinterpret_cast<hipStream_t*>(r->aux_streams);
-            ev = reinterpret_cast<hipEvent_t*>(r->events);
-        }
-    }
-    hipEvent_t take() { return ev[next++ % n_ev]; }
-    // the stream for independent launch group j (main when there are no auxiliary streams)
-    hipStream_t stream(int j) const { return n ? aux[j % n] : main; }
-    // every auxiliary stream waits for what `from` has issued so far
-    hipError_t fork(hipStream_t from) {
-        if (!n) return hipSuccess;
-        hipEvent_t e = take();
-        hipError_t r = hipEventRecord(e, from);
-        for (int j = 0; j < n && r == hipSuccess; ++j) {
-            r = hipStreamWaitEvent(aux[j], e, 0);
-            used[j] = true;
-        }
-        return r;
-    }
-    // auxiliary streams first.. wait for what `from` has issued so far (appended after their queues)
-    hipError_t fork_from(hipStream_t from, int first) {
-        if (n <= first) return hipSuccess;
-        hipEvent_t e = take();
-        hipError_t r = hipEventRecord(e, from);
-        for (int j = first; j < n && r == hipSuccess; ++j) {
-            r = hipStreamWaitEvent(aux[j], e, 0);
-            used[j] = true;
-        }
-        return r;
-    }
-    // the main stream waits for everything the auxiliary streams have issued
-    hipError_t join() {
-        if (!n) return hipSuccess;
-        for (int j = 0; j < n; ++j) {
-            if (!used[j]) continue;
-            hipEvent_t e = take();
-            hipError_t r = hipEventRecord(e, aux[j]);
-            if (r == hipSuccess) r = hipStreamWaitEvent(main, e, 0);
-            if (r != hipSuccess) return r;
-            used[j] = false;
-        }
-        return hipSuccess;
-    }
-};
-
 #define SPW_CHECK(x)                                  \
     do {                                              \
         hipError_t e_ = (x);                          \
@@ -418,13 +360,10 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.scale = scale;
     en.seed = r->seed;
     en.seed_dev = r->seed_dev;
-    Aux ax(r, st);
-    SPW_CHECK(ax.fork(st));   // the object encoder beside the relation encoder (auxiliary streams only)
     {
-        const hipStream_t sn = ax.stream(0);
-        Prof pn{r, sn};
+        Prof pn{r, st};
         SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
-        SPW_CHECK(launch_enc_node(en, r->math, sn));
+        SPW_CHECK(launch_enc_node(en, r->math, st));
         SPW_CHECK(pn.after(SPWGNN_K_ENC_NODE));
     }
 
@@ -470,7 +409,6 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         SPW_CHECK(launch_enc_edge(ee, kmath(r, kX6EncEdge), st));
         SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
     }
-    SPW_CHECK(ax.join());
 
     const int S = r->mp_steps;
     Prof prof{r, st};
@@ -764,135 +702,6 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         }
         SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
     }
-    // ---- after the step loop: independent work forked onto the auxiliary streams (spwgnn_run.n_aux;
-    // without them every launch below runs on `st` in this order) ----
-    Aux ax(r, st);
-    SPW_CHECK(ax.fork(st));
-    // ---- weight gradients ----
-    const int64_t RE = w.RE, RN = w.RN;
-    auto edge_row = [&](WgSpec& g, int64_t xoff, int64_t yoff, int tk, int tb) {
-        g.x = c.f(xoff); g.x_ld = kLdE; g.x_width = kFE; g.x_ones = kFE; g.x_count = RE; g.x_stride = 0;
-        g.y = c.f(yoff); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE; g.y_stride = 0;
-        g.rows = RE; g.kx_pad = 160; g.ny_pad = 160;
-        g.tk = tk; g.tb = tb; g.k_rows = kFE; g.k_row0 = 0; g.bias_row = kFE;
-    };
-    int32_t e;
-    ReduceBatch rb{};
-    // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
-    auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
-    const int b16xy = b16 ? (kB16X | kB16Y) : 0;
-    auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
-                       int yw, int kxp, int nyp) {
-        g.x = c.f(xoff); g.x_ld = xld; g.x_width = xw; g.x_ones = xones; g.x_count = nN; g.x_stride = xstride;
-        g.y = c.f(yoff); g.y_ld = yld; g.y_width = yw; g.y_count = nN; g.y_stride = RN;
-        g.rows = nN * S; g.kx_pad = kxp; g.ny_pad = nyp;
-        g.xmode = XM_CM; g.ymode = YM_CM;   // chunk-major node rows
-    };
-    hipStream_t gst = st;
-    const int nlo = ax.n > 1 ? ax.n - 1 : 1;   // auxiliary streams 1.. (or 0 alone) for the loop-only gradients
-    // gradients that read only the step loop's arrays (W2, W1b, W1c, W3, omp.0 a and P parts, omp.1)
-    gst = ax.stream(ax.n > 1 ? 1 + 0 % nlo : 0);
-    {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
-        // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
-        WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
-        g.xmode = XM_H1; g.ymode = YM_DH2;
-        g.x_count = g.y_count = g.rows = RE * S;
-        g.recompute = true;
-        g.b16 = b16 ? kB16A : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(ax.n > 1 ? 1 + 1 % nlo : 0);
-    {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
-        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(ax.n > 1 ? 1 + 2 % nlo : 0);
-    {   // rmp.0 rows 250..349 (W1c)
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
-        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(ax.n > 1 ? 1 + 3 % nlo : 0);
-    {   // rmp.2 (W3, b3): X = [H2s | deg]
-        WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
-        g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(ax.n > 1 ? 1 + 4 % nlo : 0);
-    {   // omp.0 rows 100..199 (effect part)
-        WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(ax.n > 1 ? 1 + 5 % nlo : 0);
-    {   // omp.0 rows 200..299 (P part)
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(ax.n > 1 ? 1 + 6 % nlo : 0);
-    {   // omp.1 (Wo2, bo2), x' column order → Keras order
-        WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
-        g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    // the object-encoder backward and the gradients that read its outputs (omp.0 c_o part, om.0, om.1)
-    EncNodeBwdArgs enb{};
-    enb.n_nodes = b->n_nodes;
-    enb.dco = c.f(w.dco);
-    enb.co = c.f(w.co);
-    enb.zo1 = z1_rebuilt(r) ? nullptr : c.f(w.zo1);
-    enb.pos = b->pos;
-    enb.w_om0 = c.pk(PK_OM0);
-    enb.b_om0 = c.pk(PB_OM0);
-    enb.om1t = c.pk(PK_OM1T);
-    enb.wo1ct = kmath(r, kX6NodeBwd) != MATH_F32 ? c.pk(PK_WO1CT) : nullptr;
-    enb.do1 = c.f(w.do1_at(0));
-    enb.do1_step = w.do1_at(1) - w.do1_at(0);
-    enb.S = S;
-    enb.dzo2 = c.f(w.dzo2);
-    enb.dzo1 = c.f(w.dzo1);
-    enb.scale = scale;
-    if (kmath(r, kX6NodeBwd) != MATH_F32) {
-        enb.x_wo1ct = c.x6(X6_WO1CT);
-        enb.x_om1t = c.x6(X6_OM1T);
-    }
-    SPW_CHECK(prof.before(SPWGNN_K_ENC_NODE_BWD));
-    SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), ax.stream(0)));
-    SPW_CHECK(prof.after(SPWGNN_K_ENC_NODE_BWD));
-
-    gst = ax.stream(0);
-    {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
-        WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
-        if (kmath(r, kX6NodeBwd) != MATH_F32) {   // c_oᵀ·Σ_s do1_s: Σ do1 stored by k_enc_node_bwd
-            g.y = c.f(w.dco);
-            g.rows = nN;
-            g.y_stride = 0;
-        }
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(0);
-    {   // om.0: X = [y, w | 1]
-        WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
-        g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
-        g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    gst = ax.stream(0);
-    {   // om.1
-        WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
-        g.rows = nN; g.y_stride = 0;
-        if (z1_rebuilt(r)) {
-            g.xp = reinterpret_cast<const float4*>(b->pos);
-            g.w0 = c.pk(PK_OM0);
-            g.b0 = c.pk(PB_OM0);
-        }
-        g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
-    }
-    // main stream: dA, then the relation-encoder backward
     if (rebuild) {
         DaArgs da{};
         da.n_eblocks = b->n_eblocks;
@@ -935,17 +744,49 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     SPW_CHECK(launch_enc_edge_bwd(eeb, kmath(r, kX6EncEdgeBwd), st));
     SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
 
-    // the relation-encoder gradients (rm.0-3, W1a) after it: the main stream and auxiliary streams 1..
-    SPW_CHECK(ax.fork_from(st, 1));
-    gst = (ax.n > 1 && 0 % ax.n != 0) ? ax.stream(0 % ax.n) : st;
+    EncNodeBwdArgs enb{};
+    enb.n_nodes = b->n_nodes;
+    enb.dco = c.f(w.dco);
+    enb.co = c.f(w.co);
+    enb.zo1 = z1_rebuilt(r) ? nullptr : c.f(w.zo1);
+    enb.pos = b->pos;
+    enb.w_om0 = c.pk(PK_OM0);
+    enb.b_om0 = c.pk(PB_OM0);
+    enb.om1t = c.pk(PK_OM1T);
+    enb.wo1ct = kmath(r, kX6NodeBwd) != MATH_F32 ? c.pk(PK_WO1CT) : nullptr;
+    enb.do1 = c.f(w.do1_at(0));
+    enb.do1_step = w.do1_at(1) - w.do1_at(0);
+    enb.S = S;
+    enb.dzo2 = c.f(w.dzo2);
+    enb.dzo1 = c.f(w.dzo1);
+    enb.scale = scale;
+    if (kmath(r, kX6NodeBwd) != MATH_F32) {
+        enb.x_wo1ct = c.x6(X6_WO1CT);
+        enb.x_om1t = c.x6(X6_OM1T);
+    }
+    SPW_CHECK(prof.before(SPWGNN_K_ENC_NODE_BWD));
+    SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), st));
+    SPW_CHECK(prof.after(SPWGNN_K_ENC_NODE_BWD));
+
+    // ---- weight gradients ----
+    const int64_t RE = w.RE, RN = w.RN;
+    auto edge_row = [&](WgSpec& g, int64_t xoff, int64_t yoff, int tk, int tb) {
+        g.x = c.f(xoff); g.x_ld = kLdE; g.x_width = kFE; g.x_ones = kFE; g.x_count = RE; g.x_stride = 0;
+        g.y = c.f(yoff); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE; g.y_stride = 0;
+        g.rows = RE; g.kx_pad = 160; g.ny_pad = 160;
+        g.tk = tk; g.tb = tb; g.k_rows = kFE; g.k_row0 = 0; g.bias_row = kFE;
+    };
+    int32_t e;
+    ReduceBatch rb{};
     {   // rm.0: X = [d | 1]
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
         g.b16 = b16 ? kB16Y : 0;   // Y = dz1
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
-    gst = (ax.n > 1 && 1 % ax.n != 0) ? ax.stream(1 % ax.n) : st;
+    // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
+    auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
     {
         WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g);
         if (z1_rebuilt(r)) {
@@ -954,15 +795,85 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.b0 = c.pk(PB_RM0);
         }
         g.b16 = b16 ? kB16Y : 0;   // X rebuilt from d; Y = dz2
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
     }
-    gst = (ax.n > 1 && 2 % ax.n != 0) ? ax.stream(2 % ax.n) : st;
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e; }
-    gst = (ax.n > 1 && 3 % ax.n != 0) ? ax.stream(3 % ax.n) : st;
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e; }
-    gst = (ax.n > 1 && 4 % ax.n != 0) ? ax.stream(4 % ax.n) : st;
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), gst, rb, &prof))) return e; }
-    SPW_CHECK(ax.join());
+    const int b16xy = b16 ? (kB16X | kB16Y) : 0;
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e; }
+    {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
+        // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
+        WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
+        g.xmode = XM_H1; g.ymode = YM_DH2;
+        g.x_count = g.y_count = g.rows = RE * S;
+        g.recompute = true;
+        g.b16 = b16 ? kB16A : 0;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
+                       int yw, int kxp, int nyp) {
+        g.x = c.f(xoff); g.x_ld = xld; g.x_width = xw; g.x_ones = xones; g.x_count = nN; g.x_stride = xstride;
+        g.y = c.f(yoff); g.y_ld = yld; g.y_width = yw; g.y_count = nN; g.y_stride = RN;
+        g.rows = nN * S; g.kx_pad = kxp; g.ny_pad = nyp;
+        g.xmode = XM_CM; g.ymode = YM_CM;   // chunk-major node rows
+    };
+    {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
+        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // rmp.0 rows 250..349 (W1c)
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
+        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // rmp.2 (W3, b3): X = [H2s | deg]
+        WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
+        g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
+        WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
+        if (kmath(r, kX6NodeBwd) != MATH_F32) {   // c_oᵀ·Σ_s do1_s: Σ do1 stored by k_enc_node_bwd
+            g.y = c.f(w.dco);
+            g.rows = nN;
+            g.y_stride = 0;
+        }
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // omp.0 rows 100..199 (effect part)
+        WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // omp.0 rows 200..299 (P part)
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // omp.1 (Wo2, bo2), x' column order → Keras order
+        WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
+        g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // om.0: X = [y, w | 1]
+        WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
+        g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
+        g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
+    {   // om.1
+        WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
+        g.rows = nN; g.y_stride = 0;
+        if (z1_rebuilt(r)) {
+            g.xp = reinterpret_cast<const float4*>(b->pos);
+            g.w0 = c.pk(PK_OM0);
+            g.b0 = c.pk(PB_OM0);
+        }
+        g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof))) return e;
+    }
     SPW_CHECK(launch_wgrad_reduce_all(rb, st));
     return SPWGNN_OK;
 }

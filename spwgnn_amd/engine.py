@@ -31,35 +31,6 @@ def _require_gpu(t: torch.Tensor, what: str):
 MATH_MODES = {"f32": _lib.MATH_F32, "x6": _lib.MATH_X6, "bf16": _lib.MATH_BF16}
 
 
-class AuxStreams:
-    """Caller-owned auxiliary HIP streams and events for spwgnn_run.n_aux: at small batches the
-    library forks its independent launches (object encoder, object-encoder backward, the weight
-    gradients) onto them and joins them back into the call's stream (include/spwgnn.h)."""
-
-    def __init__(self, device, n: int = 3):
-        self.device = torch.device(device)
-        self.streams = [torch.cuda.Stream(self.device) for _ in range(n)]
-        self._hip = C.CDLL("libamdhip64.so")   # the HIP runtime torch (and the library) run on
-        self.events = []
-        for _ in range(2 * n + 8):
-            e = C.c_void_p()
-            if self._hip.hipEventCreateWithFlags(C.byref(e), 0x2) != 0:   # hipEventDisableTiming
-                raise _lib.SpwgnnError("hipEventCreateWithFlags failed")
-            self.events.append(e.value)
-        self._s = (C.c_void_p * n)(*[s.cuda_stream for s in self.streams])
-        self._e = (C.c_void_p * len(self.events))(*self.events)
-
-    def fill(self, r: "_lib.RunC"):
-        r.n_aux = len(self.streams)
-        r.n_events = len(self.events)
-        r.aux_streams = C.cast(self._s, C.c_void_p)
-        r.events = C.cast(self._e, C.c_void_p)
-
-    def __del__(self):
-        for e in getattr(self, "events", []):
-            self._hip.hipEventDestroy(C.c_void_p(e))
-
-
 @dataclass
 class RunConfig:
     mp_steps: int = REF_MP_STEPS
@@ -70,7 +41,6 @@ class RunConfig:
     prof_kernel: int = 0                 # SPWGNN_K_* to bracket with HIP events (bench only)
     prof_events: Optional[list] = None   # raw hipEvent_t handles, 2 per launch
     seed_dev: Optional[torch.Tensor] = None   # (1,) int64 device word holding the dropout key (replayable steps)
-    aux: Optional[AuxStreams] = None          # auxiliary streams for independent launches (small batches)
 
     def cstruct(self) -> _lib.RunC:
         r = _lib.RunC()
@@ -91,8 +61,6 @@ class RunConfig:
             if self.seed_dev.device.type != "cuda" or self.seed_dev.dtype != torch.int64:
                 raise ValueError("seed_dev must be a (1,) int64 device tensor")
             r.seed_dev = self.seed_dev.data_ptr()
-        if self.aux is not None:
-            self.aux.fill(r)
         return r
 
 

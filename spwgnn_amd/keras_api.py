@@ -143,10 +143,10 @@ class KerasModel:
         read from the device, and the epoch sums accumulated on the device."""
         net, ctr = self.net, self._ctr
 
-        def body(batch, target, ws, bce, z, dz, aux):
+        def body(batch, target, ws, bce, z, dz):
             w3 = self._w3[batch.n_towers]        # created before the first (eager) run of a geometry
             E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_COUNTER)
-            run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key, aux=aux)
+            run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key)
             E.forward(net.flat.data, batch, run, ws, logits=z)
             out3, _ = E.bce(z, target, bce, dlogits=dz)
             self._tot.add_(out3.double() * w3)

@@ -117,17 +117,14 @@ class StaticBatch:
 class ReplayStep:
     """One batch geometry's training step (forward, BCE, backward, Adam) as a replayed hipGraph.
 
-    `body(batch, target, ws, bce, z, dz, aux)` issues the step's launches on the current stream (and
-    the auxiliary streams `aux`, E.AuxStreams or None, which the library forks its independent
-    launches onto and joins back); it is run eagerly on the first call (a real step) and captured
-    right after, then replayed."""
+    `body(batch, target, ws, bce, z, dz)` issues the step's launches on the current stream; it is
+    run eagerly on the first call (a real step) and captured right after, then replayed."""
 
-    def __init__(self, plan: HostPlan, device, body: Callable, graph: bool = True, aux: bool = True):
+    def __init__(self, plan: HostPlan, device, body: Callable, graph: bool = True):
         self.static = StaticBatch(plan, device)
         self.device = self.static.device
         self.ws = E.Workspace(self.device)
         self.bce = E.BceScratch(self.device)
-        self.aux = E.AuxStreams(self.device) if aux else None
         n = plan.n_nodes
         self.z = torch.empty(n, dtype=torch.float32, device=self.device)
         self.dz = torch.empty(n, dtype=torch.float32, device=self.device)
@@ -137,7 +134,7 @@ class ReplayStep:
         self.replays = 0
 
     def _issue(self):
-        self.body(self.static.batch, self.static.target, self.ws, self.bce, self.z, self.dz, self.aux)
+        self.body(self.static.batch, self.static.target, self.ws, self.bce, self.z, self.dz)
 
     def __call__(self, plan: HostPlan, target: np.ndarray):
         self.static.load(plan, target)
@@ -158,10 +155,8 @@ class ReplayStep:
 class ReplayCache:
     """ReplaySteps keyed by batch geometry (full batches and the epoch's last partial batch)."""
 
-    def __init__(self, device, make_body: Callable[[], Callable], graph: bool = True, max_entries: int = 8,
-                 aux: bool = True):
+    def __init__(self, device, make_body: Callable[[], Callable], graph: bool = True, max_entries: int = 8):
         self.device, self.make_body, self.graph, self.max_entries = device, make_body, graph, max_entries
-        self.aux = aux
         self.steps: Dict[tuple, ReplayStep] = {}
 
     def __call__(self, plan: HostPlan, target: np.ndarray):
@@ -170,7 +165,7 @@ class ReplayCache:
         if st is None:
             if len(self.steps) >= self.max_entries:       # bounded: drop the oldest geometry
                 self.steps.pop(next(iter(self.steps)))
-            st = self.steps[key] = ReplayStep(plan, self.device, self.make_body(), self.graph, self.aux)
+            st = self.steps[key] = ReplayStep(plan, self.device, self.make_body(), self.graph)
         st(plan, target)
         return st
 

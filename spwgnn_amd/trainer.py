@@ -117,10 +117,9 @@ class Trainer:
         w = n_nodes / (n_global or n_nodes)
         grads = torch.empty_like(self.params)
 
-        def body(batch, target, ws, bce, z, dz, aux):
+        def body(batch, target, ws, bce, z, dz):
             E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_SPLITMIX, self.seed, self.rank)
-            run = E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, math=self.math, seed_dev=ctr.key,
-                              aux=aux)
+            run = E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, math=self.math, seed_dev=ctr.key)
             E.forward(self.params, batch, run, ws, logits=z)
             out3, _ = E.bce(z, target, bce, dlogits=dz)
             E.backward(self.params, batch, run, ws, dz, grads=grads)

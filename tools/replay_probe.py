@@ -21,10 +21,8 @@ plans, tg, n_global = bench.make_workload(cfg, 0, dev, 1, plans=True)
 plan, tgt = plans[0], tg[0]
 tr = Trainer(P.to_flat(P.glorot_uniform(0), device=dev), mp_steps=cfg["S"], dropout=0.1, seed=7, math=cfg["math"])
 rs = ReplayStep(plan, dev, tr.replay_body(plan.n_nodes, n_global))
-rs0 = ReplayStep(plan, dev, tr.replay_body(plan.n_nodes, n_global), aux=False)   # one stream only
 for _ in range(20):
     rs(plan, tgt)
-    rs0(plan, tgt)
 torch.cuda.synchronize()
 
 
@@ -41,7 +39,6 @@ src, dst = plan.src, plan.dst
 out = {
     "full_call_ms": timed(lambda: rs(plan, tgt)),
     "replay_only_ms": timed(lambda: rs.graph.replay()),
-    "replay_one_stream_ms": timed(lambda: rs0.graph.replay()),
     "load_only_ms": timed(lambda: rs.static.load(plan, tgt)),
     "plan_build_ms": timed(lambda: HostPlan.build(plan.arrays[0][:, :3], plan.tower_nodes, src, dst, plan.tower_edges,
                                                   edge_cap=30)),
