@@ -45,6 +45,9 @@ typedef struct spwgnn_param_info {
 } spwgnn_param_info;
 
 int32_t spwgnn_version(void);
+/* sizeof the ABI structs as this library was compiled (bindings check their own layouts against it):
+ * which = 0 spwgnn_batch, 1 spwgnn_run, 2 spwgnn_plan_sizes, 3 spwgnn_param_info; -1 otherwise. */
+int32_t spwgnn_struct_size(int32_t which);
 const char* spwgnn_strerror(int32_t status);
 int32_t spwgnn_param_tensor_count(void);
 int64_t spwgnn_param_count(void);                 /* padded flat length (floats)       */

@@ -53,6 +53,7 @@ def _declare(lib: C.CDLL) -> None:
     i32, i64, vp, f32 = C.c_int32, C.c_int64, C.c_void_p, C.c_float
     sig = {
         "spwgnn_version": (i32, []),
+        "spwgnn_struct_size": (i32, [i32]),
         "spwgnn_strerror": (C.c_char_p, [i32]),
         "spwgnn_param_tensor_count": (i32, []),
         "spwgnn_param_count": (i64, []),
@@ -94,6 +95,10 @@ def lib() -> C.CDLL:
         if lib_.spwgnn_version() != ABI_VERSION:
             raise SpwgnnError(f"{path} implements ABI {lib_.spwgnn_version()}, this binding expects {ABI_VERSION}: "
                               "rebuild with `python -m spwgnn_amd.build`")
+        for which, st in enumerate((BatchC, RunC, PlanSizes, ParamInfo)):
+            if lib_.spwgnn_struct_size(which) != C.sizeof(st):
+                raise SpwgnnError(f"{path} was built with a different {st.__name__} layout "
+                                  f"({lib_.spwgnn_struct_size(which)} vs {C.sizeof(st)} bytes): rebuild it")
         _lib = lib_
     return _lib
 

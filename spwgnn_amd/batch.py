@@ -23,11 +23,19 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
-def default_nw_max(max_nodes: int) -> int:
+SMALL_BATCH_TOWERS = 2048   # below this a batch cannot fill the chip's 2,048 edge waves anyway
+
+
+def default_nw_max(max_nodes: int, n_towers: int = 1 << 30) -> int:
     """Nodes per wave-tile: at least one whole tower. Up to 16 nodes the backward segment sums run
     as one one-hot matrix product (receiver rows 0-15, sender rows 16-31), so small towers are
-    packed up to 16 nodes per wave; larger towers take one wave-tile each (≤ 32 nodes)."""
-    return 16 if max_nodes <= 16 else int(min(_NW_LIMIT, max_nodes))
+    packed up to 16 nodes per wave; larger towers take one wave-tile each (≤ 32 nodes). A small
+    batch (fewer towers than the edge kernels have waves) takes one tower per wave-tile instead:
+    each wave then walks one tower's blocks, not two or three, which is the step's latency at
+    batch 32 (the reference's fit, main.py:92-98)."""
+    if max_nodes > 16:
+        return int(min(_NW_LIMIT, max_nodes))
+    return max(int(max_nodes), 1) if n_towers < SMALL_BATCH_TOWERS else 16
 
 
 _NW_LIMIT = 32
@@ -100,7 +108,7 @@ class HostPlan:
         if int(tower_edges.sum()) != len(src) or len(src) != len(dst):
             raise ValueError("edge counts do not match the edge list")
         if nw_max is None:
-            nw_max = default_nw_max(int(tower_nodes.max()) if T else 1)
+            nw_max = default_nw_max(int(tower_nodes.max()) if T else 1, T)
         if T and int(tower_nodes.max()) > _NW_LIMIT:
             raise ValueError(f"towers of more than {_NW_LIMIT} nodes are not supported by this build")
         cap = None

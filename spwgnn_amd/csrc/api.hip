@@ -501,9 +501,11 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     if (g.rows <= 0) return SPWGNN_OK;
     if (rb.n >= kWgSlots) return SPWGNN_E_ARG;
     float* const slab = c.f(w.slab) + (int64_t)rb.n * w.slot_floats;
-    // the row-chunked kernels: up to 1024 chunks of ≥ 512 rows, as many as the slot holds
+    // the row-chunked kernels: chunks of ≥ 512 rows, but at least one per CU (256) while a chunk
+    // keeps ≥ one 32-row block — small batches spread over the chip instead of walking a few
+    // chunks serially; at most 1024 chunks and what the slot holds
     const int64_t slot_chunks = w.slot_floats / ((int64_t)g.kx_pad * g.ny_pad);
-    int64_t chunks = (g.rows + 32 * 16 - 1) / (32 * 16);
+    int64_t chunks = std::max<int64_t>((g.rows + 32 * 16 - 1) / (32 * 16), std::min<int64_t>((g.rows + 31) / 32, 256));
     chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, std::min<int64_t>(1024, slot_chunks)));
     int64_t rpc = up((g.rows + chunks - 1) / chunks, 32);
     chunks = (g.rows + rpc - 1) / rpc;

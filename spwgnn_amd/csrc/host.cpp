@@ -56,6 +56,16 @@ extern "C" {
 
 int32_t spwgnn_version(void) { return SPWGNN_ABI_VERSION; }
 
+int32_t spwgnn_struct_size(int32_t which) {
+    switch (which) {
+        case 0: return (int32_t)sizeof(spwgnn_batch);
+        case 1: return (int32_t)sizeof(spwgnn_run);
+        case 2: return (int32_t)sizeof(spwgnn_plan_sizes);
+        case 3: return (int32_t)sizeof(spwgnn_param_info);
+        default: return -1;
+    }
+}
+
 const char* spwgnn_strerror(int32_t st) {
     switch (st) {
         case SPWGNN_OK: return "ok";

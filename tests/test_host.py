@@ -332,8 +332,8 @@ def test_capacity_plan_shares_geometry_and_edge_layout():
         src, dst = (e[:, 0] * 6 + e[:, 2]).astype(np.int32), (e[:, 0] * 6 + e[:, 3]).astype(np.int32)
         te = np.bincount(e[:, 0], minlength=32).astype(np.int32)
         nodes = np.full(32, 6, np.int32)
-        plain = HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te)
-        cap = HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te, edge_cap=30)
+        plain = HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te, nw_max=16)
+        cap = HostPlan.build(obj.reshape(-1, 3), nodes, src, dst, te, edge_cap=30, nw_max=16)
         geo.add(cap.geometry)
         assert cap.n_wtiles == plain.n_wtiles == 16 and cap.n_eblocks == 32 >= plain.n_eblocks
         wp, wc = plain.arrays[3], cap.arrays[3]
@@ -363,3 +363,17 @@ def test_adam_lr_table_is_keras_adam_lr_t():
     assert out[0] == 0.0
     assert np.array_equal(out[1:], want)
     assert _lib.lib().spwgnn_adam_lr_table(5e-4, 0.9, 0.999, 1, out.ctypes.data) != 0
+
+
+def test_small_batches_take_one_tower_per_wave_tile():
+    """default_nw_max: below SMALL_BATCH_TOWERS towers of ≤ 16 boxes one tower per wave-tile (more
+    waves for a batch that cannot fill the chip), from there on packed up to 16 nodes; > 16 boxes
+    always one tower per tile."""
+    from spwgnn_amd.batch import SMALL_BATCH_TOWERS, HostPlan, default_nw_max
+    assert default_nw_max(6, 32) == 6 and default_nw_max(6, SMALL_BATCH_TOWERS) == 16
+    assert default_nw_max(20, 32) == 20 and default_nw_max(20, 10 ** 6) == 20
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(32, 6, seed=1, fully_connected=True)
+    e = np.array(O.dense_to_edges(Rs, Rr), np.int64).reshape(-1, 4)
+    te = np.bincount(e[:, 0], minlength=32).astype(np.int32)
+    p = HostPlan.build(obj.reshape(-1, 3), np.full(32, 6, np.int32), e[:, 0] * 6 + e[:, 2], e[:, 0] * 6 + e[:, 3], te)
+    assert p.n_wtiles == 32 and p.nw_max == 6 and p.n_eblocks == 32
