@@ -377,3 +377,33 @@ def test_small_batches_take_one_tower_per_wave_tile():
     te = np.bincount(e[:, 0], minlength=32).astype(np.int32)
     p = HostPlan.build(obj.reshape(-1, 3), np.full(32, 6, np.int32), e[:, 0] * 6 + e[:, 2], e[:, 0] * 6 + e[:, 3], te)
     assert p.n_wtiles == 32 and p.nw_max == 6 and p.n_eblocks == 32
+
+
+def test_input_validation_errors():
+    """The boundary's error behaviour: a relation column that is not one-hot, a
+    receiver without a sender, wrongly shaped relation matrices and towers beyond the 32-box
+    limit raise instead of silently summing rows (Keras' batch_dot would)."""
+    from spwgnn_amd import TowerBatch
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(2, 4, seed=3, fully_connected=True)
+    bad = Rs.copy()
+    bad[0, 1, 0] = 1.0                       # column 0 of tower 0 now has two senders
+    with pytest.raises(_lib.SpwgnnError, match="one-hot"):
+        TowerBatch.from_dense(obj, bad, Rr, device="cpu")
+    half = Rs.copy()
+    half[0, :, 3] = 0.0                      # column 3: a receiver without a sender
+    with pytest.raises(_lib.SpwgnnError, match="one-hot"):
+        TowerBatch.from_dense(obj, half, Rr, device="cpu")
+    scaled = Rs * 2.0                        # not {0, 1}
+    with pytest.raises(_lib.SpwgnnError):
+        TowerBatch.from_dense(obj, scaled, Rr, device="cpu")
+    with pytest.raises(ValueError):
+        TowerBatch.from_dense(obj, Rs[:, :, :5], Rr[:, :, :5], device="cpu")
+    big = (D.synthetic_towers(1, 33, seed=0) / 170).astype(np.float32)
+    with pytest.raises(ValueError, match="33|32"):
+        TowerBatch.fully_connected(big, device="cpu")
+    # an all-zero column (inactive relation) is valid and dropped
+    off = Rs.copy(), Rr.copy()
+    off[0][0, :, 2] = 0.0
+    off[1][0, :, 2] = 0.0
+    b = TowerBatch.from_dense(obj, off[0], off[1], device="cpu")
+    assert b.n_edges == 2 * 12 - 1
