@@ -386,8 +386,8 @@ def timed_steps(trainer, step_in, kid, n_micro, steps, slots):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 10; 500 for replayed configs)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; 20 for replayed configs)")
     ap.add_argument("--config", type=int, default=0, choices=sorted(CONFIGS),
                     help="BASELINE.json config (1-5); 0 = the headline metric's configuration")
     ap.add_argument("--towers", type=int, default=None, help="towers per GPU (overrides the config)")
@@ -409,6 +409,12 @@ def main():
     for k, a in (("towers", args.towers), ("nodes", args.nodes), ("S", args.mp_steps), ("math", args.math)):
         if a is not None:
             cfg[k] = a
+    # a replayed step is ~0.4 ms: 10 of them are shorter than one host hiccup on a shared box, so
+    # replayed configs time 500 (0.2 s) unless told otherwise
+    if args.steps is None:
+        args.steps = 500 if cfg.get("replay") else 10
+    if args.warmup is None:
+        args.warmup = 20 if cfg.get("replay") else 3
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

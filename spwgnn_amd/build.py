@@ -13,7 +13,7 @@ CSRC = HERE / "csrc"
 INCLUDE = HERE.parent / "include"
 LIB = HERE / "libspwgnn_hip.so"
 OBJDIR = HERE / "csrc" / "build"
-SOURCES = ["host.cpp", "api.hip", "kernels_fwd.hip", "kernels_bwd.hip", "kernels_misc.hip"]
+SOURCES = ["host.cpp", "api.hip", "kernels_fwd.hip", "kernels_bwd.hip", "kernels_misc.hip", "kernels_team.hip"]
 HEADERS = ["spwgnn_layout.h", "device_common.h", "gemm_blocks.h", "kernels.h"]
 ARCH = os.environ.get("SPWGNN_ARCH", "gfx950")
 

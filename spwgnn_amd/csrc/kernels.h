@@ -253,6 +253,22 @@ struct ReduceArgs {
     int perm;              // 1: omp.1 column permutation (slab col f' → tensor col wo2_perm(f'))
 };
 
+// k_wgrad_ws shapes (KXP × NYP, Y row-major, rebuilt X, bf16-stored operands) as one batched launch
+enum WsVariant : int {
+    WSV_160_160 = 0, WSV_160_160_ROW, WSV_128_160, WSV_160_128, WSV_128_128, WSV_XD_EDGE, WSV_XD_NODE,
+    WSV_XD_EDGE_B16Y, WSV_160_160_ROW_B16, WSV_160_160_B16,   // bf16 math only
+    WSV_NONE = -1
+};
+struct WsJob {
+    WgWsArgs a;
+    int variant, wg0;      // WsVariant; first workgroup of the job in the batched grid
+};
+constexpr int kMaxWsJobs = 16;
+struct WsBatch {           // the k_wgrad_ws gradients of one backward (k_wgrad_ws_batch)
+    WsJob j[kMaxWsJobs];
+    int n, wgs;
+};
+
 constexpr int kMaxReduce = 16;
 struct ReduceBatch {       // the weight gradients of one backward, reduced in one launch (blockIdx.y)
     ReduceArgs r[kMaxReduce];
@@ -292,6 +308,9 @@ enum MathMode : int { MATH_F32 = 0, MATH_X6 = 1, MATH_BF16 = 2 };   // = SPWGNN_
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st);
 hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
                            hipStream_t st, int b16 = 0);
+// the variant k_wgrad_ws runs for these arguments (WSV_NONE: no such kernel)
+int wgrad_ws_variant(const WgWsArgs& a, int kx_pad, int ny_pad, int yrow, int mask, int math, int b16);
+hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st);
 hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st, int b16 = 0);
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st);
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
@@ -300,6 +319,16 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);
 hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers, int mode, float* out, hipStream_t st);
+
+// Team kernels (kernels_team.hip): one block per workgroup of waves that split each layer's output
+// tiles — the latency-bound small batches (the reference's batch 32) up to kTeamMaxBlocks blocks
+constexpr int kTeamMaxBlocks = 512;
+bool team_blocks(int n_blocks);   // 32-row blocks of the launch (edge or node blocks)
+hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st);
+hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st);
+hipError_t launch_node_bwd_team(const NodeBwdArgs& a, int math, hipStream_t st);
+hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipStream_t st);
+hipError_t launch_enc_edge_bwd_team(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
 // persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)

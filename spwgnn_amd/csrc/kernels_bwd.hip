@@ -639,6 +639,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
+    if ((math == MATH_X6 || math == MATH_BF16) && a.dco_sum && team_blocks((a.n_nodes + 31) / 32))
+        return launch_node_bwd_team(a, math, st);
     if (math == MATH_BF16) {
         const int w = (a.n_nodes + 31) / 32;
         hipLaunchKernelGGL((k_node_bwd_x6<1, 1, 4>), dim3((w + 3) / 4), dim3(256), 0, st, a);
@@ -1029,6 +1031,7 @@ hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st
     // one 32-edge block per wave at two waves per SIMD, weight images shared by the workgroup's 4
     // waves (x6: 2.44 → 2.33 ms against two blocks per wave at one wave per SIMD with per-wave rings)
     constexpr int NC = 1, NW = 4;
+    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks(a.n_eblocks)) return launch_enc_edge_bwd_team(a, math, st);
     const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
     if (math == MATH_BF16) {
         if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, true, NW>), g, dim3(256), 0, st, a);

@@ -1113,6 +1113,7 @@ hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st) {
 }
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
+    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks(waves)) return launch_enc_node_team(a, math, st);
     if (math == MATH_X6) {
         hipLaunchKernelGGL((k_enc_node_x6<3, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
@@ -1130,6 +1131,7 @@ hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st) {
 }
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
     const bool train = a.z1 || a.ed;   // z1 null with ed set: training, z1 rebuilt by the W1 gradient
+    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks(a.n_eblocks)) return launch_enc_edge_team(a, math, train, st);
     if (math == MATH_X6 || math == MATH_BF16) {
         // one 32-edge block per wave at two waves per SIMD, weight images shared by the workgroup's
         // 4 waves (x6: 2.48 → 2.11 ms against two blocks per wave at one wave per SIMD, per-wave rings)
@@ -1201,6 +1203,7 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st) {
+    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks((a.n_nodes + 31) / 32)) return launch_node_fwd_team(a, math, st);
     const int waves = (a.n_nodes + 31) / 32;
     if (math == MATH_X6) {
         // one 32-node column tile per wave at two waves per SIMD (measured: 0.58 vs 0.62 ms for

@@ -997,16 +997,17 @@ struct WsSet4 {
 // (XD 2), with the encoders' own first-layer arithmetic (dense2 + relu on the same pack):
 // bit-identical to the activations the encoders no longer store.
 // B16 (bf16 math, §3g): X (kB16X) and/or Y (kB16Y) stored as bf16 with the fp32 element layout.
-template <int KXP, int NYP, int YROW, bool MASK, int NP = 3, int XD = 0, int B16 = 0>
-__global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void k_wgrad_ws(WgWsArgs a) {
+// The body of one workgroup `bid` of a weight gradient; smem: two stage buffers of W::BUF bytes
+// (k_wgrad_ws: its own; k_wgrad_ws_batch: the largest variant's, shared by every job of the batch).
+template <int KXP, int NYP, int YROW, bool MASK, int NP, int XD, int B16>
+__device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* smem) {
     using W = WsStage<KXP, NYP, YROW, MASK>;
     using IX = X6Img<KXP>;
     using IY = X6Img<NYP>;
     constexpr int MX = KXP / 32, MY = NYP / 32;
-    __shared__ __attribute__((aligned(16))) char buf[2][W::BUF];
+    auto buf = [&](int p) { return smem + p * W::BUF; };   // (offsets, not a pointer array: keeps the LDS address space)
     const int tid = threadIdx.x;
-    const int64_t t0 = (int64_t)blockIdx.x * a.stages_per_wg;
+    const int64_t t0 = (int64_t)bid * a.stages_per_wg;
     const int64_t nst = a.nbs * a.S;
     const int T = t0 < nst ? (int)min<int64_t>(a.stages_per_wg, nst - t0) : 0;
     if (tid < 256) {
@@ -1025,7 +1026,7 @@ void k_wgrad_ws(WgWsArgs a) {
         for (int y = 0; y < MY; ++y) oy[y] = IY::roff(lane, MY * wy + y);
         __syncthreads();
         for (int t = 0; t < T; ++t) {
-            const char* Xs = buf[t & 1];
+            const char* Xs = buf(t & 1);
             const char* Ys = Xs + W::IMX;
             bf16x8 yb[MY][3], xa[2][3];
             IX::template get<NP>(Xs, ox[0], xa[0]);
@@ -1048,7 +1049,7 @@ void k_wgrad_ws(WgWsArgs a) {
             }
             __syncthreads();
         }
-        float* out = a.slab + (int64_t)blockIdx.x * KXP * NYP;
+        float* out = a.slab + (int64_t)bid * KXP * NYP;
 #pragma unroll
         for (int x = 0; x < MX; ++x)
 #pragma unroll
@@ -1154,13 +1155,13 @@ void k_wgrad_ws(WgWsArgs a) {
 #pragma unroll
         for (int k = 0; k < (KXP / 4 + 7) / 8; ++k) {
             const int c4 = c0 + 8 * k;
-            if (c4 >= W::GX && c4 < KXP / 4) IX::template put<NP>(buf[p], rr, c4, f4zero());
+            if (c4 >= W::GX && c4 < KXP / 4) IX::template put<NP>(buf(p), rr, c4, f4zero());
         }
         if (!YROW) {
 #pragma unroll
             for (int k = 0; k < (NYP / 4 + 7) / 8; ++k) {
                 const int c4 = c0 + 8 * k;
-                if (c4 >= W::GY && c4 < NYP / 4) IY::template put<NP>(buf[p] + W::IMX, rr, c4, f4zero());
+                if (c4 >= W::GY && c4 < NYP / 4) IY::template put<NP>(buf(p) + W::IMX, rr, c4, f4zero());
             }
         }
     }
@@ -1168,32 +1169,73 @@ void k_wgrad_ws(WgWsArgs a) {
     fetch(0, R0);
     fetch(1, R1);
     fetch(2, R2);
-    build(R0, buf[0]);
+    build(R0, buf(0));
     __syncthreads();
     // iteration t: stream stage t+3 into set t%3, build stage t+1 (set (t+1)%3) into buffer (t+1)&1
     int t = 0;
     for (; t + 3 <= T - 1; t += 3) {
         fetch(t + 3, R0);
-        build(R1, buf[(t + 1) & 1]);
+        build(R1, buf((t + 1) & 1));
         __syncthreads();
         fetch(t + 4, R1);
-        build(R2, buf[t & 1]);
+        build(R2, buf(t & 1));
         __syncthreads();
         fetch(t + 5, R2);
-        build(R0, buf[(t + 1) & 1]);
+        build(R0, buf((t + 1) & 1));
         __syncthreads();
     }
     if (t < T - 1) {
-        build(R1, buf[(t + 1) & 1]);
+        build(R1, buf((t + 1) & 1));
         __syncthreads();
         ++t;
     }
     if (t < T - 1) {
-        build(R2, buf[(t + 1) & 1]);
+        build(R2, buf((t + 1) & 1));
         __syncthreads();
         ++t;
     }
     __syncthreads();
+}
+
+template <int KXP, int NYP, int YROW, bool MASK, int NP = 3, int XD = 0, int B16 = 0>
+__global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_wgrad_ws(WgWsArgs a) {
+    __shared__ __attribute__((aligned(16))) char buf[2 * WsStage<KXP, NYP, YROW, MASK>::BUF];
+    wgrad_ws_body<KXP, NYP, YROW, MASK, NP, XD, B16>(a, blockIdx.x, buf);
+}
+
+// Every stored-operand weight gradient of a backward in ONE launch: workgroup b runs job k's
+// workgroup b − wg0[k] (job ranges in order; the job and its variant are workgroup-uniform). At the
+// reference's batch 32 each gradient is a few workgroups of one or two stages, so eleven launches
+// cost their ramp-up eleven times; batched they overlap.
+constexpr int kWsMaxBuf = WsStage<160, 160, 0, false>::BUF;
+template <int NP>
+__global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_wgrad_ws_batch(WsBatch b) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * kWsMaxBuf];
+    int k = 0;
+    while (k + 1 < b.n && (int)blockIdx.x >= b.j[k + 1].wg0) ++k;
+    const WsJob& job = b.j[k];
+    const int bid = (int)blockIdx.x - job.wg0;
+    switch (job.variant) {
+        case WSV_160_160: wgrad_ws_body<160, 160, 0, false, NP, 0, 0>(job.a, bid, smem); break;
+        case WSV_160_160_ROW: wgrad_ws_body<160, 160, 1, false, NP, 0, 0>(job.a, bid, smem); break;
+        case WSV_128_160: wgrad_ws_body<128, 160, 0, true, NP, 0, 0>(job.a, bid, smem); break;
+        case WSV_160_128: wgrad_ws_body<160, 128, 0, true, NP, 0, 0>(job.a, bid, smem); break;
+        case WSV_128_128: wgrad_ws_body<128, 128, 0, true, NP, 0, 0>(job.a, bid, smem); break;
+        case WSV_XD_EDGE: wgrad_ws_body<160, 160, 0, false, NP, 1, 0>(job.a, bid, smem); break;
+        case WSV_XD_NODE: wgrad_ws_body<128, 128, 0, true, NP, 2, 0>(job.a, bid, smem); break;
+        default:
+            if constexpr (NP == 1) {   // bf16 math's bf16-stored edge operands (§3g)
+                switch (job.variant) {
+                    case WSV_XD_EDGE_B16Y: wgrad_ws_body<160, 160, 0, false, 1, 1, kB16Y>(job.a, bid, smem); break;
+                    case WSV_160_160_ROW_B16: wgrad_ws_body<160, 160, 1, false, 1, 0, kB16X | kB16Y>(job.a, bid, smem); break;
+                    case WSV_160_160_B16: wgrad_ws_body<160, 160, 0, false, 1, 0, kB16X | kB16Y>(job.a, bid, smem); break;
+                    default: break;
+                }
+            }
+            break;
+    }
 }
 
 // dW = Σ_c slab[c] in chunk order (deterministic), scattered into the Keras tensors (kernel rows,
@@ -1418,51 +1460,62 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
 #endif
     return hipGetLastError();
 }
-hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
-                           hipStream_t st, int b16) {
-    const dim3 g(wgs), b(kWsThreads);
-    if (b16 && math != MATH_BF16) return hipErrorInvalidValue;
+int wgrad_ws_variant(const WgWsArgs& a, int kx_pad, int ny_pad, int yrow, int mask, int math, int b16) {
+    if (b16 && math != MATH_BF16) return WSV_NONE;
     if (a.xd) {   // the rm.1 gradient with X = [z1 | 1] rebuilt from (dx, dy)
-        if (kx_pad != 160 || ny_pad != 160 || yrow || mask) return hipErrorInvalidValue;
-        if (b16 == kB16Y)
-            hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1, kB16Y>), g, b, 0, st, a);
-        else if (b16)
-            return hipErrorInvalidValue;
-        else if (math == MATH_BF16)
-            hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1>), g, b, 0, st, a);
-        else
-            hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 3, 1>), g, b, 0, st, a);
-        return hipGetLastError();
+        if (kx_pad != 160 || ny_pad != 160 || yrow || mask) return WSV_NONE;
+        if (b16 == kB16Y) return WSV_XD_EDGE_B16Y;
+        return b16 ? WSV_NONE : WSV_XD_EDGE;
     }
     if (a.xp) {   // the om.1 gradient with X = [zo1 | 1] rebuilt from the node positions
-        if (kx_pad != 128 || ny_pad != 128 || yrow || !mask) return hipErrorInvalidValue;
-        if (math == MATH_BF16)
-            hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 1, 2>), g, b, 0, st, a);
-        else
-            hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 3, 2>), g, b, 0, st, a);
-        return hipGetLastError();
+        if (kx_pad != 128 || ny_pad != 128 || yrow || !mask || b16) return WSV_NONE;
+        return WSV_XD_NODE;
     }
     if (b16) {   // the encoder-side edge operands of bf16 math (rm.2, rm.3: X, Y; W1a: X = c_r, Y = dA rows)
-        if (kx_pad != 160 || ny_pad != 160 || mask || b16 != (kB16X | kB16Y)) return hipErrorInvalidValue;
-        if (yrow) hipLaunchKernelGGL((k_wgrad_ws<160, 160, 1, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a);
-        else hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a);
-        return hipGetLastError();
+        if (kx_pad != 160 || ny_pad != 160 || mask || b16 != (kB16X | kB16Y)) return WSV_NONE;
+        return yrow ? WSV_160_160_ROW_B16 : WSV_160_160_B16;
     }
-#define SPW_WS(KX, NY, YR, MK)                                                                   \
-    if (kx_pad == KX && ny_pad == NY && yrow == YR && (mask != 0) == MK) {                     \
-        if (math == MATH_BF16)                                                                 \
-            hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK, 1>), g, b, 0, st, a);               \
-        else                                                                                   \
-            hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK>), g, b, 0, st, a);                  \
-        return hipGetLastError();                                                              \
-    }
-    SPW_WS(160, 160, 0, false)
-    SPW_WS(160, 160, 1, false)
-    SPW_WS(128, 160, 0, true)
-    SPW_WS(160, 128, 0, true)
-    SPW_WS(128, 128, 0, true)
+    const bool mk = mask != 0;
+    if (kx_pad == 160 && ny_pad == 160 && !mk) return yrow ? WSV_160_160_ROW : WSV_160_160;
+    if (yrow) return WSV_NONE;
+    if (kx_pad == 128 && ny_pad == 160 && mk) return WSV_128_160;
+    if (kx_pad == 160 && ny_pad == 128 && mk) return WSV_160_128;
+    if (kx_pad == 128 && ny_pad == 128 && mk) return WSV_128_128;
+    return WSV_NONE;
+}
+// one gradient on its own launch (the per-shape kernels; SPWGNN_DIAG A/B of the batched launch)
+hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, int yrow, int mask, int math,
+                           hipStream_t st, int b16) {
+    const int v = wgrad_ws_variant(a, kx_pad, ny_pad, yrow, mask, math, b16);
+    const dim3 g(wgs), b(kWsThreads);
+    const bool bf = math == MATH_BF16;
+    switch (v) {
+#define SPW_WS(V, KX, NY, YR, MK, XD)                                                              \
+        case V:                                                                                     \
+            if (bf) hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK, 1, XD>), g, b, 0, st, a);        \
+            else hipLaunchKernelGGL((k_wgrad_ws<KX, NY, YR, MK, 3, XD>), g, b, 0, st, a);           \
+            break;
+        SPW_WS(WSV_160_160, 160, 160, 0, false, 0)
+        SPW_WS(WSV_160_160_ROW, 160, 160, 1, false, 0)
+        SPW_WS(WSV_128_160, 128, 160, 0, true, 0)
+        SPW_WS(WSV_160_128, 160, 128, 0, true, 0)
+        SPW_WS(WSV_128_128, 128, 128, 0, true, 0)
+        SPW_WS(WSV_XD_EDGE, 160, 160, 0, false, 1)
+        SPW_WS(WSV_XD_NODE, 128, 128, 0, true, 2)
 #undef SPW_WS
-    return hipErrorInvalidValue;
+        case WSV_XD_EDGE_B16Y: hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1, kB16Y>), g, b, 0, st, a); break;
+        case WSV_160_160_ROW_B16: hipLaunchKernelGGL((k_wgrad_ws<160, 160, 1, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a); break;
+        case WSV_160_160_B16: hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st) {
+    if (b.n <= 0) return hipSuccess;
+    if (b.n > kMaxWsJobs || b.wgs <= 0) return hipErrorInvalidValue;
+    if (math == MATH_BF16) hipLaunchKernelGGL(k_wgrad_ws_batch<1>, dim3(b.wgs), dim3(kWsThreads), 0, st, b);
+    else hipLaunchKernelGGL(k_wgrad_ws_batch<3>, dim3(b.wgs), dim3(kWsThreads), 0, st, b);
+    return hipGetLastError();
 }
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {
     if (rb.n <= 0) return hipSuccess;

@@ -1,0 +1,664 @@
+// Latency-oriented ("team") variants of the transposed-orientation chain kernels, for small batches.
+//
+// At the reference's own training shape (main.py:92-98: batch 32; BASELINE config 1) a chain kernel
+// has one 32-edge block per tower and a wave walks its block through the whole layer chain: the
+// relation encoder is 4 layers × 5 output tiles × 10 k-blocks × 6 MFMAs = 1,200 dependent-ish
+// 32-cycle products on ONE wave (≈ 18 µs of matrix time alone, 37 µs measured) while 1,000 SIMDs
+// idle. Here a workgroup of five waves takes one block and wave T owns output tile T of every layer:
+// 60 MFMAs per layer per wave. Layer outputs are exchanged through LDS in their C layout — the C
+// layout of a tile IS the B operand of the next layer's k-blocks 2t, 2t+1 (tchain_x6), so the
+// exchange is a plain per-lane store and load, no transposition. Every output tile sees the same
+// products in the same order as tgemm_x6 (k-blocks ascending, mfma32_x6's product order), so a
+// team kernel's results are bit-identical to the one-wave-per-block kernel's.
+// Weight fragments: wave T reads only its tile's steps (u = kb·NT_OUT + T) straight from the x6
+// image (L2); the next layer's fragment kb is requested as soon as this layer's k-block kb has
+// issued, so it arrives during the rest of the layer, the epilogue and the barrier.
+#include "kernels.h"
+#include <cstdlib>
+
+namespace spw {
+
+#ifdef SPWGNN_DIAG   // phase stamps (shader clock) of workgroup 0's waves 0 and 4: spwgnn_diag_team_stamps
+__device__ unsigned long long g_team_stamps[2][16];
+#define TEAM_STAMP(i)                                                                              \
+    do {                                                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+        if (blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == 256)) g_team_stamps[threadIdx.x >> 8][i] = t_; \
+    } while (0)
+#else
+#define TEAM_STAMP(i) do {} while (0)
+#endif
+
+constexpr int kTeamEdge = 5;   // waves per edge block (150-wide layers: 5 tiles of 32 features)
+
+// LDS exchange of C-layout tiles, already split: [buf][tile][kh][part][lane] uint4 = the bf16 parts
+// (split2, as tgemm_x6 splits them) of registers 8kh .. 8kh+7 of the tile — the B operand of the
+// next layer's k-block 2t + kh. The producer splits its tile once; the consumers only read.
+template <int NT, int NP>
+struct TeamAct {
+    uint4* s;
+    __device__ __forceinline__ uint4* at(int buf, int t, int kh, int p, int lane) const {
+        return s + (((buf * NT + t) * 2 + kh) * NP + p) * 64 + lane;
+    }
+    __device__ __forceinline__ void put(int buf, int t, const f32x16& x, int lane) const {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            uint32_t sp[3][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(x[8 * kh + 2 * m], x[8 * kh + 2 * m + 1], sp[0][m], sp[1][m], sp[2][m]);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) *at(buf, t, kh, p, lane) = make_uint4(sp[p][0], sp[p][1], sp[p][2], sp[p][3]);
+        }
+    }
+    // the split B operand of k-block kb (tchain_x6: registers 8(kb&1) .. +7 of tile kb>>1)
+    __device__ __forceinline__ void get(int buf, int kb, uint32_t (&sp)[3][4], int lane) const {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const uint4 u = p < NP ? *at(buf, kb >> 1, kb & 1, p, lane) : make_uint4(0u, 0u, 0u, 0u);
+            sp[p][0] = u.x; sp[p][1] = u.y; sp[p][2] = u.z; sp[p][3] = u.w;
+        }
+    }
+};
+// the exchange barrier: waits for this wave's LDS writes only (__syncthreads would also drain the
+// in-flight weight-fragment refills and the global stores of the layer's epilogue)
+__device__ __forceinline__ void team_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+// B values in registers (8 per k-block) → the split operand
+__device__ __forceinline__ void split8(const float (&v)[8], uint32_t (&sp)[3][4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) split2(v[2 * m], v[2 * m + 1], sp[0][m], sp[1][m], sp[2][m]);
+}
+
+// wave T's fragments of one x6 image (the parts the math uses)
+template <int NKB, int NP>
+struct TeamFrags {
+    uint4 f[NKB][3];
+    __device__ __forceinline__ void load_kb(const uint4* __restrict__ img, int nt_out, int T, int lane, int kb) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) f[kb][p] = img[((kb * nt_out + T) * 3 + p) * 64 + lane];
+    }
+    __device__ __forceinline__ void load(const uint4* __restrict__ img, int nt_out, int T, int lane) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) load_kb(img, nt_out, T, lane, kb);
+    }
+};
+
+// acc = Σ_kb W(kb, T)ᵀ·B(kb) (tgemm_x6's per-tile sum); getsp(kb, sp) supplies k-block kb's split
+// B operand. K-block kb+1's operand is requested before kb's products issue; after k-block kb,
+// next(kb) may refill f[kb] with the next layer's fragment.
+template <int NKB, int NP, class GetSp, class Next>
+__device__ __forceinline__ f32x16 team_gemm(TeamFrags<NKB, NP>& F, GetSp&& getsp, Next&& next, f32x16 acc = zero16()) {
+    uint32_t sp[2][3][4];
+    getsp(0, sp[0]);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        bf16x8 a[3], b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            a[p] = as_bf16x8(p < NP ? F.f[kb][p] : make_uint4(0u, 0u, 0u, 0u));
+            b[p] = as_bf16x8(make_uint4(sp[kb & 1][p][0], sp[kb & 1][p][1], sp[kb & 1][p][2], sp[kb & 1][p][3]));
+        }
+        if (kb + 1 < NKB) getsp(kb + 1, sp[(kb + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = mfma32_x6<NP>(a, b, acc);
+        next(kb);
+        __builtin_amdgcn_sched_barrier(0);   // keep the refills behind their k-block's products
+    }
+    return acc;
+}
+
+// ---- one tile of the chunk-major / sign-bit helpers (store_cm, store_pos_bits, apply_pos_bits)
+template <int KH>
+__device__ __forceinline__ void store_cm_tile(float* __restrict__ blk, const f32x16& x, int t, int lane) {
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (32 * t + 8 * q + 4 < 2 * KH)
+            *reinterpret_cast<float4*>(blk + cm_offk<KH>(j, 32 * t + 8 * q + 4 * h)) =
+                make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+}
+template <int KH>
+__device__ __forceinline__ void store_cm_tile(float* __restrict__ blk, const f32x16& x, int t, int lane, bool valid) {
+    if (valid) {
+        store_cm_tile<KH>(blk, x, t, lane);
+    } else {
+        f32x16 z = zero16();
+        store_cm_tile<KH>(blk, z, t, lane);
+    }
+}
+template <int KH>
+__device__ __forceinline__ f32x16 load_cm_tile(const float* __restrict__ blk, int t, int lane) {
+    const int j = lane & 31, h = lane >> 5;
+    f32x16 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (32 * t + 8 * q + 4 < 2 * KH) v = *reinterpret_cast<const float4*>(blk + cm_offk<KH>(j, 32 * t + 8 * q + 4 * h));
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+    return x;
+}
+// a chunk-major block's half rows as the B operand (HalfRows: lane half h holds features KH·h ..)
+template <int KH>
+struct TeamHalf {
+    static constexpr int Q = KH / 4;
+    float4 raw[Q];
+    __device__ __forceinline__ void load(const float* __restrict__ blk, int lane) {
+        const float* p = blk + ((lane >> 5) * 32 + (lane & 31)) * 4;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) raw[q] = *reinterpret_cast<const float4*>(p + 256 * q);
+    }
+    __device__ __forceinline__ void operator()(int kb, uint32_t (&sp)[3][4]) const {
+        const float4 x = raw[2 * kb];
+        const float4 y = 2 * kb + 1 < Q ? raw[2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        split8(v, sp);
+    }
+};
+// B operand from C-layout tiles held in registers (tchain_x6: k-block kb = registers 8(kb&1).. of tile kb>>1)
+template <int NT>
+struct TeamRegs {
+    const f32x16 (&x)[NT];
+    __device__ __forceinline__ void operator()(int kb, uint32_t (&sp)[3][4]) const {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = x[kb >> 1][8 * (kb & 1) + e];
+        split8(v, sp);
+    }
+};
+template <int KH>
+__device__ __forceinline__ void store_cm_tile_b16(uint16_t* __restrict__ blk, const f32x16& x, int t, int lane) {
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (32 * t + 8 * q + 4 < 2 * KH)
+            *reinterpret_cast<uint2*>(blk + cm_offk<KH>(j, 32 * t + 8 * q + 4 * h)) =
+                pack4_bf16(make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]));
+}
+// bits 16t .. 16t+15 of the lane's words (store_pos_bits of NT tiles): the tile's half of word t>>1;
+// the last tile of an odd NT owns its whole word (upper half zero, as store_pos_bits leaves it)
+template <int NT>
+__device__ __forceinline__ void store_pos_bits_tile(uint32_t* __restrict__ words, const f32x16& x, int t, int lane) {
+    uint32_t w = 0u;
+#pragma unroll
+    for (int r = 15; r >= 0; --r) w = __builtin_amdgcn_alignbit(w, __float_as_uint(x[r]) + 0x7fffffffu, 31);
+    uint32_t* p = words + 64 * (t >> 1) + lane;
+    if ((NT & 1) && t == NT - 1) *p = w;
+    else reinterpret_cast<uint16_t*>(p)[t & 1] = (uint16_t)w;
+}
+__device__ __forceinline__ void apply_pos_bits_tile(const uint32_t* __restrict__ words, f32x16& x, int t, int lane, float scale) {
+    const uint32_t w = words[64 * (t >> 1) + lane] >> (16 * (t & 1));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = mask_bit(x[r] * scale, w, r);
+}
+// a tile's bias values (padded vector, feature rho(r, h) + 32t), loaded ahead of the product
+__device__ __forceinline__ void bias_tile(float (&bv)[16], const float* __restrict__ b, int t, int h) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bv[r] = b[rho(r, 0) + 4 * h + 32 * t];
+}
+template <bool RELU>
+__device__ __forceinline__ void bias_act_tile(f32x16& x, const float (&bv)[16]) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float v = x[r] + bv[r];
+        x[r] = RELU ? relu(v) : v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// rm encoder (k_enc_edge_x6's chain, Networks.py:75,77): d → relu(rm.0) → 3 × (150×150 + relu) →
+// dropout = c_r → A = c_r·W1a + b1, one 32-edge block per 5-wave workgroup.
+template <bool TRAIN, int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_team(EncEdgeArgs a) {
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];   // ≤ 60 KiB
+    const TeamAct<kTeamEdge, NP> act{act_s};
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int blk = blockIdx.x;
+    const int64_t e = (int64_t)blk * 32 + j;
+    TEAM_STAMP(0);
+    TeamFrags<10, NP> F;
+    F.load(a.x_rm1, 5, T, lane);   // layer 1's fragments stream in during layer 0
+    const int src = a.esrc[e], dst = a.edst[e];
+    float dx = 0.f, dy = 0.f;
+    if (src >= 0) {
+        const float4 ps = reinterpret_cast<const float4*>(a.pos)[src];
+        const float4 pd = reinterpret_cast<const float4*>(a.pos)[dst];
+        dx = pd.x - ps.x;  // Networks.py:58-62 (receiver − sender), (x, y)
+        dy = pd.y - ps.y;
+    }
+    if (TRAIN && a.ed && T == 0 && h == 0) a.ed[e] = make_float2(dx, dy);
+    const bool drop = a.dropout_on && src >= 0;   // the dropout key's node fields, loaded early
+    const uint32_t d_tw = drop ? (uint32_t)a.node_tower[src] : 0u, d_ls = drop ? (uint32_t)a.node_local[src] : 0u,
+                   d_ld = drop ? (uint32_t)a.node_local[dst] : 0u;
+    f32x16 x;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = rho(r, 0) + 4 * h + 32 * T;
+        x[r] = relu(dense2(dx, dy, a.w_rm0[f], a.w_rm0[160 + f], a.b_rm0[f]));
+    }
+    const int64_t cmo = (int64_t)blk * kCmBlk;
+    uint32_t* const mb = TRAIN ? a.zmask + (int64_t)blk * 4 * 3 * 64 : nullptr;
+    auto save = [&](float* base, int layer, const f32x16& z, bool b16) {
+        if (base) {
+            if (B16 && b16) store_cm_tile_b16<kKhE>(reinterpret_cast<uint16_t*>(base) + cmo, z, T, lane);
+            else store_cm_tile<kKhE>(base + cmo, z, T, lane);
+        }
+        if (layer >= 0) store_pos_bits_tile<5>(mb + layer * 3 * 64, z, T, lane);
+    };
+    TEAM_STAMP(1);
+    if (TRAIN) save(a.z1, 0, x, false);
+    act.put(0, T, x, lane);
+    team_sync();
+    TEAM_STAMP(2);
+    const uint4* const next_img[4] = {a.x_rm2, a.x_rm3, a.x_w1a, nullptr};
+    const float* const bias[4] = {a.b_rm1, a.b_rm2, a.b_rm3, a.b_w1a};
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        float bv[16];
+        bias_tile(bv, bias[l], T, h);
+        x = team_gemm(
+            F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(l & 1, kb, sp, lane); },
+            [&](int kb) {
+                if (l < 3) F.load_kb(next_img[l], 5, T, lane, kb);
+            });
+        TEAM_STAMP(3 + 2 * l);
+        if (l < 3) {
+            bias_act_tile<true>(x, bv);   // rm's last Dense is linear; relu from Networks.py:75
+        } else {
+            bias_act_tile<false>(x, bv);
+        }
+        if (l == 2 && drop) {   // Networks.py:77
+            const uint32_t key = drop_row_key(run_seed(a), 1u, d_tw, d_ls, d_ld);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * T;
+                x[r] = drop_keep(key, (uint32_t)f, a.thresh) ? x[r] * a.scale : 0.f;
+            }
+        }
+        if (l == 3) {
+            save(a.A, -1, x, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
+        } else {
+            if (TRAIN) save(l == 0 ? a.z2 : l == 1 ? a.z3 : a.cr, l + 1, x, true);
+            act.put((l + 1) & 1, T, x, lane);
+            team_sync();
+            TEAM_STAMP(4 + 2 * l);
+        }
+    }
+    TEAM_STAMP(10);
+}
+
+// ------------------------------------------------------------------------------------------------
+// rm encoder backward (k_enc_edge_bwd_x6's chain): dc_r = dA·W1aᵀ (B from the dA half rows, read by
+// every wave), then dz4 .. dz1 through the rm layers' transposed images.
+template <int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_bwd_team(EncEdgeBwdArgs a) {
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    const TeamAct<kTeamEdge, NP> act{act_s};
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int blk = blockIdx.x;
+    const int64_t e = (int64_t)blk * 32 + j;
+    TeamFrags<10, NP> F;
+    F.load(a.x_w1at, 5, T, lane);
+    float4 raw[kKhE / 4];
+    if constexpr (B16) {
+        const uint2* row = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.dA) + e * kLdE + kKhE * h);
+#pragma unroll
+        for (int q = 0; q < kKhE / 4; ++q) raw[q] = unpack4_bf16(row[q]);
+    } else {
+        const float4* row = reinterpret_cast<const float4*>(a.dA + e * kLdE + kKhE * h);
+#pragma unroll
+        for (int q = 0; q < kKhE / 4; ++q) raw[q] = row[q];
+    }
+    const int64_t cmo = (int64_t)blk * kCmBlk;
+    const uint32_t* const mb = a.zmask + (int64_t)blk * 4 * 3 * 64;
+    const uint4* const next_img[4] = {a.x_rm3t, a.x_rm2t, a.x_rm1t, nullptr};
+    float* const out[4] = {a.dz4, a.dz3, a.dz2, a.dz1};
+    f32x16 x = team_gemm(
+        F,
+        [&](int kb, uint32_t (&sp)[3][4]) {
+            const float4 p = raw[2 * kb];
+            const float4 q = 2 * kb + 1 < kKhE / 4 ? raw[2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+            split8(v, sp);
+        },
+        [&](int kb) { F.load_kb(next_img[0], 5, T, lane, kb); });   // dc_r = dA·W1aᵀ
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        apply_pos_bits_tile(mb + (3 - l) * 3 * 64, x, T, lane, l == 0 ? a.scale : 1.f);   // relu (+ dropout) of layer 3 − l
+        if constexpr (B16) store_cm_tile_b16<kKhE>(reinterpret_cast<uint16_t*>(out[l]) + cmo, x, T, lane);
+        else store_cm_tile<kKhE>(out[l] + cmo, x, T, lane);
+        if (l == 3) break;
+        act.put(l & 1, T, x, lane);
+        team_sync();
+        x = team_gemm(
+            F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(l & 1, kb, sp, lane); },
+            [&](int kb) {
+                if (l < 2) F.load_kb(next_img[l + 1], 5, T, lane, kb);
+            });
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// om encoder (k_enc_node_x6's chain, Networks.py:76,78): every wave rebuilds the four tiles of
+// z1 = relu(om.0(y, w)) and of P0 (the 'propagation' input) in registers — cheap VALU and loads — so
+// no layer output crosses waves: wave T < 4 owns tile T of c_o, waves 0..4 tile T of U0 and V0.
+template <int NP>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_node_team(EncNodeArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = blockIdx.x;
+    const int n = nb * 32 + j;
+    const bool valid = n < a.n_nodes;
+    const int nc = valid ? n : a.n_nodes - 1;
+    TeamFrags<7, NP> F;
+    if (T < 4) F.load(a.x_om1, 4, T, lane);
+    else F.load(a.x_w1b, 5, T, lane);
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;
+    if (T < 4) {
+        const float4 p = reinterpret_cast<const float4*>(a.pos)[nc];
+        f32x16 Z[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * t;
+                Z[t][r] = relu(dense2(p.y, p.z, a.w_om0[f], a.w_om0[128 + f], a.b_om0[f]));   // Networks.py:65-71: (y, width)
+            }
+        if (a.zo1) {
+            f32x16 zt = Z[0];   // tile T (selected: a runtime index would put the array in scratch)
+#pragma unroll
+            for (int t = 1; t < 4; ++t)
+                if (T == t) zt = Z[t];
+            store_cm_tile<kKhN>(a.zo1 + bN, zt, T, lane, valid);
+        }
+        float bv[16];
+        bias_tile(bv, a.b_om1, T, h);
+        const uint32_t key = a.dropout_on ? drop_row_key(run_seed(a), 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu) : 0u;
+        f32x16 C = team_gemm(F, TeamRegs<4>{Z}, [&](int kb) { F.load_kb(a.x_w1b, 5, T, lane, kb); });
+        bias_act_tile<true>(C, bv);   // relu(om(.)) — Networks.py:76
+        if (a.dropout_on) {           // Networks.py:78
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = rho(r, 0) + 4 * h + 32 * T;
+                C[r] = drop_keep(key, (uint32_t)f, a.thresh) ? C[r] * a.scale : 0.f;
+            }
+        }
+        store_cm_tile<kKhN>(a.co + bN, C, T, lane, valid);
+    }
+    // P0: the 'propagation' input (Networks.py:29,79), ld 100 → workspace ld 128
+    f32x16 P[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.prop && f0 < kFN && valid) v = *reinterpret_cast<const float4*>(a.prop + (int64_t)n * kFN + f0);
+            P[t][4 * q] = v.x; P[t][4 * q + 1] = v.y; P[t][4 * q + 2] = v.z; P[t][4 * q + 3] = v.w;
+        }
+    if (T < 4) {
+        f32x16 pt = P[0];
+#pragma unroll
+        for (int t = 1; t < 4; ++t)
+            if (T == t) pt = P[t];
+        store_cm_tile<kKhN>(a.P0 + bN, pt, T, lane, valid);
+    }
+    f32x16 U = team_gemm(F, TeamRegs<4>{P}, [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
+    store_cm_tile<kKhE>(a.U0 + bE, U, T, lane, valid);
+    U = team_gemm(F, TeamRegs<4>{P}, [&](int) {});
+    store_cm_tile<kKhE>(a.V0 + bE, U, T, lane, valid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// node side of one step (k_node_fwd_x6's chain, Networks.py:88-96): waves 0..3 own the four node
+// tiles of a, o1, x' and P' (three LDS exchanges), all five waves one tile each of U', V'.
+template <int NP>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_node_fwd_team(NodeFwdArgs a) {
+    __shared__ uint4 act_s[2 * 4 * 2 * NP * 64];
+    const TeamAct<4, NP> act{act_s};
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = blockIdx.x;
+    const bool valid = nb * 32 + j < a.n_nodes;
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;
+    const bool nw = T < 4;   // node-tile wave
+    TeamFrags<10, NP> F10;
+    TeamFrags<7, NP> F;
+    const uint4* const first7 = a.cw_in ? a.x_wo1a : a.x_wo1c;
+    if (nw) F10.load(a.x_w3a, 4, T, lane);
+    f32x16 O;
+    if (nw) {
+        // a = tanh([H2s | deg]·[W3; b3])   (Networks.py:88, layer 3 after the sum)
+        f32x16 E;
+        {
+            TeamHalf<kKhE> hr;
+            hr.load(a.H2s + bE, lane);
+            E = team_gemm(F10, hr, [&](int kb) {
+                if (kb < 7) F.load_kb(first7, 4, T, lane, kb);
+            });
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * T;
+            E[r] = f < kFN ? fast_tanh(E[r]) : 0.f;
+        }
+        if (a.a_out) store_cm_tile<kKhN>(a.a_out + bN, E, T, lane, valid);
+        act.put(0, T, E, lane);
+        // o1 = relu([c_o | a | P]·Wo1 + bo1): c_o·Wo1c (or step 0's stored accumulator) first
+        if (a.cw_in) {
+            O = load_cm_tile<kKhN>(a.cw_in + bN, T, lane);
+        } else {
+            TeamHalf<kKhN> hr;
+            hr.load(a.co + bN, lane);
+            O = team_gemm(F, hr, [&](int kb) { F.load_kb(a.x_wo1a, 4, T, lane, kb); });
+            if (a.cw_out) store_cm_tile<kKhN>(a.cw_out + bN, O, T, lane);
+        }
+    }
+    team_sync();
+    if (nw) {
+        O = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
+                      [&](int kb) { F.load_kb(a.x_wo1p, 4, T, lane, kb); }, O);
+        {
+            TeamHalf<kKhN> hr;
+            hr.load(a.P + bN, lane);
+            float bv[16];
+            bias_tile(bv, a.bo1, T, h);
+            O = team_gemm(F, hr, [&](int kb) { F.load_kb(a.x_wo2, 4, T, lane, kb); }, O);
+            bias_act_tile<true>(O, bv);
+        }
+        if (a.o1_out) store_cm_tile<kKhN>(a.o1_out + bN, O, T, lane, valid);
+        act.put(1, T, O, lane);
+    }
+    team_sync();
+    if (nw) {
+        // x' = o1·Wo2' + bo2'; P' = tanh(x'[0:100] + P); logit = x'[100]  (Networks.py:91, 94)
+        float bv[16];
+        bias_tile(bv, a.bo2p, T, h);
+        const f32x16 P = load_cm_tile<kKhN>(a.P + bN, T, lane);
+        f32x16 X = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
+                             [&](int kb) {
+                                 if (a.U) F.load_kb(a.x_w1b, 5, T, lane, kb);
+                             });
+        bias_act_tile<false>(X, bv);
+        if (T == 3 && a.logits && h == 1 && valid) a.logits[nb * 32 + j] = X[0];   // x' row 100 = rho(0, 1) + 96
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * T;
+            X[r] = f < kFN ? fast_tanh(X[r] + P[r]) : 0.f;   // X := P'
+        }
+        store_cm_tile<kKhN>(a.Pn + bN, X, T, lane, valid);
+        act.put(0, T, X, lane);
+    } else if (a.U) {
+        F.load(a.x_w1b, 5, T, lane);
+    }
+    team_sync();
+    if (a.U) {   // U' = P'·W1b, V' = P'·W1c for the next step
+        f32x16 U = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
+                             [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
+        store_cm_tile<kKhE>(a.U + bE, U, T, lane, valid);
+        U = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
+        store_cm_tile<kKhE>(a.V + bE, U, T, lane, valid);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// node side of one backward step (k_node_bwd_x6's chain, x6/bf16 math with dco_sum): waves 0..3 own
+// the node tiles of dP, dx, do1, dP_out and g (two LDS exchanges), all five waves one tile of G3.
+template <int NP>
+__global__ __launch_bounds__(256, 1) void k_node_bwd_team(NodeBwdArgs a) {
+    __shared__ uint4 act_s[2 * 4 * 2 * NP * 64];
+    const TeamAct<4, NP> act{act_s};
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = blockIdx.x;
+    const bool valid = nb * 32 + j < a.n_nodes;
+    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;
+    constexpr bool nw = true;   // four waves, one per SIMD (the full register file: 512 per lane)
+    TeamFrags<10, NP> F10;
+    TeamFrags<7, NP> F;
+    if (nw && !a.first) F10.load(a.x_w1bt, 4, T, lane);
+    else if (nw && !a.tail) F.load(a.x_wo2t, 4, T, lane);
+    f32x16 D = zero16();
+    if (nw && !a.first) {   // dP = dPin + dU·W1bᵀ + dV·W1cᵀ
+        D = load_cm_tile<kKhN>(a.dPin + bN, T, lane);
+        TeamHalf<kKhE> hr;
+        hr.load(a.dU + bE, lane);
+        D = team_gemm(F10, hr, [&](int kb) { F10.load_kb(a.x_w1ct, 4, T, lane, kb); }, D);
+        hr.load(a.dV + bE, lane);
+        D = team_gemm(F10, hr, [&](int) {}, D);
+        if (!a.tail) F.load(a.x_wo2t, 4, T, lane);
+    }
+    if (a.tail) {   // dP0 = d/d 'propagation' (ld 100)
+        if (nw && valid) {
+            const int64_t n = (int64_t)nb * 32 + j;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int f0 = 32 * T + 8 * q + 4 * h;
+                if (f0 < kFN) *reinterpret_cast<float4*>(a.dprop + n * kFN + f0) = make_float4(D[4 * q], D[4 * q + 1], D[4 * q + 2], D[4 * q + 3]);
+            }
+        }
+        return;
+    }
+    f32x16 dP;
+    if (nw) {
+        const f32x16 Pn = load_cm_tile<kKhN>(a.Pn + bN, T, lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * T;
+            D[r] = f < kFN ? D[r] * (1.f - Pn[r] * Pn[r]) : 0.f;   // tanh' (Networks.py:91)
+        }
+        // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
+        store_cm_tile<kKhN>(a.dPout + bN, D, T, lane, valid);
+        dP = D;
+        if (a.first && T == 3 && h == 1) D[0] = valid ? a.dlogits[nb * 32 + j] : 0.f;   // x' row 100 = logit
+        store_cm_tile<kKhN>(a.dx + bN, D, T, lane, valid);
+        act.put(0, T, D, lane);
+    }
+    team_sync();
+    if (nw) {   // do1 = dx'·Wo2'ᵀ ⊙ [o1 > 0]
+        const f32x16 O1 = load_cm_tile<kKhN>(a.o1 + bN, T, lane);
+        f32x16 G = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
+                             [&](int kb) { F.load_kb(a.x_wo1pt, 4, T, lane, kb); });
+#pragma unroll
+        for (int r = 0; r < 16; ++r) G[r] = O1[r] > 0.f ? G[r] : 0.f;
+        store_cm_tile<kKhN>(a.do1 + bN, G, T, lane, valid);
+        act.put(1, T, G, lane);
+    }
+    team_sync();
+    if (nw) {
+        // P part of omp's input → dP_s
+        D = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
+                      [&](int kb) { F.load_kb(a.x_wo1at, 4, T, lane, kb); });
+#pragma unroll
+        for (int r = 0; r < 16; ++r) D[r] += dP[r];
+        store_cm_tile<kKhN>(a.dPout + bN, D, T, lane, valid);
+        // effect part → g = da ⊙ (1 − a²)
+        const f32x16 Aa = load_cm_tile<kKhN>(a.a + bN, T, lane);
+        D = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
+                      [&](int kb) { F.load_kb(a.x_w3t, 5, T, lane, kb); });
+#pragma unroll
+        for (int r = 0; r < 16; ++r) D[r] = D[r] * (1.f - Aa[r] * Aa[r]);
+        store_cm_tile<kKhN>(a.g + bN, D, T, lane, valid);
+        act.put(0, T, D, lane);
+    }
+    team_sync();
+    // G3 = g·W3ᵀ (the per-edge dh2 is G3[receiver]): tile T, and wave 0 also tile 4
+    f32x16 H = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int kb) {
+        if (T == 0) F.load_kb(a.x_w3t, 5, 4, lane, kb);
+    });
+    store_cm_tile<kKhE>(a.G3 + bE, H, T, lane, valid);
+    if (T == 0) {
+        H = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
+        store_cm_tile<kKhE>(a.G3 + bE, H, 4, lane, valid);
+    }
+}
+
+bool team_blocks(int n_blocks) {
+#ifdef SPWGNN_DIAG   // A/B: SPWGNN_NO_TEAM=1 keeps the one-wave-per-block kernels at every size
+    static const bool off = getenv("SPWGNN_NO_TEAM") && atoi(getenv("SPWGNN_NO_TEAM"));
+    if (off) return false;
+#endif
+    return n_blocks > 0 && n_blocks <= kTeamMaxBlocks;
+}
+
+hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipStream_t st) {
+    const dim3 g(a.n_eblocks), b(64 * kTeamEdge);
+    if (math == MATH_BF16) {
+        if (train && a.b16) hipLaunchKernelGGL((k_enc_edge_team<true, 1, true>), g, b, 0, st, a);
+        else if (train) hipLaunchKernelGGL((k_enc_edge_team<true, 1, false>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_enc_edge_team<false, 1, false>), g, b, 0, st, a);
+    } else if (math == MATH_X6) {
+        if (train) hipLaunchKernelGGL((k_enc_edge_team<true, 3, false>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_enc_edge_team<false, 3, false>), g, b, 0, st, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st) {
+    const dim3 g((a.n_nodes + 31) / 32), b(64 * kTeamEdge);
+    if (math == MATH_BF16) hipLaunchKernelGGL((k_enc_node_team<1>), g, b, 0, st, a);
+    else if (math == MATH_X6) hipLaunchKernelGGL((k_enc_node_team<3>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st) {
+    const dim3 g((a.n_nodes + 31) / 32), b(64 * kTeamEdge);
+    if (math == MATH_BF16) hipLaunchKernelGGL((k_node_fwd_team<1>), g, b, 0, st, a);
+    else if (math == MATH_X6) hipLaunchKernelGGL((k_node_fwd_team<3>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_node_bwd_team(const NodeBwdArgs& a, int math, hipStream_t st) {
+    if (!a.dco_sum) return hipErrorInvalidValue;
+    const dim3 g((a.n_nodes + 31) / 32), b(64 * kTeamEdge);
+    if (math == MATH_BF16) hipLaunchKernelGGL((k_node_bwd_team<1>), g, dim3(256), 0, st, a);
+    else if (math == MATH_X6) hipLaunchKernelGGL((k_node_bwd_team<3>), g, dim3(256), 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_enc_edge_bwd_team(const EncEdgeBwdArgs& a, int math, hipStream_t st) {
+    const dim3 g(a.n_eblocks), b(64 * kTeamEdge);
+    if (math == MATH_BF16) {
+        if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_team<1, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_enc_edge_bwd_team<1, false>), g, b, 0, st, a);
+    } else if (math == MATH_X6) {
+        hipLaunchKernelGGL((k_enc_edge_bwd_team<3, false>), g, b, 0, st, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace spw
+
+#ifdef SPWGNN_DIAG
+extern "C" int32_t spwgnn_diag_team_stamps(unsigned long long* out32) {
+    return hipMemcpyFromSymbol(out32, HIP_SYMBOL(spw::g_team_stamps), sizeof(spw::g_team_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
