@@ -593,14 +593,16 @@ def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
     print(json.dumps(out), flush=True)
 
 
-# kernel families: one SPWGNN_K_* id over several kernels of different shapes (listed in the table,
-# never named as "the dominant kernel" — a roofline belongs to one kernel)
+# kernel families: one SPWGNN_K_* id over several weight-gradient shapes. Batched (the default:
+# k_wgrad_ws_batch, one launch per backward) the family IS one kernel and can be named dominant;
+# unbatched (SPWGNN_WS_UNBATCHED, one launch per shape) it is listed but never named — a roofline
+# belongs to one kernel.
 FAMILIES = ("wgrad_ws",)
 
 
 def dominant(table) -> str:
     """The single kernel with the largest time per step in this run's kernel table."""
-    single = {k: v for k, v in table.items() if k not in FAMILIES}
+    single = {k: v for k, v in table.items() if k not in FAMILIES or v.get("batched")}
     return max(single, key=lambda k: single[k]["ms_per_step"]) if single else "edge_fwd"
 
 
@@ -620,7 +622,10 @@ def kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, config, wl, steps=2
                        "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
                        "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
         if name in FAMILIES:
-            table[name]["family"] = "several kernels of different shapes under one id; frac over the family"
+            table[name]["batched"] = bool(per_step <= n_micro)
+            table[name]["family"] = ("one launch per backward batching every weight-gradient shape (k_wgrad_ws_batch)"
+                                     if per_step <= n_micro else
+                                     "several kernels of different shapes under one id; frac over the family")
     return table
 
 

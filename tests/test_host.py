@@ -205,6 +205,22 @@ def test_bench_pmc_names_match_committed_summaries():
         assert bench.step_hbm(config, 10.0, math, wl) is not None, path
 
 
+def test_bench_dominant_kernel_rule():
+    """The roofline names the kernel with the largest ms per step; the weight-gradient family counts
+    as one kernel only when it ran as one batched launch per backward (k_wgrad_ws_batch)."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    table = {"edge_fwd": {"ms_per_step": 3.7}, "dA": {"ms_per_step": 2.4},
+             "wgrad_ws": {"ms_per_step": 4.6, "batched": True}}
+    assert bench.dominant(table) == "wgrad_ws"
+    table["wgrad_ws"]["batched"] = False
+    assert bench.dominant(table) == "edge_fwd"
+    assert bench.dominant({}) == "edge_fwd"
+
+
 def test_plan_without_any_edge_and_empty_batch():
     """Single-box towers: no edge list at all (NULL src/dst through the C-ABI), one padding block
     per wave-tile; an empty batch is rejected before the library is called."""
