@@ -582,6 +582,21 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
             SPW_CHECK(launch_wgrad_ws(wa, (int)wgs, g.kx_pad, g.ny_pad, g.ymode == YM_ROW, mask, math, st, g.b16));
             if (prof) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_WS));
         }
+    } else if (math != MATH_F32 && (g.xmode == XM_NODE_O || (g.xmode == XM_EDGE_D && g.xd))) {
+        // the 3-column first-layer gradients: a vector-ALU stream over Y (k_wgrad_pos3)
+        const bool node = g.xmode == XM_NODE_O;
+        Pos3Args pa{};
+        pa.y = g.y;
+        pa.pos = reinterpret_cast<const float4*>(b->pos);
+        pa.ed = g.xd;
+        pa.esrc = b->edge_src;
+        pa.slab = slab;
+        pa.count = g.rows;
+        pa.nblk = (g.rows + 31) / 32;
+        const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>(pa.nblk, std::min<int64_t>(512, slot_chunks)));
+        pa.blk_per_wg = (pa.nblk + wgs - 1) / wgs;
+        chunks = (pa.nblk + pa.blk_per_wg - 1) / pa.blk_per_wg;
+        SPW_CHECK(launch_wgrad_pos3(pa, (int)chunks, node, (g.b16 & kB16Y) != 0, st));
     } else {
     // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
     const bool ws = g.recompute && math != MATH_F32 && (math == MATH_BF16 || !getenv_flag("SPWGNN_W2G_OLD"));
@@ -797,6 +812,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
         g.b16 = b16 ? kB16Y : 0;   // Y = dz1
+        if (z1_rebuilt(r)) g.xd = reinterpret_cast<const float2*>(c.f(w.ed));   // k_wgrad_pos3 reads d
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)

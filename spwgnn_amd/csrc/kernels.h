@@ -314,6 +314,16 @@ hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st);
 hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st, int b16 = 0);
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st);
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
+// k_wgrad_pos3: the 3-column first-layer gradients (rm.0, om.0) in the split-bf16 maths
+struct Pos3Args {
+    const float* y;          // chunk-major Y (fp32, or bf16 with the fp32 element layout: b16)
+    const float4* pos;       // om.0: X = (y, w) of the node positions
+    const float2* ed;        // rm.0: the encoder's per-edge (dx, dy) (padding edge: esrc < 0 → X = 0)
+    const int32_t* esrc;
+    float* slab;             // [chunks][32][NYP]
+    int64_t nblk, blk_per_wg, count;
+};
+hipError_t launch_wgrad_pos3(const Pos3Args& a, int chunks, bool node, bool b16, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank, hipStream_t st);

@@ -1366,6 +1366,99 @@ __global__ void k_tower_readout(const float* __restrict__ z, const int32_t* __re
 }
 
 // ------------------------------------------------------------------------------------------------
+// The two first-layer gradients whose X has three columns (rm.0: X = [pos[dst] − pos[src] | 1],
+// padding edge → 0; om.0: X = [pos[n].y, pos[n].z | 1], rows ≥ count → 0), in the split-bf16 maths:
+// dW[k][f] = Σ_rows X[row][k]·Y[row][f] is a 3-column contraction — 6 FLOPs per Y element against
+// 4 (2 in bf16 storage) bytes of it, far below the ridge point, so it runs on the vector ALUs as a
+// stream over Y (exact fp32 fmas, no split) instead of padded 32-row MFMA tiles behind two barriers
+// per 32-row stage (k_wgrad_x6: config 3's rm.0 gradient 1.3 ms at 2 TB/s). A workgroup owns a
+// contiguous range of 32-row blocks; thread (row i = tid & 31, piece g = tid >> 5) keeps the three
+// sums of chunk-major pieces g, g + 8, ... of row i over the range (fixed order), the 32 rows of a
+// piece are summed across the half-wave in a fixed butterfly, and the slab rows 0-2 (kernel rows d0,
+// d1 / y, w and the bias row) go to this workgroup's chunk for k_wgrad_reduce_all. Pieces past the
+// row's last one (qh ≥ NQH) re-read the last piece and are never written out.
+template <int KH, bool NODE, bool B16>
+__global__ __launch_bounds__(256) void k_wgrad_pos3(Pos3Args a) {
+    constexpr int NQH = KH / 2, NK = (NQH + 7) / 8, NYP = KH == kKhE ? 160 : 128, BLK = KH * 64;
+    constexpr int UB = 4;   // blocks whose loads are issued together (the loop is latency-bound)
+    const int tid = threadIdx.x, i = tid & 31, g = tid >> 5;
+    const int64_t b0 = (int64_t)blockIdx.x * a.blk_per_wg, b1 = min(a.nblk, b0 + a.blk_per_wg);
+    float4 s0[NK], s1[NK], s2[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) s0[k] = s1[k] = s2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t bg = b0; bg < b1; bg += UB) {
+        float x0[UB], x1[UB], x2[UB];
+        float4 y[UB][NK];
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            const bool in = bg + u < b1;
+            const int64_t b = in ? bg + u : b1 - 1;
+            const int64_t row = b * 32 + i;
+            if constexpr (NODE) {
+                const bool ok = in && row < a.count;
+                const float4 p = a.pos[ok ? row : 0];
+                x0[u] = ok ? p.y : 0.f;
+                x1[u] = ok ? p.z : 0.f;
+                x2[u] = ok ? 1.f : 0.f;
+            } else {   // d from the encoder's stored per-edge (dx, dy): no dependent gathers
+                const bool ok = in && a.esrc[row] >= 0;
+                const float2 d = a.ed[row];
+                x0[u] = ok ? d.x : 0.f;
+                x1[u] = ok ? d.y : 0.f;
+                x2[u] = ok ? 1.f : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int qh = min(g + 8 * k, NQH - 1);
+                const int64_t el = b * BLK + (qh * 32 + i) * 4;
+                y[u][k] = B16 ? unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.y) + el))
+                              : *reinterpret_cast<const float4*>(a.y + el);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const float4 v = y[u][k];
+                s0[k] = make_float4(__builtin_fmaf(x0[u], v.x, s0[k].x), __builtin_fmaf(x0[u], v.y, s0[k].y),
+                                    __builtin_fmaf(x0[u], v.z, s0[k].z), __builtin_fmaf(x0[u], v.w, s0[k].w));
+                s1[k] = make_float4(__builtin_fmaf(x1[u], v.x, s1[k].x), __builtin_fmaf(x1[u], v.y, s1[k].y),
+                                    __builtin_fmaf(x1[u], v.z, s1[k].z), __builtin_fmaf(x1[u], v.w, s1[k].w));
+                s2[k] = make_float4(__builtin_fmaf(x2[u], v.x, s2[k].x), __builtin_fmaf(x2[u], v.y, s2[k].y),
+                                    __builtin_fmaf(x2[u], v.z, s2[k].z), __builtin_fmaf(x2[u], v.w, s2[k].w));
+            }
+    }
+    auto hsum = [&](float v) {   // the 32 rows of this half-wave, fixed butterfly
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+        return v;
+    };
+    float* out = a.slab + (int64_t)blockIdx.x * 32 * NYP;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        const int qh = g + 8 * k;
+        if (qh >= NQH) continue;   // uniform per half-wave
+        const float4 r0 = make_float4(hsum(s0[k].x), hsum(s0[k].y), hsum(s0[k].z), hsum(s0[k].w));
+        const float4 r1 = make_float4(hsum(s1[k].x), hsum(s1[k].y), hsum(s1[k].z), hsum(s1[k].w));
+        const float4 r2 = make_float4(hsum(s2[k].x), hsum(s2[k].y), hsum(s2[k].z), hsum(s2[k].w));
+        if (i == 0) {
+            const int f = KH * (qh & 1) + 4 * (qh >> 1);   // features f .. f+3 (chunk-major piece qh)
+            *reinterpret_cast<float4*>(out + f) = r0;
+            *reinterpret_cast<float4*>(out + NYP + f) = r1;
+            *reinterpret_cast<float4*>(out + 2 * NYP + f) = r2;
+        }
+    }
+}
+hipError_t launch_wgrad_pos3(const Pos3Args& a, int chunks, bool node, bool b16, hipStream_t st) {
+    if (chunks <= 0) return hipSuccess;
+    const dim3 g(chunks), b(256);
+    if (node && !b16) hipLaunchKernelGGL((k_wgrad_pos3<kKhN, true, false>), g, b, 0, st, a);
+    else if (!node && !b16) hipLaunchKernelGGL((k_wgrad_pos3<kKhE, false, false>), g, b, 0, st, a);
+    else if (!node && b16) hipLaunchKernelGGL((k_wgrad_pos3<kKhE, false, true>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 hipError_t launch_wgrad(const WgradArgs& a, int chunks, int math, hipStream_t st) {
     const dim3 g(chunks), b(kWgThreads);
 #define SPW_WG(XM, YM, KX, NY)                                                               \
