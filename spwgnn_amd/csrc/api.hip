@@ -576,6 +576,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
             j.a = wa;
             j.variant = v;
             j.wg0 = wsb->wgs;
+            j.gn = j.gi = 0;
             wsb->wgs += (int)wgs;
         } else {
             if (prof) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_WS));
@@ -634,6 +635,25 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
     ra.bias_row = g.bias_row;
     ra.perm = g.perm;
     return SPWGNN_OK;
+}
+
+// Jobs [first, first + n) of the batch read one operand in common (the node rows P / do1): run them
+// as an interleaved group (k_wgrad_ws_batch) when their row ranges match — the same workgroup count,
+// a multiple of the 8 XCDs, over the same stage partition; otherwise they stay in sequence.
+static void ws_group(WsBatch* wsb, int first, int n) {
+    if (!wsb || n < 2 || first < 0 || first + n > wsb->n || getenv_flag("SPWGNN_WS_NOGROUP")) return;
+    const WsJob& j0 = wsb->j[first];
+    const int w0 = (first + 1 < wsb->n ? wsb->j[first + 1].wg0 : wsb->wgs) - j0.wg0;
+    if (w0 <= 0 || w0 % 8) return;
+    for (int i = 1; i < n; ++i) {
+        const WsJob& ji = wsb->j[first + i];
+        const int wi = (first + i + 1 < wsb->n ? wsb->j[first + i + 1].wg0 : wsb->wgs) - ji.wg0;
+        if (wi != w0 || ji.a.stages_per_wg != j0.a.stages_per_wg || ji.a.nbs != j0.a.nbs || ji.a.S != j0.a.S) return;
+    }
+    for (int i = 0; i < n; ++i) {
+        wsb->j[first + i].gn = n;
+        wsb->j[first + i].gi = i;
+    }
 }
 
 int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w, char* base,
@@ -847,6 +867,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.rows = nN * S; g.kx_pad = kxp; g.ny_pad = nyp;
         g.xmode = XM_CM; g.ymode = YM_CM;   // chunk-major node rows
     };
+    const int grp0 = wsb.n;   // W1b, W1c, omp.0 P part (X = P), omp.0 effect part (Y = do1): one group
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
@@ -857,6 +878,17 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
     }
+    {   // omp.0 rows 200..299 (P part)
+        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+    }
+    {   // omp.0 rows 100..199 (effect part)
+        WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+    }
+    if (wsp) ws_group(wsp, grp0, wsb.n - grp0);
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
@@ -870,16 +902,6 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.rows = nN;
             g.y_stride = 0;
         }
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
-    }
-    {   // omp.0 rows 100..199 (effect part)
-        WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
-    }
-    {   // omp.0 rows 200..299 (P part)
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order

@@ -262,6 +262,7 @@ enum WsVariant : int {
 struct WsJob {
     WgWsArgs a;
     int variant, wg0;      // WsVariant; first workgroup of the job in the batched grid
+    int gn, gi;            // operand-sharing group (ws_group): its size (≤ 1: none) and this job's index
 };
 constexpr int kMaxWsJobs = 16;
 struct WsBatch {           // the k_wgrad_ws gradients of one backward (k_wgrad_ws_batch)

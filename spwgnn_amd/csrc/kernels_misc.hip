@@ -1215,8 +1215,18 @@ void k_wgrad_ws_batch(WsBatch b) {
     __shared__ __attribute__((aligned(16))) char smem[2 * kWsMaxBuf];
     int k = 0;
     while (k + 1 < b.n && (int)blockIdx.x >= b.j[k + 1].wg0) ++k;
+    int bid = (int)blockIdx.x - b.j[k].wg0;
+    if (b.j[k].gn > 1) {
+        // an operand-sharing group of G jobs with the same row ranges (ws_group): slot q of the group
+        // runs job q/8 mod G on its workgroup (q/8/G)·8 + q mod 8, so the G workgroups of one row
+        // range sit 8 slots apart — on one XCD (workgroups go round-robin over the 8 XCDs) at the
+        // same time, and the shared operand's rows come from that XCD's L2 after the first read
+        const int first = k - b.j[k].gi, G = b.j[k].gn;
+        const int q = (int)blockIdx.x - b.j[first].wg0, r = q >> 3;
+        k = first + r % G;
+        bid = (r / G) * 8 + (q & 7);
+    }
     const WsJob& job = b.j[k];
-    const int bid = (int)blockIdx.x - job.wg0;
     switch (job.variant) {
         case WSV_160_160: wgrad_ws_body<160, 160, 0, false, NP, 0, 0>(job.a, bid, smem); break;
         case WSV_160_160_ROW: wgrad_ws_body<160, 160, 1, false, NP, 0, 0>(job.a, bid, smem); break;
