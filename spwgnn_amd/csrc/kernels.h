@@ -336,6 +336,9 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
 constexpr int kTeamMaxBlocks = 512;
 bool team_blocks(int n_blocks);   // 32-row blocks of the launch (edge or node blocks)
 hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st);
+hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st);
+hipError_t launch_edge_bwd_team(const EdgeBwdArgs& a, int math, hipStream_t st);
+hipError_t launch_dA_team(const DaArgs& a, int math, hipStream_t st);
 hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_bwd_team(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipStream_t st);

@@ -845,6 +845,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
+    if (math != MATH_F32 && a.nw_max <= 16 && a.no_dA && team_blocks(a.n_wtiles))   // small batches
+        return launch_edge_bwd_team(a, math, st);
     if (math != MATH_F32 && a.nw_max <= 16) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
         // no_dA: dA = Σ_s dh1pre_s is rebuilt once after the step loop by k_dA_x6 (launch_dA)
@@ -1021,6 +1023,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st) {
+    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks(a.n_eblocks)) return launch_dA_team(a, math, st);
     const dim3 g(edge_grid(a.n_eblocks, 8)), b(512);
     if (math == MATH_BF16 && a.b16) hipLaunchKernelGGL((k_dA_x6<1, true>), g, b, 0, st, a);
     else if (math == MATH_BF16) hipLaunchKernelGGL((k_dA_x6<1>), g, b, 0, st, a);

@@ -1156,6 +1156,8 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 }
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
+    // small batches: a workgroup of five waves per wave-tile, one output tile per wave (kernels_team.hip)
+    if ((math == MATH_X6 || math == MATH_BF16) && a.nw_max <= 16 && team_blocks(a.n_wtiles)) return launch_edge_fwd_team(a, math, st);
     if (math == MATH_BF16) {
 #ifdef SPWGNN_DIAG   // 1: A rows from 8 cached blocks; 3: U, V rows of the tile's first node (wrong results)
         static const int bdbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;

@@ -598,6 +598,382 @@ __global__ __launch_bounds__(256, 1) void k_node_bwd_team(NodeBwdArgs a) {
     }
 }
 
+// ---- edge side of one propagation step (k_edge_fwd_x6 for ≤ 16-node wave-tiles), team form ----
+// A workgroup of five waves takes one wave-tile; wave T owns output feature tile T of h2 (and its
+// receiver sums): per 32-edge block it builds and splits the whole h1 = relu(A + U[s] + V[r]) k-block
+// by k-block (the A operand, as k_edge_fwd_x6 does) and runs tile T's products with W2 fragments read
+// straight from the x6 image (L2; no 150 KB LDS fill). Products, their per-accumulator order, the
+// epilogue and the one-hot receiver sum of tile T are k_edge_fwd_x6's (mfma32_x6 / NodeSum16X6), so
+// H2s and both masks are bit-identical. Wave 0 writes the h1 > 0 words, wave T the h2 > 0 word of
+// tile T (wave 0 also the zero padding words 5-7).
+template <int NP, bool AB16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a) {
+    constexpr int PF = 2;   // A/U/V k-blocks in flight
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wt = blockIdx.x;
+    if (wt >= a.n_wtiles) return;
+    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    uint4 wf[10][NP];   // tile T's W2 fragments, all ten k-blocks
+#pragma unroll
+    for (int kb = 0; kb < 10; ++kb)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) wf[kb][p] = a.x_w2[((kb * 5 + T) * 3 + p) * 64 + lane];
+    const float b2 = a.b2[32 * T + i];
+    f32x4 nacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};   // NodeSum16X6 sub-tiles 2T, 2T+1
+    const int key = n0 + (lane & 15);
+    const int m1off = lane < 4 ? lane : kKhE + lane - 4;
+    struct KB { float4 a[2], u[2], v[2]; };
+    for (int bb = 0; bb < nb; ++bb) {
+        const int blk = fb + bb;
+        const int s = a.esrc[(int64_t)blk * 32 + i], d = a.edst[(int64_t)blk * 32 + i];
+        const bool valid = s >= 0;
+        const uint64_t vmask = __ballot(valid);
+        const float vf = valid ? 1.f : 0.f;
+        const int sc = valid ? s : n0, dc = valid ? d : n0;
+        const int64_t ai = (int64_t)blk * kCmBlk + h * 128 + i * 4;
+        const float4* U4 = reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128);
+        const float4* V4 = reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128);
+        auto ld = [&](int kb, KB& r) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int q = min(2 * kb + c, kKhE / 4 - 1);
+                if constexpr (AB16)
+                    r.a[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + ai + 256 * q));
+                else
+                    r.a[c] = *reinterpret_cast<const float4*>(a.A + ai + 256 * q);
+                r.u[c] = U4[64 * q];
+                r.v[c] = V4[64 * q];
+            }
+        };
+        uint32_t* mrow = (a.mask1 && T == 0) ? a.mask1 + (int64_t)blk * kLdE : nullptr;
+        KB ring[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) ld(k, ring[k]);
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % PF];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
+                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
+                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
+                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
+            }
+            if (kb + PF < 10) ld(kb + PF, cr);
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            if (mrow) {   // h1 > 0 bits of the block's real chunks (as k_edge_fwd_x6)
+                uint64_t bal[2][4];
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) bal[c][f] = __ballot(xv[4 * c + f] > 0.f);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int q = 2 * kb + c;
+                    if (q < kKhE / 4) {
+                        uint32_t v[8];
+                        int ln[8];
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) {
+                            v[2 * f] = (uint32_t)bal[c][f];
+                            ln[2 * f] = f;
+                            v[2 * f + 1] = (uint32_t)(bal[c][f] >> 32);
+                            ln[2 * f + 1] = 4 + f;
+                        }
+                        const uint32_t stg = writelane8_batched(0u, v, ln);
+                        if (lane < 8) mrow[m1off + 4 * q] = stg;
+                    }
+                }
+            }
+            bf16x8 ap[3], bp[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
+            acc = mfma32_x6<NP>(ap, bp, acc);
+        }
+        if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;   // features 152..159 (padding)
+        const uint32_t vh = (uint32_t)vmask >> (4 * h);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float v = relu(acc[r] + b2);
+            if (T == 4 && i == kDegCol - 128) v = 1.f;   // degree column (multiplies b3)
+            acc[r] = mask_bit(v, vh, rho(r, 0));
+        }
+        if (a.mask2) {   // h2 > 0 bits of tile T: word m2_pos(edge, T) = 8·edge + T, in register edge >> 3
+            uint32_t mw2[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += 8) {
+                uint64_t bal[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) bal[r] = __ballot(acc[r0 + r] > 0.f);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int e0 = rho(r0 + r, 0), e1 = rho(r0 + r, 1);
+                    mw2[e0 >> 3] = writelane((uint32_t)bal[r], 8 * (e0 & 7) + T, mw2[e0 >> 3]);
+                    mw2[e1 >> 3] = writelane((uint32_t)(bal[r] >> 32), 8 * (e1 & 7) + T, mw2[e1 >> 3]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            uint32_t* m2row = a.mask2 + (int64_t)blk * kM2Blk;
+            const int t7 = lane & 7;
+            if (t7 == T || (T == 0 && t7 >= 5))
+#pragma unroll
+                for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = t7 == T ? mw2[k] : 0u;
+        }
+        // receiver sum of tile T (NodeSum16X6::add for t = T)
+        {
+            const int g = lane >> 4;
+            uint32_t oh[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                uint32_t w = 0u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int e = 2 * m + q, base = 8 * (e >> 2) + (e & 3);
+                    const int d0 = __builtin_amdgcn_readlane(d, base), d1 = __builtin_amdgcn_readlane(d, base + 16);
+                    const int d2 = __builtin_amdgcn_readlane(d, base + 4), d3 = __builtin_amdgcn_readlane(d, base + 20);
+                    const int dn = g == 0 ? d0 : g == 1 ? d1 : g == 2 ? d2 : d3;
+                    w |= (dn == key ? 0x3F80u : 0u) << (16 * q);
+                }
+                oh[m] = w;
+            }
+            const bf16x8 ao = as_bf16x8(make_uint4(oh[0], oh[1], oh[2], oh[3]));
+            uint32_t P[2][3][4];
+#pragma unroll
+            for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    split2(acc[8 * sh + 2 * m], acc[8 * sh + 2 * m + 1], P[sh][0][m], P[sh][1][m], P[sh][2][m]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(P[0][p][m], P[1][p][m], false, false);
+                    P[0][p][m] = r[0];
+                    P[1][p][m] = r[1];
+                }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int p = NP - 1; p >= 0; --p)
+                    nacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        ao, as_bf16x8(make_uint4(P[u][p][0], P[u][p][1], P[u][p][2], P[u][p][3])), nacc[u], 0, 0, 0);
+        }
+    }
+    // H2s rows of tile T (NodeSum16X6::store for sub-tiles 2T, 2T+1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int node = 4 * (lane >> 4) + r;
+        if (node < nn) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int f = 32 * T + 16 * u + (lane & 15);
+                if (f < 2 * kKhE) a.H2s[cm_index<kKhE>(n0 + node, f)] = nacc[u][r];
+            }
+        }
+    }
+}
+
+// ---- edge side of one backward step (k_edge_bwd_x6 without dA: x6/bf16 rebuild it), team form ----
+// Five waves per wave-tile; wave T owns feature tile T of dh1 = dh2pre·W2ᵀ: every wave builds the
+// whole dh2pre = G3[receiver] ⊙ [h2 > 0] operand k-block by k-block, multiplies it by its tile's W2ᵀ
+// fragments (from the x6 image in L2), masks with [h1 > 0] and runs tile T's one-hot receiver/sender
+// sums — k_edge_bwd_x6's products in its per-accumulator order, so dU and dV are bit-identical.
+template <int NP>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_edge_bwd_team(EdgeBwdArgs a) {
+    constexpr int PF = 2;
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wt = blockIdx.x;
+    if (wt >= a.n_wtiles) return;
+    const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
+    const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    uint4 wf[10][NP];   // tile T's W2ᵀ fragments
+#pragma unroll
+    for (int kb = 0; kb < 10; ++kb)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) wf[kb][p] = a.x_w2t[((kb * 5 + T) * 3 + p) * 64 + lane];
+    const int key = i < 16 ? n0 + i : n0 + i - 16;   // one-hot rows: receivers, then senders
+    f32x16 nacc = zero16();
+    struct KB { float4 g[2]; };
+    for (int bb = 0; bb < nb; ++bb) {
+        const int blk = fb + bb;
+        const int64_t e = (int64_t)blk * 32 + i;
+        const int d = a.edst[e], s_ = a.esrc[e];
+        const bool valid = d >= 0;
+        uint32_t w[5];
+        load_m2(a.mask2 + (int64_t)blk * kM2Blk, i, w);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) w[t] = valid ? w[t] : 0u;
+        const uint32_t m1w = a.mask1[(int64_t)blk * kLdE + i + 32 * T];
+        const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
+                                    : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
+        const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
+        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + cm_index<kKhE>(valid ? d : n0, 0) + h * 128);
+        auto ld = [&](int kb, KB& r) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
+        };
+        KB ring[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) ld(k, ring[k]);
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % PF];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int q = 2 * kb + c;
+                const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
+                xv[4 * c + 0] = mask_bit(cr.g[c].x, bits, 0);
+                xv[4 * c + 1] = mask_bit(cr.g[c].y, bits, 1);
+                xv[4 * c + 2] = mask_bit(cr.g[c].z, bits, 2);
+                xv[4 * c + 3] = mask_bit(cr.g[c].w, bits, 3);
+            }
+            if (kb + PF < 10) ld(kb + PF, cr);
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            bf16x8 ap[3], bp[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
+            acc = mfma32_x6<NP>(ap, bp, acc);
+        }
+        // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32T+i, rows = edges rho(r,h))
+        const uint32_t mh = m1w >> (4 * h);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = mask_bit(acc[r], mh, rho(r, 0));
+#pragma unroll
+        for (int sh = 0; sh < 2; ++sh) {
+            uint32_t oh[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                uint32_t wv = 0u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int ee = 2 * m + q;
+                    const int d0 = __builtin_amdgcn_readlane(d, rho(8 * sh + ee, 0));
+                    const int d1 = __builtin_amdgcn_readlane(d, rho(8 * sh + ee, 1));
+                    const int s0 = __builtin_amdgcn_readlane(s_, rho(8 * sh + ee, 0));
+                    const int s1 = __builtin_amdgcn_readlane(s_, rho(8 * sh + ee, 1));
+                    const int node = i < 16 ? (h ? d1 : d0) : (h ? s1 : s0);
+                    wv |= (node == key ? 0x3F80u : 0u) << (16 * q);
+                }
+                oh[m] = wv;
+            }
+            const bf16x8 ao = as_bf16x8(make_uint4(oh[0], oh[1], oh[2], oh[3]));
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(acc[8 * sh + 2 * m], acc[8 * sh + 2 * m + 1], hw[m], mw[m], lw[m]);
+            if constexpr (NP == 3) {
+                nacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3])), nacc, 0, 0, 0);
+                nacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3])), nacc, 0, 0, 0);
+            }
+            nacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3])), nacc, 0, 0, 0);
+        }
+    }
+    // nacc reg r = row rho(r,h): rows 0..15 receiver nodes (dV), 16..31 sender nodes (dU)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = rho(r, h);
+        const int node = row & 15;
+        if (node < nn && 32 * T + i < 2 * kKhE) {
+            float* o = row < 16 ? a.dV : a.dU;
+            o[cm_index<kKhE>(n0 + node, 32 * T + i)] = nacc[r];
+        }
+    }
+}
+
+// ---- dA = Σ_s dh1pre_s (k_dA_x6), team form: five waves per 32-edge block, wave T owns feature
+// tile T; the same products, per-accumulator order and step order (S−1 first) as k_dA_x6.
+template <int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_dA_team(DaArgs a) {
+    constexpr int PF = 2;
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int blk = blockIdx.x;
+    if (blk >= a.n_eblocks) return;
+    uint4 wf[10][NP];   // tile T's W2ᵀ fragments
+#pragma unroll
+    for (int kb = 0; kb < 10; ++kb)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) wf[kb][p] = a.x_w2t[((kb * 5 + T) * 3 + p) * 64 + lane];
+    const int d = a.edst[(int64_t)blk * 32 + i];
+    const bool valid = d >= 0;
+    f32x16 dacc = zero16();
+    struct KB { float4 g[2]; };
+    for (int s = a.S - 1; s >= 0; --s) {
+        uint32_t w[5];
+        load_m2(a.mask2 + s * a.m2_step + (int64_t)blk * kM2Blk, i, w);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) w[t] = valid ? w[t] : 0u;
+        const uint32_t m1w = a.mask1[s * a.m1_step + (int64_t)blk * kLdE + i + 32 * T];
+        const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
+                                    : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
+        const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
+        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + s * a.g3_step + cm_index<kKhE>(valid ? d : 0, 0) + h * 128);
+        auto ld = [&](int kb, KB& r) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
+        };
+        KB ring[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) ld(k, ring[k]);
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % PF];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int q = 2 * kb + c;
+                const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
+                xv[4 * c + 0] = mask_bit(cr.g[c].x, bits, 0);
+                xv[4 * c + 1] = mask_bit(cr.g[c].y, bits, 1);
+                xv[4 * c + 2] = mask_bit(cr.g[c].z, bits, 2);
+                xv[4 * c + 3] = mask_bit(cr.g[c].w, bits, 3);
+            }
+            if (kb + PF < 10) ld(kb + PF, cr);
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            bf16x8 ap[3], bp[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
+            acc = mfma32_x6<NP>(ap, bp, acc);
+        }
+        const uint32_t mh = m1w >> (4 * h);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dacc[r] += mask_bit(acc[r], mh, rho(r, 0));
+    }
+    if constexpr (B16) {   // bf16 math: dA feeds MFMA operands only (§3g)
+        __bf16* dArow = reinterpret_cast<__bf16*>(a.dA) + (int64_t)blk * 32 * kLdE + i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * T] = (__bf16)dacc[r];
+    } else {
+        float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * T] = dacc[r];
+    }
+}
+
 bool team_blocks(int n_blocks) {
 #ifdef SPWGNN_DIAG   // A/B: SPWGNN_NO_TEAM=1 keeps the one-wave-per-block kernels at every size
     static const bool off = getenv("SPWGNN_NO_TEAM") && atoi(getenv("SPWGNN_NO_TEAM"));
@@ -606,6 +982,35 @@ bool team_blocks(int n_blocks) {
     return n_blocks > 0 && n_blocks <= kTeamMaxBlocks;
 }
 
+hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st) {
+    if (a.nw_max > 16) return hipErrorInvalidValue;
+    const dim3 g(a.n_wtiles), b(64 * kTeamEdge);
+    if (math == MATH_BF16) {
+        if (a.a_b16) hipLaunchKernelGGL((k_edge_fwd_team<1, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_edge_fwd_team<1, false>), g, b, 0, st, a);
+    } else if (math == MATH_X6 && !a.a_b16) {
+        hipLaunchKernelGGL((k_edge_fwd_team<3, false>), g, b, 0, st, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_edge_bwd_team(const EdgeBwdArgs& a, int math, hipStream_t st) {
+    if (a.nw_max > 16 || !a.no_dA) return hipErrorInvalidValue;
+    const dim3 g(a.n_wtiles), b(64 * kTeamEdge);
+    if (math == MATH_BF16) hipLaunchKernelGGL((k_edge_bwd_team<1>), g, b, 0, st, a);
+    else if (math == MATH_X6) hipLaunchKernelGGL((k_edge_bwd_team<3>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_dA_team(const DaArgs& a, int math, hipStream_t st) {
+    const dim3 g(a.n_eblocks), b(64 * kTeamEdge);
+    if (math == MATH_BF16 && a.b16) hipLaunchKernelGGL((k_dA_team<1, true>), g, b, 0, st, a);
+    else if (math == MATH_BF16) hipLaunchKernelGGL((k_dA_team<1, false>), g, b, 0, st, a);
+    else if (math == MATH_X6) hipLaunchKernelGGL((k_dA_team<3, false>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
 hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipStream_t st) {
     const dim3 g(a.n_eblocks), b(64 * kTeamEdge);
     if (math == MATH_BF16) {
