@@ -496,7 +496,8 @@ struct WgSpec {
 // Each weight gradient writes its per-chunk slabs into its own slot; the ordered chunk sums of all
 // of them run as one batched launch at the end of the backward (launch_wgrad_reduce_all).
 static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, float* grads, int math, hipStream_t st,
-                         ReduceBatch& rb, const Prof* prof = nullptr, WsBatch* wsb = nullptr) {
+                         ReduceBatch& rb, const Prof* prof = nullptr, WsBatch* wsb = nullptr,
+                         Pos3Batch* p3 = nullptr) {
     const Ws& w = c.w;
     if (g.rows <= 0) return SPWGNN_OK;
     if (rb.n >= kWgSlots) return SPWGNN_E_ARG;
@@ -597,7 +598,9 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>(pa.nblk, std::min<int64_t>(512, slot_chunks)));
         pa.blk_per_wg = (pa.nblk + wgs - 1) / wgs;
         chunks = (pa.nblk + pa.blk_per_wg - 1) / pa.blk_per_wg;
-        SPW_CHECK(launch_wgrad_pos3(pa, (int)chunks, node, (g.b16 & kB16Y) != 0, st));
+        if (!p3) return SPWGNN_E_ARG;
+        if (node) { p3->n = pa; p3->cn = (int)chunks; }
+        else { p3->e = pa; p3->ce = (int)chunks; p3->b16e = (g.b16 & kB16Y) != 0; }
     } else {
     // the x6 W2 gradient: one warp-specialized workgroup per CU over contiguous edge-block ranges
     const bool ws = g.recompute && math != MATH_F32 && (math == MATH_BF16 || !getenv_flag("SPWGNN_W2G_OLD"));
@@ -827,13 +830,14 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     ReduceBatch rb{};
     WsBatch wsb{};
     WsBatch* const wsp = getenv_flag("SPWGNN_WS_UNBATCHED") ? nullptr : &wsb;   // A/B: one launch per gradient
+    Pos3Batch p3{};
     {   // rm.0: X = [d | 1]
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
         g.b16 = b16 ? kB16Y : 0;   // Y = dz1
         if (z1_rebuilt(r)) g.xd = reinterpret_cast<const float2*>(c.f(w.ed));   // k_wgrad_pos3 reads d
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
@@ -845,12 +849,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.b0 = c.pk(PB_RM0);
         }
         g.b16 = b16 ? kB16Y : 0;   // X rebuilt from d; Y = dz2
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     const int b16xy = b16 ? (kB16X | kB16Y) : 0;
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e; }
+    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e; }
+    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e; }
+    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e; }
     {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
         // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
@@ -858,7 +862,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
         g.b16 = b16 ? kB16A : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {
@@ -871,28 +875,28 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // omp.0 rows 100..199 (effect part)
         WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
         g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     if (wsp) ws_group(wsp, grp0, wsb.n - grp0);
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
         WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
@@ -902,18 +906,18 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.rows = nN;
             g.y_stride = 0;
         }
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
@@ -924,8 +928,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.b0 = c.pk(PB_OM0);
         }
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp))) return e;
+        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
+    SPW_CHECK(launch_wgrad_pos3(p3, st));
     if (wsb.n > 0) {
         SPW_CHECK(prof.before(SPWGNN_K_WGRAD_WS));
         SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st));

@@ -324,7 +324,12 @@ struct Pos3Args {
     float* slab;             // [chunks][32][NYP]
     int64_t nblk, blk_per_wg, count;
 };
-hipError_t launch_wgrad_pos3(const Pos3Args& a, int chunks, bool node, bool b16, hipStream_t st);
+struct Pos3Batch {          // the backward's two k_wgrad_pos3 gradients, one launch
+    Pos3Args e, n;         // rm.0 (edge rows), om.0 (node rows)
+    int ce, cn;            // their workgroups (0: not queued)
+    int b16e;              // rm.0's Y (dz1) stored as bf16
+};
+hipError_t launch_wgrad_pos3(const Pos3Batch& p, hipStream_t st);
 hipError_t launch_bce(const BceArgs& a, hipStream_t st);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank, hipStream_t st);
@@ -339,6 +344,7 @@ hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_bwd_team(const EdgeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_dA_team(const DaArgs& a, int math, hipStream_t st);
+hipError_t launch_enc_node_bwd_team(const EncNodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_bwd_team(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipStream_t st);

@@ -1103,6 +1103,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
 hipError_t launch_enc_node_bwd(const EncNodeBwdArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
     if (math != MATH_F32 && a.wo1ct && a.x_wo1ct && a.x_om1t) {
+        if (team_blocks(waves)) return launch_enc_node_bwd_team(a, math, st);   // small batches
         if (math == MATH_BF16) hipLaunchKernelGGL((k_enc_node_bwd_x6<1, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((k_enc_node_bwd_x6<3, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();

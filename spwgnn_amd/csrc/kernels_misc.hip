@@ -1388,11 +1388,11 @@ __global__ void k_tower_readout(const float* __restrict__ z, const int32_t* __re
 // d1 / y, w and the bias row) go to this workgroup's chunk for k_wgrad_reduce_all. Pieces past the
 // row's last one (qh ≥ NQH) re-read the last piece and are never written out.
 template <int KH, bool NODE, bool B16>
-__global__ __launch_bounds__(256) void k_wgrad_pos3(Pos3Args a) {
+__device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid) {
     constexpr int NQH = KH / 2, NK = (NQH + 7) / 8, NYP = KH == kKhE ? 160 : 128, BLK = KH * 64;
     constexpr int UB = 4;   // blocks whose loads are issued together (the loop is latency-bound)
     const int tid = threadIdx.x, i = tid & 31, g = tid >> 5;
-    const int64_t b0 = (int64_t)blockIdx.x * a.blk_per_wg, b1 = min(a.nblk, b0 + a.blk_per_wg);
+    const int64_t b0 = (int64_t)bid * a.blk_per_wg, b1 = min(a.nblk, b0 + a.blk_per_wg);
     float4 s0[NK], s1[NK], s2[NK];
 #pragma unroll
     for (int k = 0; k < NK; ++k) s0[k] = s1[k] = s2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1443,7 +1443,7 @@ __global__ __launch_bounds__(256) void k_wgrad_pos3(Pos3Args a) {
         for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
         return v;
     };
-    float* out = a.slab + (int64_t)blockIdx.x * 32 * NYP;
+    float* out = a.slab + (int64_t)bid * 32 * NYP;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
         const int qh = g + 8 * k;
@@ -1459,13 +1459,17 @@ __global__ __launch_bounds__(256) void k_wgrad_pos3(Pos3Args a) {
         }
     }
 }
-hipError_t launch_wgrad_pos3(const Pos3Args& a, int chunks, bool node, bool b16, hipStream_t st) {
-    if (chunks <= 0) return hipSuccess;
-    const dim3 g(chunks), b(256);
-    if (node && !b16) hipLaunchKernelGGL((k_wgrad_pos3<kKhN, true, false>), g, b, 0, st, a);
-    else if (!node && !b16) hipLaunchKernelGGL((k_wgrad_pos3<kKhE, false, false>), g, b, 0, st, a);
-    else if (!node && b16) hipLaunchKernelGGL((k_wgrad_pos3<kKhE, false, true>), g, b, 0, st, a);
-    else return hipErrorInvalidValue;
+// rm.0 (edge rows) and om.0 (node rows) in one launch: workgroups [0, ce) take the edge job
+template <bool B16E>
+__global__ __launch_bounds__(256) void k_wgrad_pos3(Pos3Args e, Pos3Args n, int ce) {
+    if ((int)blockIdx.x < ce) wgrad_pos3_body<kKhE, false, B16E>(e, blockIdx.x);
+    else wgrad_pos3_body<kKhN, true, false>(n, blockIdx.x - ce);
+}
+hipError_t launch_wgrad_pos3(const Pos3Batch& p, hipStream_t st) {
+    if (p.ce + p.cn <= 0) return hipSuccess;
+    const dim3 g(p.ce + p.cn), b(256);
+    if (p.b16e) hipLaunchKernelGGL((k_wgrad_pos3<true>), g, b, 0, st, p.e, p.n, p.ce);
+    else hipLaunchKernelGGL((k_wgrad_pos3<false>), g, b, 0, st, p.e, p.n, p.ce);
     return hipGetLastError();
 }
 

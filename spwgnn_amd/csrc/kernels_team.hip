@@ -974,6 +974,60 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_dA_team(DaArgs a) {
     }
 }
 
+// ---- object-encoder backward (k_enc_node_bwd_x6), team form: four waves per 32-node block, wave T
+// owns feature tile T of dc_o = (Σ_s do1_s)·Wo1cᵀ and of the om.1ᵀ product; the layer input is
+// exchanged through LDS in its split C layout. Same products and order: bit-identical.
+template <int NP>
+__global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
+    __shared__ uint4 act_s[4 * 2 * NP * 64];
+    const TeamAct<4, NP> act{act_s};
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = blockIdx.x;
+    const int n = nb * 32 + j;
+    const bool valid = n < a.n_nodes;
+    const int64_t bN = (int64_t)nb * kCmBlkN;
+    TeamFrags<7, NP> F;
+    F.load(a.x_wo1ct, 4, T, lane);
+    // Σ_s do1_s in backward step order S-1..0 (the Y of the Wo1c weight gradient), every tile
+    f32x16 E[4], Z[4];
+    load_cm<4>(a.do1 + (int64_t)(a.S - 1) * a.do1_step + bN, E, lane);
+    for (int s = a.S - 2; s >= 0; --s) {
+        load_cm<4>(a.do1 + (int64_t)s * a.do1_step + bN, Z, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) E[t] += Z[t];
+    }
+    {
+        f32x16 et = E[0];   // tile T (selected: a runtime index would put the array in scratch)
+#pragma unroll
+        for (int t = 1; t < 4; ++t)
+            if (T == t) et = E[t];
+        store_cm_tile<kKhN>(a.dco + bN, et, T, lane, valid);
+    }
+    f32x16 D = team_gemm(F, TeamRegs<4>{E}, [&](int kb) { F.load_kb(a.x_om1t, 4, T, lane, kb); });   // dc_o
+    const f32x16 C = load_cm_tile<kKhN>(a.co + bN, T, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) D[r] = C[r] > 0.f ? D[r] * a.scale : 0.f;
+    store_cm_tile<kKhN>(a.dzo2 + bN, D, T, lane, valid);
+    act.put(0, T, D, lane);
+    team_sync();
+    f32x16 G = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
+    f32x16 Zt;
+    if (a.zo1) {
+        Zt = load_cm_tile<kKhN>(a.zo1 + bN, T, lane);
+    } else {   // the forward's own first-layer arithmetic (k_enc_node_x6), not a stored row
+        const float4 p = reinterpret_cast<const float4*>(a.pos)[valid ? n : a.n_nodes - 1];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, 0) + 4 * h + 32 * T;
+            Zt[r] = relu(dense2(p.y, p.z, a.w_om0[f], a.w_om0[128 + f], a.b_om0[f]));
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) G[r] = Zt[r] > 0.f ? G[r] : 0.f;
+    store_cm_tile<kKhN>(a.dzo1 + bN, G, T, lane, valid);
+}
+
 bool team_blocks(int n_blocks) {
 #ifdef SPWGNN_DIAG   // A/B: SPWGNN_NO_TEAM=1 keeps the one-wave-per-block kernels at every size
     static const bool off = getenv("SPWGNN_NO_TEAM") && atoi(getenv("SPWGNN_NO_TEAM"));
@@ -1008,6 +1062,13 @@ hipError_t launch_dA_team(const DaArgs& a, int math, hipStream_t st) {
     if (math == MATH_BF16 && a.b16) hipLaunchKernelGGL((k_dA_team<1, true>), g, b, 0, st, a);
     else if (math == MATH_BF16) hipLaunchKernelGGL((k_dA_team<1, false>), g, b, 0, st, a);
     else if (math == MATH_X6) hipLaunchKernelGGL((k_dA_team<3, false>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_enc_node_bwd_team(const EncNodeBwdArgs& a, int math, hipStream_t st) {
+    const dim3 g((a.n_nodes + 31) / 32), b(256);
+    if (math == MATH_BF16) hipLaunchKernelGGL((k_enc_node_bwd_team<1>), g, b, 0, st, a);
+    else if (math == MATH_X6) hipLaunchKernelGGL((k_enc_node_bwd_team<3>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
