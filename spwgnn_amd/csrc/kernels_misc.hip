@@ -434,19 +434,28 @@ template <int W>
 struct X6Img {
     static constexpr int ROWB = W * 2, PART = 32 * ROWB;
     __device__ static __forceinline__ int sigma(int r) { return (ROWB % 256 == 0) ? (r & 7) : ((r >> 2) & 1); }
-    // within a unit the four 8-byte granules are XOR-permuted by row & 3: the 32 rows one wave's
-    // staging store touches then spread over all 32 store banks (2-way, the minimum for b64)
-    // instead of 4 of them; a row's unit still holds the same 8 dwords, so the transposed reads
-    // stay conflict-free
+    // Within a unit the four 8-byte granules are XOR-permuted by gsw(row). The staging store
+    // (ds_write_b64: groups of 16 lanes = 16 consecutive rows of one 4-column group, banks mod 32)
+    // is conflict-free when (row pitch, unit swizzle, granule swizzle) give 16 distinct 8-byte slots
+    // mod 32 banks: at W = 128 (pitch ≡ 0) the unit swizzle contributes row bits 0-1, so the granules
+    // take bits 2-3; at W = 160 (pitch ≡ 16 dwords) the pitch gives bit 0 and the unit swizzle bit 2,
+    // so the granules take bits 1 and 3. (Was `row & 3` at every width: 4-way / 2-way store
+    // conflicts, SQ_LDS_BANK_CONFLICT in profiles/r02_pmc_sq.json.) The granule permutation stays
+    // inside a unit, so the transposed reads keep their 64 distinct banks.
+    __device__ static __forceinline__ int gsw(int r) {
+        if constexpr (W == 32) return r & 3;
+        else if constexpr (ROWB % 256 == 0) return (r >> 2) & 3;
+        else return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+    }
     __device__ static __forceinline__ int woff(int rr, int c4) {
-        return rr * ROWB + 32 * ((c4 >> 2) ^ sigma(rr)) + 8 * ((c4 & 3) ^ (rr & 3));
+        return rr * ROWB + 32 * ((c4 >> 2) ^ sigma(rr)) + 8 * ((c4 & 3) ^ gsw(rr));
     }
     // lane's read offset for 16-column tile t: group g = lane>>4 reads rows 4g..4g+3 (elements 0-3)
     // and 16+4g..16+4g+3 (elements 4-7, at + 16·ROWB) — the k order of the 16x16x32 operand, the
-    // same for both operands of a product
+    // same for both operands of a product (row + 16 has the same sigma and gsw as row)
     __device__ static __forceinline__ int roff(int lane, int t) {
         const int li = lane & 15, row = 4 * (lane >> 4) + (li >> 2);
-        return row * ROWB + 32 * (t ^ sigma(row)) + 8 * ((li & 3) ^ (row & 3));
+        return row * ROWB + 32 * (t ^ sigma(row)) + 8 * ((li & 3) ^ gsw(row));
     }
     // NP = 1 (bf16 math): the h part only
     template <int NP = 3>
