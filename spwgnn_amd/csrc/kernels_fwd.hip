@@ -907,11 +907,17 @@ struct NodeSum16X6 {
 #ifndef SPWGNN_EFWD_PF_B16
 #define SPWGNN_EFWD_PF_B16 2
 #endif
-template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false>   // AB16: A stored as bf16 (§3g)
-__global__ __launch_bounds__(NW16 ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu(NW16 ? 2 : 1, NW16 ? 2 : 1)))
+#ifndef SPWGNN_EFWD32_PF
+#define SPWGNN_EFWD32_PF 1
+#endif
+// W8 (≤ 32-node tiles): 8 waves at two per SIMD (256 registers: the 32-node sum and a short ring)
+// instead of 4 at one per SIMD with a 5-k-block ring
+template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false, bool W8 = false>   // AB16: A stored as bf16 (§3g)
+__global__ __launch_bounds__((NW16 || W8) ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu((NW16 || W8) ? 2 : 1, (NW16 || W8) ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     // bf16 math (NP = 1): a k-block is 5 MFMAs, too short to cover a load one k-block ahead
-    constexpr int kWaves = NW16 ? 8 : 4, kX6Pf = NW16 ? (NP == 1 ? SPWGNN_EFWD_PF_B16 : SPWGNN_EFWD_PF) : 5;
+    constexpr int kWaves = (NW16 || W8) ? 8 : 4;
+    constexpr int kX6Pf = NW16 ? (NP == 1 ? SPWGNN_EFWD_PF_B16 : SPWGNN_EFWD_PF) : (W8 ? SPWGNN_EFWD32_PF : 5);
     static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
     __shared__ uint4 wl[DBG == 2 ? 64 : 50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
     if constexpr (DBG != 2) {
@@ -1194,8 +1200,9 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
 #endif
         else if (a.nw_max <= 16)
             hipLaunchKernelGGL(k_edge_fwd_x6<true>, dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
-        else
-            hipLaunchKernelGGL(k_edge_fwd_x6<false>, dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);
+        else   // ≤ 32-node tiles: two waves per SIMD (config 5: 37.5 -> 34.4 ms per forward, A/B on one box;
+               // 36 spilled registers, an inference-only instantiation without the mask code spills 612)
+            hipLaunchKernelGGL((k_edge_fwd_x6<false, 0, 3, false, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         return hipGetLastError();
     }
     if (a.nw_max <= 16)
