@@ -313,7 +313,7 @@ def step_hbm(config: int, ms_per_step: float, math: str, workload: str):
             return None
         # one Adam per training step; one weight prep per forward (inference replays)
         steps = meta.get("steps") or d.get("k_adam", {}).get("dispatches", 0) or \
-            d.get("k_prep_weights", {}).get("dispatches", 0)
+            d.get("k_prep", {}).get("dispatches", 0) or d.get("k_prep_weights", {}).get("dispatches", 0)
         if not steps:
             return None
         tot = sum(v.get("hbm_read_bytes", 0.0) * v["dispatches"] + v.get("hbm_write_bytes", 0.0) * v["dispatches"]

@@ -170,6 +170,7 @@ static void build_packs(const Ws& w, PrepArgs& pa) {
         // A operands of the transposed-orientation MLP chains are k4-blocked (gemm_blocks.h);
         // W2/W2ᵀ (LDS images built by the edge kernels), rm.0/om.0 and the biases stay row-major
         d.k4 = !(pid == PK_W2 || pid == PK_W2T || pid == PK_RM0 || pid == PK_OM0 || pack_rows(pid) == 1);
+        d.bias_row = -1;
         pa.desc[pid] = d;
     };
     // forward [in][out]
@@ -181,7 +182,9 @@ static void build_packs(const Ws& w, PrepArgs& pa) {
     mk(PK_W1B, T_RMP0K, 100, 150, 150, 0, 0);
     mk(PK_W1C, T_RMP0K, 100, 150, 250, 0, 0);
     mk(PK_W2, T_RMP1K, 150, 150, 0, 0, 0);
-    mk(PK_W3A, T_RMP2K, 150, 100, 0, 0, 0);   // row 150 (bias) patched below
+    mk(PK_W3A, T_RMP2K, 150, 100, 0, 0, 0);
+    pa.desc[PK_W3A].bias_row = 150;             // row 150 = rmp.2 bias (the degree column multiplies it)
+    pa.desc[PK_W3A].bias_off = T(T_RMP2B).offset;
     mk(PK_WO1C, T_OMP0K, 100, 100, 0, 0, 0);
     mk(PK_WO1A, T_OMP0K, 100, 100, 100, 0, 0);
     mk(PK_WO1P, T_OMP0K, 100, 100, 200, 0, 0);
@@ -307,28 +310,24 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     pa.params = params;
     pa.pk = c.f(w.pk);
     build_packs(w, pa);
-    SPW_CHECK(launch_prep_weights(pa, st));
-    // rmp.2 bias → row 150 of PK_W3A (one small copy; stream-ordered, capturable)
-    // (k4-blocked: element (150, c) sits at ((150/4)·128 + c)·4 + 150%4, a 16-byte stride)
-    SPW_CHECK(hipMemcpy2DAsync(c.f(w.pk + w.ps.off[PK_W3A] + ((150 / 4) * kLdN) * 4 + 150 % 4), 4 * sizeof(float),
-                               params + param_table().t[T_RMP2B].offset, sizeof(float), sizeof(float), 100,
-                               hipMemcpyDeviceToDevice, st));
-    if (r->math != MATH_F32) {   // after the W3A bias row: the images are split from the packs
-        PrepX6Args xa{};
+    // packs and, for the split-bf16 maths, the x6 images: one launch (one of the ≈ 20 of a small step)
+    PrepX6Args xa{};
+    if (r->math != MATH_F32) {
         xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
         for (int id = 0; id < X6_COUNT; ++id) {
             const X6Spec& sp = kX6Specs[id];
             X6Desc& d = xa.d[id];
-            d.src = c.pk(sp.pack);
-            d.cols = pack_cols(sp.pack);
-            d.k4 = pa.desc[sp.pack].k4;
+            d.pack = sp.pack;
             d.nt_out = sp.nt_out;
             d.nkb = sp.nkb;
             d.kh = sp.kh;
             d.dst = w.x6off[id];
+            // an image reads pack elements (k < rows, col < cols) only
+            if ((sp.kh ? 2 * sp.kh : 16 * sp.nkb) > pack_rows(sp.pack) || 32 * sp.nt_out > pack_cols(sp.pack))
+                return SPWGNN_E_SHAPE;
         }
-        SPW_CHECK(launch_prep_x6(xa, st));
     }
+    SPW_CHECK(launch_prep(pa, r->math != MATH_F32 ? &xa : nullptr, st));
     const bool drop = r->training && r->dropout > 0.f;
     const uint32_t thresh = (uint32_t)std::min(4294967295.0, std::floor((double)r->dropout * 4294967296.0));
     const float scale = drop ? 1.0f / (1.0f - r->dropout) : 1.0f;

@@ -205,7 +205,7 @@ __host__ __device__ __forceinline__ bool drop_keep(uint32_t rowkey, uint32_t fea
 }
 
 // ---------------------------------------------------------------------------------------------
-// Packed (zero-padded) weight copies built by k_prep_weights at the start of every call.
+// Packed (zero-padded) weight copies built by k_prep at the start of every call.
 enum PackId : int {
     PK_RM1 = 0, PK_RM2, PK_RM3, PK_W1A,       // [160][160] [in][out]
     PK_OM1,                                    // [128][128]

@@ -194,7 +194,7 @@ __device__ __forceinline__ void load_half(const float* __restrict__ row_plus_khh
 }
 
 // ---- transposed orientation: out[t] += Wᵀ·in with the [K][N] weight as a k4-blocked image
-// W4[((k>>2)·N + col)·4 + (k&3)] (built by k_prep_weights). The A operand of lane (i, h) at
+// W4[((k>>2)·N + col)·4 + (k&3)] (built by k_prep). The A operand of lane (i, h) at
 // k-step kk of input tile tp is W[rho(kk,h) + 32tp][32t + i]; k-steps 4g..4g+3 are the 4
 // consecutive features 8g + 4h + 0..3 — one 16-byte load per tile per 4 MFMAs, and the 32 lanes
 // of a half read 512 contiguous bytes. (One dword load per MFMA caps the matrix pipe near 50 %;
@@ -378,7 +378,7 @@ constexpr int kX6Ring = 3;
 // ---- transposed orientation in split-bf16 math (x6), NC column tiles of 32 rows per wave:
 // out[c][T] += Wᵀ·B[c] over NKB k-blocks of 16. getb(c, kb, v) supplies the 8 fp32 B values of
 // lane (j, h) for k-block kb (split into three bf16 parts here, once per k-block); the weight image
-// (k_prep_x6) holds, per step u = kb·NT_OUT + T, the three matching A-operand parts of lane (i, h),
+// (k_prep) holds, per step u = kb·NT_OUT + T, the three matching A-operand parts of lane (i, h),
 // 16 bytes each: [u][part][lane] uint4. Steps stream through a D-deep ring of static slots (fully
 // unrolled; the loads of step u + D issue before step u's MFMAs).
 template <int NT_OUT, int NKB, int NC, int D = kX6Ring, int PARTS = 3, class GetB>

@@ -12,7 +12,8 @@ struct PackDesc {
     int32_t src_ld, src_row0;
     int32_t transpose, perm;
     int32_t k4;        // 1: k4-blocked image W4[((r>>2)·cols + c)·4 + (r&3)] (16-byte A-operand fragments)
-    int32_t pad0;
+    int32_t bias_row;  // ≥ 0: destination row filled from a bias vector (PK_W3A row 150 = rmp.2 bias)
+    int64_t bias_off;  // floats into the flat params of that bias vector
 };
 struct PrepArgs {
     const float* params;
@@ -20,7 +21,8 @@ struct PrepArgs {
     PackDesc desc[PK_COUNT];  // by value (kernel-argument memory): no host→device copy, capturable
 };
 
-// Split-bf16 (x6) operand images of the weights, built from the fp32 packs after k_prep_weights.
+// Split-bf16 (x6) operand images of the weights, built in the same launch as the fp32 packs (k_prep)
+// from the pack elements they hold (pack_elem: the values are computed from the flat params, not read back).
 // Transposed-orientation A operands of tgemm_x6: [step u = kb·nt_out + T][part][lane] uint4 (8 bf16),
 // element e of lane (i, h) = W[k(kb, e, h)][32T + i] with
 //   kh == 0 (chain: B is a C layout)          k = 16kb + 8(e>>2) + 4h + (e&3)
@@ -50,10 +52,9 @@ constexpr X6Spec kX6Specs[X6_COUNT] = {
     {X6_OM1T, PK_OM1T, 4, 7, 0},
 };
 struct X6Desc {
-    const float* src;   // fp32 pack [rows][cols] (k4-blocked if k4)
-    int32_t cols, k4;
+    int32_t pack;       // source fp32 pack (PackId): element (k, col) of it
     int32_t nt_out, nkb;
-    int32_t kh, pad0;
+    int32_t kh;
     int64_t dst;        // uint4 offset into the image buffer
 };
 struct PrepX6Args {
@@ -294,9 +295,9 @@ struct AdamArgs {
 };
 
 // Host launchers (defined next to their kernels; each returns hipGetLastError()).
-hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st);
+// packs and (x: non-null) the x6 images in one launch
+hipError_t launch_prep(const PrepArgs& a, const PrepX6Args* x, hipStream_t st);
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st);
-hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st);
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st);

@@ -1,6 +1,6 @@
 // Forward kernels of the propagation network (Networks.py:31-96) for gfx950.
 //
-//   k_prep_weights   zero-padded / transposed / permuted copies of the 22 Keras tensors
+//   k_prep           zero-padded / transposed / permuted copies of the 22 Keras tensors + x6 images
 //   k_enc_node       om encoder (Networks.py:76,78) + P0 copy + first U/V projections
 //   k_enc_edge       rm encoder (Networks.py:75,77) + step-invariant part of rmp layer 1
 //   k_edge_fwd       per step: h1 = relu(A + U[s] + V[r]) → h2 = relu(h1·W2 + b2) → receiver
@@ -14,33 +14,40 @@
 namespace spw {
 
 // ------------------------------------------------------------------------------------------------
-__global__ void k_prep_weights(PrepArgs a) {
-    const int id = blockIdx.y;
-    const PackDesc& d = a.desc[id];
-    const int total = d.rows * d.cols;
-    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-        int r, c;
-        if (d.k4) {  // idx = ((r>>2)·cols + c)·4 + (r&3)
-            const int q = idx >> 2, kb = q / d.cols;
-            c = q - kb * d.cols;
-            r = 4 * kb + (idx & 3);
-        } else {
-            r = idx / d.cols;
-            c = idx - r * d.cols;
-        }
-        int sa = d.transpose ? c : r;  // source row (before row0)
-        int sb = d.transpose ? r : c;  // source col (before perm)
-        float v = 0.f;
-        if (d.perm) sb = wo2_perm(sb);
-        if (sa >= 0 && sa < d.src_rows && sb >= 0 && sb < d.src_cols)
-            v = a.params[d.src_off + (int64_t)(sa + d.src_row0) * d.src_ld + sb];
-        a.pk[d.dst_off + idx] = v;
-    }
+// Element (r, c) of pack d, straight from the flat Keras params (zero padding outside the source).
+__device__ __forceinline__ float pack_elem(const PackDesc& d, const float* __restrict__ params, int r, int c) {
+    if (r == d.bias_row) return c < d.src_cols ? params[d.bias_off + c] : 0.f;
+    const int sa = d.transpose ? c : r;                                   // source row (before row0)
+    const int sb = d.perm ? wo2_perm(d.transpose ? r : c) : (d.transpose ? r : c);   // source col
+    return (sa >= 0 && sa < d.src_rows && sb >= 0 && sb < d.src_cols)
+               ? params[d.src_off + (int64_t)(sa + d.src_row0) * d.src_ld + sb] : 0.f;
 }
 
-// x6 operand images (kernels.h X6Desc): one thread per (step, lane) splits its 8 weights once.
-__global__ void k_prep_x6(PrepX6Args a) {
-    const X6Desc& d = a.d[blockIdx.y];
+// One launch per call: rows blockIdx.y < PK_COUNT write the zero-padded / transposed / permuted
+// packs; the rows after them (x non-null) write the x6 operand images (kernels.h X6Desc), one thread
+// per (step, lane) splitting its 8 weights, taken from the same pack elements (pack_elem) so the
+// images need not wait for the packs.
+__global__ void k_prep(PrepArgs a, PrepX6Args x) {
+    const int id = blockIdx.y;
+    if (id < PK_COUNT) {
+        const PackDesc& d = a.desc[id];
+        const int total = d.rows * d.cols;
+        for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+            int r, c;
+            if (d.k4) {  // idx = ((r>>2)·cols + c)·4 + (r&3)
+                const int q = idx >> 2, kb = q / d.cols;
+                c = q - kb * d.cols;
+                r = 4 * kb + (idx & 3);
+            } else {
+                r = idx / d.cols;
+                c = idx - r * d.cols;
+            }
+            a.pk[d.dst_off + idx] = pack_elem(d, a.params, r, c);
+        }
+        return;
+    }
+    const X6Desc& d = x.d[id - PK_COUNT];
+    const PackDesc& pd = a.desc[d.pack];
     const int n = d.nkb * d.nt_out * 64;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
         const int lane = idx & 63, u = idx >> 6, kb = u / d.nt_out, T = u - kb * d.nt_out;
@@ -50,12 +57,12 @@ __global__ void k_prep_x6(PrepX6Args a) {
         for (int e = 0; e < 8; ++e) {
             const int k = d.kh ? d.kh * h + 8 * kb + e : 16 * kb + 8 * (e >> 2) + 4 * h + (e & 3);
             const bool in = !d.kh || 8 * kb + e < d.kh;
-            w[e] = in ? d.src[d.k4 ? ((k >> 2) * d.cols + col) * 4 + (k & 3) : k * d.cols + col] : 0.f;
+            w[e] = in ? pack_elem(pd, a.params, k, col) : 0.f;
         }
         uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) split2(w[2 * m], w[2 * m + 1], hw[m], mw[m], lw[m]);
-        uint4* o = a.img + d.dst + (int64_t)u * 3 * 64 + lane;
+        uint4* o = x.img + d.dst + (int64_t)u * 3 * 64 + lane;
         o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
         o[64] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
         o[128] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
@@ -1113,8 +1120,8 @@ int edge_grid(int n_wtiles, int waves) {
     return need < 1 ? 1 : (need < cus ? need : cus);
 }
 
-hipError_t launch_prep_weights(const PrepArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_prep_weights, dim3(32, PK_COUNT), dim3(256), 0, st, a);
+hipError_t launch_prep(const PrepArgs& a, const PrepX6Args* x, hipStream_t st) {
+    hipLaunchKernelGGL(k_prep, dim3(32, PK_COUNT + (x ? X6_COUNT : 0)), dim3(256), 0, st, a, x ? *x : PrepX6Args{});
     return hipGetLastError();
 }
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
@@ -1129,10 +1136,6 @@ hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_enc_node, dim3((waves + 3) / 4), dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-hipError_t launch_prep_x6(const PrepX6Args& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_prep_x6, dim3(16, X6_COUNT), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {

@@ -1288,6 +1288,9 @@ __global__ void k_wgrad_reduce_all(ReduceBatch rb) {
 // Keras binary_crossentropy (Networks.py:102): clip(ŷ, 1e-7, 1-1e-7) ≡ clamp(z, ±ln((1-ε)/ε)).
 constexpr float kLogitClip = 16.11809565f;
 
+// FINAL (a.blocks == 1, e.g. the reference's batch 32): the one workgroup also writes out3, the
+// same double-precision division k_bce_final does over its one partial — one launch instead of two.
+template <bool FINAL>
 __global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
     __shared__ float sl[256], sc[256];
     float ls = 0.f, cs = 0.f;
@@ -1311,8 +1314,14 @@ __global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        a.partial[2 * blockIdx.x] = sl[0];
-        a.partial[2 * blockIdx.x + 1] = sc[0];
+        if constexpr (FINAL) {
+            a.out3[0] = (float)((double)sl[0] / (double)a.n);
+            a.out3[1] = (float)(double)sc[0];
+            a.out3[2] = (float)a.n;
+        } else {
+            a.partial[2 * blockIdx.x] = sl[0];
+            a.partial[2 * blockIdx.x + 1] = sc[0];
+        }
     }
 }
 
@@ -1639,7 +1648,11 @@ hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_bce(const BceArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_bce_partial, dim3(a.blocks), dim3(256), 0, st, a);
+    if (a.blocks == 1) {
+        hipLaunchKernelGGL(k_bce_partial<true>, dim3(1), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_bce_partial<false>, dim3(a.blocks), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_bce_final, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError();
 }
