@@ -134,3 +134,26 @@ def test_shared_weight_ring_partial_workgroups(T, N):
     got = P.from_flat(grads)
     for name, r in g_ref.items():
         assert np.abs(got[name] - r).max() <= 1e-5 * np.abs(r).max() + 1e-7, name
+
+
+@pytest.mark.parametrize("math", ["x6", "f32", "bf16"])
+@pytest.mark.parametrize("n_towers", [8, 3000])   # team kernels / wide kernels
+def test_backward_writes_every_gradient(math, n_towers):
+    """Nothing of the caller's `grads` buffer survives a backward (api.hip run_backward clears it, then
+    the reductions write the 22 Keras tensors): a NaN-filled buffer must come out bitwise equal to a
+    zero-filled one. Without the clear, 739 floats stayed NaN (measured on the GPU)."""
+    params = O.random_params(seed=13)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(n_towers, 6, seed=21, fully_connected=False)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    flat = P.to_flat(params, device="cuda")
+    ws = E.Workspace("cuda")
+    run = E.RunConfig(3, training=True, math=math)
+    z = E.forward(flat, batch, run, ws)
+    _, dz = E.bce(z, torch.tensor(tgt.reshape(-1), device="cuda"), E.BceScratch("cuda"))
+    g_nan = torch.full_like(flat, float("nan"))
+    g_zero = torch.zeros_like(flat)
+    E.backward(flat, batch, run, ws, dz, grads=g_nan)
+    E.backward(flat, batch, run, ws, dz, grads=g_zero)
+    torch.cuda.synchronize()
+    assert torch.isfinite(g_nan).all(), int((~torch.isfinite(g_nan)).sum())
+    assert torch.equal(g_nan, g_zero)
