@@ -56,6 +56,11 @@ struct Ws {
 static constexpr int kMaxChunks = 256;   // slabs per weight gradient (the ws kernels: one per CU)
 static constexpr int kWgSlots = kMaxReduce; // weight gradients per backward, reduced by one batched launch
 static constexpr int kW2gWgs = 256;   // W2 gradient: one workgroup per CU (MI355X: 256 CUs)
+// batched weight gradients (k_wgrad_ws_batch): the jobs share one grid, so a job need not fill the chip
+// by itself — a workgroup takes ≥ kWsMinStages 32-row stages (its 160×160 slab, written here and read
+// by the reduction, stays small against its operands) while a job keeps ≥ kWsMinWgs workgroups
+static constexpr int kWsMinStages = 32;
+static constexpr int kWsMinWgs = 32;
 // Diagnosis switches (A/B of superseded kernels, per-kernel math) exist only in -DSPWGNN_DIAG builds;
 // the shipping library has no environment-dependent code path.
 static bool getenv_flag(const char* name) {
@@ -565,6 +570,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         wa.b0 = g.b0;
         const int64_t nst = wa.nbs * wa.S;
         int64_t wgs = std::min<int64_t>(nst, kW2gWgs);
+        if (wsb) wgs = std::min<int64_t>(wgs, std::max<int64_t>(kWsMinWgs, (nst + kWsMinStages - 1) / kWsMinStages));
         wa.stages_per_wg = (nst + wgs - 1) / wgs;
         wgs = (nst + wa.stages_per_wg - 1) / wa.stages_per_wg;
         chunks = wgs;
@@ -667,6 +673,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     const bool b16 = store_b16(r, b);
     const int64_t nN = b->n_nodes;
     const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
+    // grads is cleared first: the reductions write the 22 Keras tensors' elements, not every float of the
+    // flat buffer (measured: without the clear 739 floats of a NaN-filled buffer stay NaN —
+    // tests/test_gpu_parity.py::test_backward_writes_every_gradient)
     SPW_CHECK(hipMemsetAsync(grads, 0, param_table().total * sizeof(float), st));
     Prof prof{r, st};
 
