@@ -402,6 +402,8 @@ def main():
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the other-math reference measurements")
     ap.add_argument("--no-kernel-table", action="store_true", help="skip the per-kernel roofline table")
     ap.add_argument("--infer", action="store_true", help="alias of --config 5")
+    ap.add_argument("--buckets", type=int, default=1,
+                    help="N>1: the flat gradient all-reduced as this many async pieces")
     args = ap.parse_args()
     if args.infer:
         args.config = 5
@@ -442,7 +444,7 @@ def run_train(args, cfg, world, rank, device):
     params = P.to_flat(P.glorot_uniform(0), device=device)
     if world > 1:
         dist.broadcast(params, 0)
-    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math)
+    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math, buckets=args.buckets)
     step_in = ((batches[0], targets[0]) if len(batches) == 1 else (batches, targets)) + (n_global,)
     n_micro = len(batches)
     for _ in range(args.warmup):
@@ -464,6 +466,10 @@ def run_train(args, cfg, world, rank, device):
         return run_replay(args, cfg, trainer, rank, device, kname, table, wl)
     ev = HipEvents(2 * MAX_LAUNCHES * n_micro * args.steps)
     per = 2 * MAX_LAUNCHES * n_micro
+    # N>1: the gradient all-reduce of every timed step between two events on the step's stream, so
+    # the line separates the collective (RCCL over xGMI) from the compute
+    ar_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(args.steps)] if world > 1 else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -471,6 +477,8 @@ def run_train(args, cfg, world, rank, device):
     for k in range(args.steps):
         # the library fills events in launch order: one slice of the array per step (and micro-batch)
         evs = ev.ev[per * k: per * (k + 1)]
+        if ar_ev:
+            trainer.ar_events = ar_ev[k]
         if n_micro == 1:
             trainer.prof_kernel, trainer.prof_events = kid, evs
             out3 = trainer.step(*step_in)
@@ -481,7 +489,17 @@ def run_train(args, cfg, world, rank, device):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    trainer.prof_kernel, trainer.prof_events = 0, None
+    trainer.prof_kernel, trainer.prof_events, trainer.ar_events = 0, None, None
+    allreduce = None
+    if ar_ev:
+        ar_ms = [a.elapsed_time(b) for a, b in ar_ev]
+        ar_t = torch.tensor([float(np.mean(ar_ms))], dtype=torch.float64, device=device)
+        dist.all_reduce(ar_t, op=dist.ReduceOp.MAX)
+        nbytes = params.numel() * params.element_size()
+        allreduce = {"allreduce_ms": round(float(ar_t.item()), 4), "bytes": nbytes, "buckets": trainer.buckets,
+                     "backend": dist.get_backend(),
+                     "note": "mean per step, max over ranks; HIP events around Trainer.allreduce on the step's "
+                             "stream (includes waiting for the slowest rank to arrive)"}
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -518,6 +536,9 @@ def run_train(args, cfg, world, rank, device):
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if allreduce:
+        out["allreduce_ms"] = allreduce["allreduce_ms"]
+        out["allreduce"] = allreduce
     if world == 1 and args.config == 0 and math == "x6" and not args.no_f32_leg:
         # the same step in the other SPWGNN_MATH_* modes, for reference: f32 MFMA (fp32-class like
         # x6) and bf16 (operands rounded to bf16, one product — BASELINE configs 3-4's arithmetic)
@@ -558,13 +579,11 @@ def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
     plan, tgt = plans[0], tg_np[0]
     rs = ReplayStep(plan, device, trainer.replay_body(plan.n_nodes, n_global))
     for _ in range(args.warmup + 1):             # the first call runs eagerly and captures
-        rs(plan, tgt)
-        trainer.iterations += 1
+        trainer.replay_step(rs, plan, tgt)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        rs(plan, tgt)
-        trainer.iterations += 1
+        trainer.replay_step(rs, plan, tgt)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     loss = float(rs.bce.out3[0].item())

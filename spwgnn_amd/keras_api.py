@@ -186,7 +186,8 @@ class KerasModel:
             self._ctr = DeviceCounters(dev, self.net._step_seed, self.iterations, self.lr, self.beta1,
                                        self.beta2)
         else:
-            self._ctr.set(key=self.net._step_seed, step=self.iterations)
+            self._ctr.set(key=self.net._step_seed, step=self.iterations, lr=self.lr, beta1=self.beta1,
+                          beta2=self.beta2)
         if self._replays is None or self._replay_graph != graph:
             self._replays = ReplayCache(dev, self._replay_body, graph=graph)
             self._replay_graph = graph

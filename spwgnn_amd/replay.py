@@ -50,13 +50,21 @@ class DeviceCounters:
         self.key = torch.tensor([_i64(key)], dtype=torch.int64, device=self.device)
         self.step = torch.tensor([int(step)], dtype=torch.int32, device=self.device)
         self.lr_table = E.adam_lr_table(LR_TABLE_LEN, lr, beta1, beta2, self.device)
+        self.hyper = (float(lr), float(beta1), float(beta2))
 
-    def set(self, key: Optional[int] = None, step: Optional[int] = None):
-        """Host values → device words (stream-ordered copies; outside any capture)."""
+    def set(self, key: Optional[int] = None, step: Optional[int] = None, lr: Optional[float] = None,
+            beta1: Optional[float] = None, beta2: Optional[float] = None):
+        """Host values → device words (stream-ordered copies; outside any capture). A changed
+        (lr, β1, β2) rebuilds the lr table IN PLACE: captured graphs keep reading its address."""
         if key is not None:
             self.key.fill_(_i64(key))
         if step is not None:
             self.step.fill_(int(step))
+        hyper = (float(self.hyper[0] if lr is None else lr), float(self.hyper[1] if beta1 is None else beta1),
+                 float(self.hyper[2] if beta2 is None else beta2))
+        if hyper != self.hyper:
+            self.lr_table.copy_(E.adam_lr_table(LR_TABLE_LEN, *hyper, self.device))
+            self.hyper = hyper
 
 
 class StaticBatch:
@@ -112,6 +120,7 @@ class StaticBatch:
         # host-side copies the wrappers keep for reporting (edge ids, counts) follow the new batch
         b = self.batch
         b.tower_edges, b.src, b.dst, b.edge_id = plan.tower_edges, plan.src, plan.dst, plan.edge_id
+        b.tower_nodes, b.node_shape = plan.tower_nodes, plan.node_shape
 
 
 class ReplayStep:

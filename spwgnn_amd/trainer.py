@@ -78,7 +78,8 @@ class Trainer:
 
     def __init__(self, params: torch.Tensor, engine=None, mp_steps: int = E.REF_MP_STEPS,
                  dropout: float = E.REF_DROPOUT, seed: int = 0, lr: float = 5e-4, beta1: float = 0.9,
-                 beta2: float = 0.999, eps: float = 1e-7, l2: float = 0.0, group=None, math: str = "x6"):
+                 beta2: float = 0.999, eps: float = 1e-7, l2: float = 0.0, group=None, math: str = "x6",
+                 buckets: int = 1):
         self.params = params
         self.engine = engine if engine is not None else HipEngine(params.device)
         self.m = torch.zeros_like(params)
@@ -92,6 +93,14 @@ class Trainer:
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.prof_kernel = 0
         self.prof_events = None
+        # gradient all-reduce: `buckets` contiguous 64-float-aligned pieces of the flat gradient, each
+        # its own async all-reduce (all in flight together, waited before Adam); ar_events: an optional
+        # (start, end) torch.cuda.Event pair recorded around the all-reduce (bench.py's allreduce_ms)
+        self.buckets = max(1, int(buckets))
+        self.ar_events = None
+        self._ctr = None          # replayed steps' device counters (replay_body)
+        self._ctr_at = 0          # the host iteration count the device step word holds
+        self._w3 = {}             # (n_nodes, 1, 1) fp64 weights of a micro-batch's [loss, correct, n]
 
     def run_config(self, micro: int = 0) -> E.RunConfig:
         # distinct dropout keys per step, per rank and per micro-batch (different towers)
@@ -99,20 +108,29 @@ class Trainer:
         return E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, seed=key, math=self.math,
                            prof_kernel=self.prof_kernel, prof_events=self.prof_events)
 
+    def _sync_counters(self):
+        """Device step word and lr table ← the host's iteration count and (lr, β1, β2), when they
+        differ (a step() or an lr change since the last replay)."""
+        from .replay import DeviceCounters
+        if self._ctr is None:
+            self._ctr = DeviceCounters(self.params.device, 0, self.iterations, self.lr, self.b1, self.b2)
+        elif self._ctr_at != self.iterations or self._ctr.hyper != (float(self.lr), float(self.b1), float(self.b2)):
+            self._ctr.set(step=self.iterations, lr=self.lr, beta1=self.b1, beta2=self.b2)
+        self._ctr_at = self.iterations
+
     def replay_body(self, n_nodes: int, n_global: Optional[int] = None):
         """The launches of one single-batch `step` for spwgnn_amd.replay.ReplayStep (hipGraph
         replay): the dropout key and Adam step are device words (spwgnn_step_advance in the
         Trainer's splitmix key mode, spwgnn_adam_dev), so every replay is the next optimizer step
-        with the masks `step` would draw. Single process only (no all-reduce inside a graph)."""
-        from .replay import DeviceCounters
+        with the masks `step` would draw. Single process only (no all-reduce inside a graph).
+
+        Run each step through `replay_step(rs, plan, target)`: a replay advances the device words
+        only, and replay_step keeps `iterations` (the host counter `step` reads) in step with them."""
         if self.world > 1:
             raise ValueError("replayed steps are single-process; DP steps use step()")
         if not isinstance(self.engine, HipEngine):
             raise ValueError("replayed steps need the HIP engine")
-        if getattr(self, "_ctr", None) is None:
-            self._ctr = DeviceCounters(self.params.device, 0, self.iterations, self.lr, self.b1, self.b2)
-        else:
-            self._ctr.set(step=self.iterations)
+        self._sync_counters()
         ctr = self._ctr
         w = n_nodes / (n_global or n_nodes)
         grads = torch.empty_like(self.params)
@@ -128,6 +146,38 @@ class Trainer:
             E.adam_dev(self.params, grads, self.m, self.v, ctr.step, ctr.lr_table, self.b1, self.b2, self.eps,
                        self.l2)
         return body
+
+    def bucket_bounds(self, n: int):
+        """[(start, end)) of the gradient buckets over a flat buffer of n floats (64-float aligned)."""
+        k = min(self.buckets, max(1, n // 64))
+        cuts = [0] + [min(n, (n * i // k + 63) // 64 * 64) for i in range(1, k)] + [n]
+        return [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+
+    def allreduce(self, acc: torch.Tensor):
+        """Σ over ranks of the node-weighted flat gradient (RCCL over xGMI with backend nccl). With
+        buckets > 1 the pieces are issued as async all-reduces, all in flight before the first wait."""
+        ev = self.ar_events
+        if ev is not None:
+            ev[0].record()
+        if self.buckets == 1:
+            dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            works = [dist.all_reduce(acc[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                     for a, b in self.bucket_bounds(acc.numel())]
+            for w in works:
+                w.wait()
+        if ev is not None:
+            ev[1].record()
+
+    def replay_step(self, rs, plan, target):
+        """One replayed optimizer step (rs: a ReplayStep/ReplayCache over `replay_body`): the
+        device words are first brought to the host's counters (a `step()` may have run in
+        between), the step runs, and the host counter advances with the device one."""
+        self._sync_counters()
+        out = rs(plan, target)
+        self.iterations += 1
+        self._ctr_at = self.iterations
+        return out
 
     def step(self, batch, target, n_global: Optional[int] = None):
         """One optimizer step. `batch`/`target` may be lists (micro-batches of this rank's shard);
@@ -156,7 +206,11 @@ class Trainer:
             out3, dz = self.engine.loss(z, tg)
             # [loss, correct, n] of this micro-batch, folded in before the engine reuses its buffer:
             # Σ loss_i·n_i, Σ correct_i, Σ n_i (the engine's out3 is one persistent tensor)
-            w3 = out3.double() * out3.new_tensor([float(b.n_nodes), 1.0, 1.0], dtype=torch.float64)
+            wt = self._w3.get((b.n_nodes, out3.device))
+            if wt is None:
+                wt = self._w3[(b.n_nodes, out3.device)] = out3.new_tensor([float(b.n_nodes), 1.0, 1.0],
+                                                                           dtype=torch.float64)
+            w3 = out3.double() * wt
             tot3 = w3 if tot3 is None else tot3 + w3
             g = self.engine.backward(self.params, b, run, dz)
             w = b.n_nodes / n_global
@@ -169,7 +223,7 @@ class Trainer:
             else:
                 acc.add_(g, alpha=w)
         if self.world > 1:
-            dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
+            self.allreduce(acc)
         self.iterations += 1
         self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
                          self.l2, 1.0)

@@ -90,9 +90,89 @@ def test_trainer_replay_equals_step():
     tb = Trainer(P.to_flat(params, device="cuda"), mp_steps=5, dropout=0.1, seed=11, math="x6")
     rs = ReplayStep(plans[0], "cuda", tb.replay_body(plans[0].n_nodes))
     for p, t in zip(plans, tgts):
-        rs(p, t)
-        tb.iterations += 1
+        tb.replay_step(rs, p, t)
     torch.cuda.synchronize()
     assert rs.replays == 2
     assert torch.equal(ta.params, tb.params) and torch.equal(ta.m, tb.m) and torch.equal(ta.v, tb.v)
-    assert int(tb._ctr.step.item()) == 3
+    assert int(tb._ctr.step.item()) == 3 and tb.iterations == 3
+
+
+def _trainer_plans(n):
+    plans, tgts = [], []
+    for seed in range(1, n + 1):
+        raw = D.synthetic_towers(32, 6, seed=seed)
+        obj = (raw / D.RELATION_THRESHOLD).astype(np.float32)
+        Rs, Rr = D.relation_matrices(raw, D.RELATION_THRESHOLD)
+        e = np.array(O.dense_to_edges(Rs, Rr), np.int64).reshape(-1, 4)
+        te = np.bincount(e[:, 0], minlength=32).astype(np.int32)
+        plans.append(HostPlan.build(obj.reshape(-1, 3), np.full(32, 6, np.int32), e[:, 0] * 6 + e[:, 2],
+                                    e[:, 0] * 6 + e[:, 3], te, edge_cap=30))
+        tgts.append(np.random.default_rng(seed).integers(0, 2, 192).astype(np.float32))
+    return plans, tgts
+
+
+def test_trainer_replay_mixed_with_step_and_lr_change():
+    """replayed steps interleaved with eager Trainer.step calls and an lr change keep
+    one step count and the current lr: replay, step, replay (lr halved), step == four eager steps
+    with the same lr schedule, bit for bit."""
+    params = O.random_params(13)
+    plans, tgts = _trainer_plans(4)
+    ta = Trainer(P.to_flat(params, device="cuda"), mp_steps=3, dropout=0.1, seed=5, math="x6")
+    for i, (p, t) in enumerate(zip(plans, tgts)):
+        if i == 2:
+            ta.lr = 2.5e-4
+        ta.step(TowerBatch.from_plan(p, "cuda"), torch.as_tensor(t, device="cuda"))
+    tb = Trainer(P.to_flat(params, device="cuda"), mp_steps=3, dropout=0.1, seed=5, math="x6")
+    rs = ReplayStep(plans[0], "cuda", tb.replay_body(plans[0].n_nodes))
+    tb.replay_step(rs, plans[0], tgts[0])
+    tb.step(TowerBatch.from_plan(plans[1], "cuda"), torch.as_tensor(tgts[1], device="cuda"))
+    tb.lr = 2.5e-4
+    tb.replay_step(rs, plans[2], tgts[2])
+    tb.step(TowerBatch.from_plan(plans[3], "cuda"), torch.as_tensor(tgts[3], device="cuda"))
+    torch.cuda.synchronize()
+    assert rs.replays == 1 and tb.iterations == 4
+    assert torch.equal(ta.params, tb.params) and torch.equal(ta.m, tb.m) and torch.equal(ta.v, tb.v)
+
+
+def test_fit_lr_change_between_fits():
+    """model.lr changed between two fit calls reaches the replayed Adam (the lr table
+    is rebuilt in place): equal to the same two fits issued eagerly."""
+    x, y = _xy(64, 4)
+    res = []
+    for graph in (True, False):
+        m = PropagationNetwork(seed=2).getModel(6)
+        m.fit(x, y, batch_size=32, epochs=1, shuffle=False, verbose=0, graph=graph)
+        m.lr = 1e-3
+        m.fit(x, y, batch_size=32, epochs=1, shuffle=False, verbose=0, graph=graph)
+        torch.cuda.synchronize()
+        res.append(m.net.flat.detach().cpu().numpy().copy())
+    assert np.array_equal(res[0], res[1])
+    # and the lr did change the trajectory
+    m = PropagationNetwork(seed=2).getModel(6)
+    m.fit(x, y, batch_size=32, epochs=2, shuffle=False, verbose=0, graph=False)
+    assert not np.array_equal(res[1], m.net.flat.detach().cpu().numpy())
+
+
+def test_capacity_plan_equals_compact_plan():
+    """a capacity-planned batch (N(N-1) relation slots per tower, fit's plan) gives the
+    same logits and weight gradients as the compact plan of the same towers, at the fp32 tolerance
+    (the padding blocks are inert; the segment sums' k-block grouping may differ)."""
+    from spwgnn_amd import engine as E
+    x, y = _xy(48, 21)
+    ds = CompactDataset(x["objects"], x["sender_relations"], x["receiver_relations"], x["propagation"])
+    idx = np.arange(48)
+    flat = P.to_flat(O.random_params(5), device="cuda")
+    tgt = torch.as_tensor(y["target"].reshape(-1), device="cuda")
+    out = []
+    for cap in (True, False):
+        b = TowerBatch.from_plan(ds.subset_plan(idx, edge_cap=cap), "cuda")
+        run = E.RunConfig(5, training=True, dropout=0.0, math="x6")
+        ws = E.Workspace("cuda")
+        z = E.forward(flat, b, run, ws)
+        _, dz = E.bce(z, tgt, E.BceScratch("cuda"))
+        g, _ = E.backward(flat, b, run, ws, dz)
+        out.append((z.cpu().numpy().copy(), P.from_flat(g)))
+    (za, ga), (zb, gb) = out
+    assert np.all(np.abs(za - zb) <= 1e-5 + 1e-5 * np.abs(zb))
+    for name, r in gb.items():
+        assert np.abs(ga[name] - r).max() <= 1e-5 * np.abs(r).max() + 1e-7, name
