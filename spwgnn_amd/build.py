@@ -13,6 +13,11 @@ CSRC = HERE / "csrc"
 INCLUDE = HERE.parent / "include"
 LIB = HERE / "libspwgnn_hip.so"
 OBJDIR = HERE / "csrc" / "build"
+# A/B and diagnosis builds (e.g. SPWGNN_CFLAGS=-DSPWGNN_DIAG): SPWGNN_BUILD_OUT names the library to
+# write instead of the in-tree one; its objects go to a directory of their own
+if os.environ.get("SPWGNN_BUILD_OUT"):
+    LIB = Path(os.environ["SPWGNN_BUILD_OUT"]).resolve()
+    OBJDIR = HERE / "csrc" / ("build_" + LIB.stem)
 SOURCES = ["host.cpp", "api.hip", "kernels_fwd.hip", "kernels_bwd.hip", "kernels_misc.hip", "kernels_team.hip"]
 HEADERS = ["spwgnn_layout.h", "device_common.h", "gemm_blocks.h", "kernels.h"]
 ARCH = os.environ.get("SPWGNN_ARCH", "gfx950")
@@ -45,6 +50,7 @@ def _stale(obj: Path, src: Path) -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     OBJDIR.mkdir(parents=True, exist_ok=True)
+    LIB.parent.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     jobs = []
     objs = []

@@ -308,6 +308,16 @@ static bool store_b16(const spwgnn_run* r, const spwgnn_batch* b) {
            !getenv_flag("SPWGNN_WG_OLD");
 }
 
+// ... and, when every kernel that writes or reads them runs its wide (non-team) form, the node-side
+// per-step arrays that only ever feed MFMA operands: H2s (node forward's W3 product, W3 gradient),
+// o1 (omp.1 gradient; the node backward reads only its sign), dU, dV (node backward's W1bᵀ/W1cᵀ
+// products, W1b/W1c gradients), g (W3 gradient) and dx (omp.1 gradient) — exact as above.
+static bool store_b16_node(const spwgnn_run* r, const spwgnn_batch* b) {
+    return store_b16(r, b) && kmath(r, kX6EdgeFwd) == MATH_BF16 && kmath(r, kX6NodeFwd) == MATH_BF16 &&
+           kmath(r, kX6NodeBwd) == MATH_BF16 && kmath(r, kX6EdgeBwd) == MATH_BF16 && b->nw_max <= 16 &&
+           !team_blocks(b->n_wtiles) && !team_blocks((b->n_nodes + 31) / 32) && !getenv_flag("SPWGNN_NODE_F32");
+}
+
 static int32_t run_forward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w,
                            char* base, float* logits, hipStream_t st) {
     Ctx c{w, base};
@@ -435,6 +445,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.mask1 = r->training ? c.u(w.m1_at(s)) : nullptr;
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
         ef.a_b16 = store_b16(r, b);
+        ef.n16 = store_b16_node(r, b);
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
         SPW_CHECK(launch_edge_fwd(ef, kmath(r, kX6EdgeFwd), st));
@@ -471,6 +482,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
             nf.x_w1b = c.x6(X6_W1B);
             nf.x_w1c = c.x6(X6_W1C);
         }
+        nf.n16 = store_b16_node(r, b);
         SPW_CHECK(prof.before(SPWGNN_K_NODE_FWD));
         SPW_CHECK(launch_node_fwd(nf, kmath(r, kX6NodeFwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_FWD));
@@ -671,6 +683,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     const int S = r->mp_steps;
     const bool rebuild = rebuild_dA(r, b);
     const bool b16 = store_b16(r, b);
+    const bool n16 = store_b16_node(r, b);
     const int64_t nN = b->n_nodes;
     const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
     // grads is cleared first: the reductions write the 22 Keras tensors' elements, not every float of the
@@ -716,6 +729,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             nb.x_wo1pt = c.x6(X6_WO1PT);
             nb.x_w3t = c.x6(X6_W3T);
         }
+        nb.n16 = n16;
         SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
         SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
@@ -739,6 +753,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.dA = c.f(w.dA);
         eb.dU = c.f(w.dU_at(s));
         eb.dV = c.f(w.dV_at(s));
+        eb.n16 = n16;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_BWD));
         SPW_CHECK(launch_edge_bwd(eb, kmath(r, kX6EdgeBwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
@@ -758,6 +773,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             nb.x_w1bt = c.x6(X6_W1BT);
             nb.x_w1ct = c.x6(X6_W1CT);
         }
+        nb.n16 = n16;
         SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
     }
     if (rebuild) {
@@ -883,11 +899,13 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
+        g.b16 = n16 ? kB16Y : 0;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // rmp.0 rows 250..349 (W1c)
         WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
         g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
+        g.b16 = n16 ? kB16Y : 0;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // omp.0 rows 200..299 (P part)
@@ -904,6 +922,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // rmp.2 (W3, b3): X = [H2s | deg]
         WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
         g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
+        g.b16 = n16 ? (kB16X | kB16Y) : 0;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
@@ -919,6 +938,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     {   // omp.1 (Wo2, bo2), x' column order → Keras order
         WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
         g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
+        g.b16 = n16 ? (kB16X | kB16Y) : 0;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     {   // om.0: X = [y, w | 1]

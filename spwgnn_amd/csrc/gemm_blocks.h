@@ -1,5 +1,6 @@
 // Register-level MFMA building blocks (fp32, v_mfma_f32_32x32x2_f32) used by every kernel.
 #pragma once
+#include <type_traits>
 #include "device_common.h"
 
 namespace spw {
@@ -110,6 +111,28 @@ __device__ __forceinline__ void store_cm_b16(uint16_t* __restrict__ blk, const f
                 *reinterpret_cast<uint2*>(blk + cm_offk<KH>(j, f0)) = pack4_bf16(v);
             }
         }
+}
+
+template <int NT>
+__device__ __forceinline__ void load_cm_b16(const uint16_t* __restrict__ blk, f32x16 (&X)[NT], int lane) {
+    constexpr int KH = NT == 5 ? kKhE : kKhN;
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * t + 8 * q + 4 * h;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (32 * t + 8 * q + 4 < 2 * KH) v = unpack4_bf16(*reinterpret_cast<const uint2*>(blk + cm_offk<KH>(j, f0)));
+            X[t][4 * q] = v.x;
+            X[t][4 * q + 1] = v.y;
+            X[t][4 * q + 2] = v.z;
+            X[t][4 * q + 3] = v.w;
+        }
+}
+// one element of a bf16-stored array (RNE; the element index of the fp32 layout)
+__device__ __forceinline__ void store_b16(float* base, int64_t idx, float v) {
+    reinterpret_cast<uint16_t*>(base)[idx] = (uint16_t)(pk_bf16(v, 0.f) & 0xffffu);
 }
 
 // ---- h2 > 0 bits (mask2) of one 32-edge block: kM2Blk words, [edge][8]; word t < 5 holds the bits
@@ -581,6 +604,13 @@ struct HalfRows {
             for (int q = 0; q < Q; ++q) raw[c][q] = *reinterpret_cast<const float4*>(p + 256 * q);
         }
     }
+    // the blocks at element offsets off[c] of the array at base
+    __device__ __forceinline__ void load_at(const float* base, const int64_t (&off)[NC], int lane) {
+        const float* blk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) blk[c] = base + off[c];
+        load(blk, lane);
+    }
     __device__ __forceinline__ void operator()(int c, int kb, float (&v)[8]) const {
         const float4 x = raw[c][2 * kb];
         const float4 y = 2 * kb + 1 < Q ? raw[c][2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -588,5 +618,30 @@ struct HalfRows {
         v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
     }
 };
+// The same operand stored as bf16 at the element index of its fp32 layout (bf16 math):
+// 8-byte loads, unpacked to fp32 (the bf16 math's operand rounding then reproduces the stored bits).
+template <int KH, int NC>
+struct HalfRowsB16 {
+    static constexpr int Q = KH / 4;
+    uint2 raw[NC][Q];
+    // the blocks at element offsets off[c] of the bf16 array at base (element e at byte 2e)
+    __device__ __forceinline__ void load_at(const float* base, const int64_t (&off)[NC], int lane) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const uint16_t* p = reinterpret_cast<const uint16_t*>(base) + off[c] + ((lane >> 5) * 32 + (lane & 31)) * 4;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) raw[c][q] = *reinterpret_cast<const uint2*>(p + 256 * q);
+        }
+    }
+    __device__ __forceinline__ void operator()(int c, int kb, float (&v)[8]) const {
+        const float4 x = unpack4_bf16(raw[c][2 * kb]);
+        const float4 y = 2 * kb + 1 < Q ? unpack4_bf16(raw[c][2 * kb + 1]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    }
+};
+// fp32 or bf16 (B16) half rows
+template <int KH, int NC, bool B16>
+using HalfRowsT = typename std::conditional<B16, HalfRowsB16<KH, NC>, HalfRows<KH, NC>>::type;
 
 }  // namespace spw

@@ -112,6 +112,7 @@ struct EdgeFwdArgs {
     uint32_t *mask1, *mask2;
     float* h1_out;     // training: h1 rows, chunk-major blocks (kCmBlk), for the W2 gradient
     int a_b16;         // bf16 math (training): A stored as bf16
+    int n16;           // bf16 math (training, wide kernels): H2s stored as bf16 (§3g, node side)
     const uint4* x_w2; // x6 image of W2 (half rows, kh 76) — the LDS B operand (math == MATH_X6)
 };
 
@@ -125,6 +126,7 @@ struct NodeFwdArgs {
     float* cw_out;
     const float *w3a, *wo1c, *wo1a, *wo1p, *wo2, *w1b, *w1c, *bo1, *bo2p;
     const uint4 *x_w3a, *x_wo1c, *x_wo1a, *x_wo1p, *x_wo2, *x_w1b, *x_w1c;   // x6 images
+    int n16;        // bf16 math (training, wide kernels): H2s read and o1 stored as bf16 (§3g, node side)
 };
 
 struct NodeBwdArgs {
@@ -139,6 +141,7 @@ struct NodeBwdArgs {
     int dco_sum;    // x6: no dco here; k_enc_node_bwd applies Wo1cᵀ once to Σ_s do1_s (linear)
     const float *w1bt, *w1ct, *wo2t, *wo1ct, *wo1at, *wo1pt, *w3t;
     const uint4 *x_w1bt, *x_w1ct, *x_wo2t, *x_wo1ct, *x_wo1at, *x_wo1pt, *x_w3t;   // x6 images
+    int n16;        // bf16 math (training, wide kernels): dU, dV, o1 read and dx, g stored as bf16 (§3g)
 };
 
 struct EdgeBwdArgs {
@@ -152,6 +155,7 @@ struct EdgeBwdArgs {
     float *dA, *dU, *dV;
     float* dh2_out;    // dh2pre rows, chunk-major blocks (kCmBlk), for the W2 gradient
     const uint4* x_w2t; // x6 image of W2ᵀ (half rows, kh 76) — the LDS B operand (math == MATH_X6)
+    int n16;           // bf16 math (training, wide kernels): dU, dV stored as bf16 (§3g, node side)
 };
 
 struct DaArgs {           // k_dA_x6: dA = Σ_s dh1pre_s, recomputed per 32-edge block
@@ -258,6 +262,7 @@ struct ReduceArgs {
 enum WsVariant : int {
     WSV_160_160 = 0, WSV_160_160_ROW, WSV_128_160, WSV_160_128, WSV_128_128, WSV_XD_EDGE, WSV_XD_NODE,
     WSV_XD_EDGE_B16Y, WSV_160_160_ROW_B16, WSV_160_160_B16,   // bf16 math only
+    WSV_128_160_B16Y, WSV_160_128_B16, WSV_128_128_B16,        // bf16 math, bf16-stored node arrays
     WSV_NONE = -1
 };
 struct WsJob {

@@ -120,7 +120,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // Node side of one backward step in split-bf16 math: the k_node_bwd chain on tgemm_x6, NC 32-node
 // column tiles per wave (launched: NC = 1 at two waves per SIMD).
 // NW > 0: weight images shared by the workgroup's waves through an LDS ring (k_node_fwd_x6).
-template <int NC, int NP = 3, int NW = 0>
+// N16 (bf16 math, §3g node side): dU, dV, o1 read and dx, g stored as bf16
+template <int NC, int NP = 3, int NW = 0, bool N16 = false>
 __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -148,19 +149,17 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     } else {
 #pragma unroll
         for (int c = 0; c < NC; ++c) load_cm<4>(a.dPin + bN(c), D[c], lane);
-        const float* blk[NC];
-        {
-            HalfRows<kKhE, NC> hr;
+        int64_t off[NC];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) blk[c] = a.dU + bE(c);
-            hr.load(blk, lane);
+        for (int c = 0; c < NC; ++c) off[c] = bE(c);
+        {
+            HalfRowsT<kKhE, NC, N16> hr;
+            hr.load_at(a.dU, off, lane);
             tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, D, a.x_w1bt, lane, wr);
         }
         {
-            HalfRows<kKhE, NC> hr;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) blk[c] = a.dV + bE(c);
-            hr.load(blk, lane);
+            HalfRowsT<kKhE, NC, N16> hr;
+            hr.load_at(a.dV, off, lane);
             tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, D, a.x_w1ct, lane, wr);
         }
     }
@@ -196,14 +195,18 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
         // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
         if (has[c]) store_cm<4>(a.dPout + bN(c), D[c], lane, valid[c]);
         if (a.first && h == 1) D[c][3][0] = valid[c] ? a.dlogits[(nb0 + c) * 32 + j] : 0.f;  // x' row 100 = logit
-        if (has[c]) store_cm<4>(a.dx + bN(c), D[c], lane, valid[c]);
+        if (has[c]) {
+            if constexpr (N16) store_cm_b16<4>(reinterpret_cast<uint16_t*>(a.dx) + bN(c), D[c], lane, valid[c]);
+            else store_cm<4>(a.dx + bN(c), D[c], lane, valid[c]);
+        }
     }
     zero2(G);
     tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(D, G, a.x_wo2t, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 O1[4];
-        load_cm<4>(a.o1 + bN(c), O1, lane);
+        if constexpr (N16) load_cm_b16<4>(reinterpret_cast<const uint16_t*>(a.o1) + bN(c), O1, lane);
+        else load_cm<4>(a.o1 + bN(c), O1, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -251,7 +254,10 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
                 const float v = Aa[t][r];
                 D[c][t][r] = D[c][t][r] * (1.f - v * v);
             }
-        if (has[c]) store_cm<4>(a.g + bN(c), D[c], lane, valid[c]);
+        if (has[c]) {
+            if constexpr (N16) store_cm_b16<4>(reinterpret_cast<uint16_t*>(a.g) + bN(c), D[c], lane, valid[c]);
+            else store_cm<4>(a.g + bN(c), D[c], lane, valid[c]);
+        }
     }
     f32x16 H[NC][5];
 #pragma unroll
@@ -640,10 +646,12 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
     if ((math == MATH_X6 || math == MATH_BF16) && a.dco_sum && team_blocks((a.n_nodes + 31) / 32))
-        return launch_node_bwd_team(a, math, st);
+        return a.n16 ? hipErrorInvalidValue : launch_node_bwd_team(a, math, st);   // team kernels: fp32 arrays
+    if (a.n16 && math != MATH_BF16) return hipErrorInvalidValue;
     if (math == MATH_BF16) {
         const int w = (a.n_nodes + 31) / 32;
-        hipLaunchKernelGGL((k_node_bwd_x6<1, 1, 4>), dim3((w + 3) / 4), dim3(256), 0, st, a);
+        if (a.n16) hipLaunchKernelGGL((k_node_bwd_x6<1, 1, 4, true>), dim3((w + 3) / 4), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_node_bwd_x6<1, 1, 4>), dim3((w + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (math == MATH_X6) {
@@ -674,7 +682,8 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 #ifndef SPWGNN_DA_PF_B16
 #define SPWGNN_DA_PF_B16 5
 #endif
-template <bool ACCUM, bool NODA = false, int NP = 3, int DBG = 0>   // DBG 3 (diagnosis): G3 rows of the tile's first node
+// N16 (bf16 math, §3g node side): dU, dV stored as bf16
+template <bool ACCUM, bool NODA = false, int NP = 3, int DBG = 0, bool N16 = false>   // DBG 3 (diagnosis): G3 rows of the tile's first node
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
     constexpr int PF = NP == 1 ? SPWGNN_EBWD_PF_B16 : SPWGNN_EBWD_PF, kWaves = 8;   // bf16: see k_dA_x6
     __shared__ uint4 wl[50 * 3 * 64];   // W2ᵀ x6 image: [kb·5 + T][part][lane]
@@ -837,7 +846,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             float* o = row < 16 ? a.dV : a.dU;   // chunk-major node rows
 #pragma unroll
             for (int t = 0; t < 5; ++t)
-                if (32 * t + i < 2 * kKhE) o[cm_index<kKhE>(n0 + node, 32 * t + i)] = nacc[t][r];
+                if (32 * t + i < 2 * kKhE) {
+                    if constexpr (N16) store_b16(o, cm_index<kKhE>(n0 + node, 32 * t + i), nacc[t][r]);
+                    else o[cm_index<kKhE>(n0 + node, 32 * t + i)] = nacc[t][r];
+                }
         }
     }
     info = ninfo;
@@ -846,7 +858,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
     if (math != MATH_F32 && a.nw_max <= 16 && a.no_dA && team_blocks(a.n_wtiles))   // small batches
-        return launch_edge_bwd_team(a, math, st);
+        return a.n16 ? hipErrorInvalidValue : launch_edge_bwd_team(a, math, st);   // team kernels: fp32 dU/dV
+    if (a.n16 && (math != MATH_BF16 || a.nw_max > 16 || !a.no_dA)) return hipErrorInvalidValue;
     if (math != MATH_F32 && a.nw_max <= 16) {
         const dim3 g(edge_grid(a.n_wtiles, 8)), b(512);   // two waves per SIMD
         // no_dA: dA = Σ_s dh1pre_s is rebuilt once after the step loop by k_dA_x6 (launch_dA)
@@ -858,7 +871,8 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
                 return hipGetLastError();
             }
 #endif
-            if (math == MATH_BF16) hipLaunchKernelGGL((k_edge_bwd_x6<false, true, 1>), g, b, 0, st, a);
+            if (math == MATH_BF16 && a.n16) hipLaunchKernelGGL((k_edge_bwd_x6<false, true, 1, 0, true>), g, b, 0, st, a);
+            else if (math == MATH_BF16) hipLaunchKernelGGL((k_edge_bwd_x6<false, true, 1>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_edge_bwd_x6<false, true>), g, b, 0, st, a);
             return hipGetLastError();
         }

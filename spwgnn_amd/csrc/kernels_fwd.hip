@@ -273,7 +273,12 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     zero_tiles(X);
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_w1a, lane);
     bias_act_rho<5, false>(X, a.b_w1a, h);
-    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, true);   // chunk-major; k_edge_fwd masks padding edges
+    if (!valid)   // padding edge: kPadA (h1 = relu(A + U + V) = 0 without a validity multiply)
+#pragma unroll
+        for (int t = 0; t < 5; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) X[t][r] = kPadA;
+    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, true);   // chunk-major
 }
 
 // The rm encoder in split-bf16 math: NC 32-edge blocks per wave (column tiles c). Launched with
@@ -361,8 +366,15 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_x6(EncEdgeArg
     zero2(X);
     tchain_x6s<5, 10, 5, NC, kX6Ring, NP, NW>(Y, X, a.x_w1a, lane, wr);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) bias_act_rho<5, false>(X[c], a.b_w1a, h);
-    save(a.A, nullptr, X, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
+    for (int c = 0; c < NC; ++c) {
+        bias_act_rho<5, false>(X[c], a.b_w1a, h);
+        // padding edge: kPadA (h1 = relu(A + U + V) = 0 in the edge kernels without a validity multiply)
+#pragma unroll
+        for (int t = 0; t < 5; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) X[c][t][r] = src[c] >= 0 ? X[c][t][r] : kPadA;
+    }
+    save(a.A, nullptr, X, true);   // chunk-major (B16: bf16, §3g)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -661,7 +673,8 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // tiles per wave (launched: NC = 1 at two waves per SIMD).
 // NW > 0: the workgroup's 4 waves share each weight image through an LDS ring (tgemm_x6_wg; no
 // early exit, a wave past the last node block runs on the clamped block and stores nothing).
-template <int NC, int NP = 3, int NW = 0>
+// N16 (bf16 math, §3g node side): H2s read and o1 stored as bf16
+template <int NC, int NP = 3, int NW = 0, bool N16 = false>
 __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int nb0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
@@ -686,11 +699,11 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
     f32x16 E[NC][4], O[NC][4];
     zero2(E);
     {
-        HalfRows<kKhE, NC> hr;
-        const float* blk[NC];
+        HalfRowsT<kKhE, NC, N16> hr;
+        int64_t off[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) blk[c] = a.H2s + bE(c);
-        hr.load(blk, lane);
+        for (int c = 0; c < NC; ++c) off[c] = bE(c);
+        hr.load_at(a.H2s, off, lane);
         tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, E, a.x_w3a, lane, wr);
     }
 #pragma unroll
@@ -732,7 +745,10 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         bias_act_rho<4, true>(O[c], a.bo1, h);
-        if (a.o1_out && has[c]) store_cm<4>(a.o1_out + bN(c), O[c], lane, valid[c]);
+        if (a.o1_out && has[c]) {
+            if constexpr (N16) store_cm_b16<4>(reinterpret_cast<uint16_t*>(a.o1_out) + bN(c), O[c], lane, valid[c]);
+            else store_cm<4>(a.o1_out + bN(c), O[c], lane, valid[c]);
+        }
     }
     // X reuses E's registers: x' = o1·Wo2' + b, then P' = tanh(x' + P) into E
     f32x16 (&X)[NC][4] = E;
@@ -819,7 +835,9 @@ struct NodeSumX6 {
         }
     }
     // reg r of tile t: node rho(r, h), feature 32t + (lane&31)
+    template <bool B16 = false>
     __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
+        static_assert(!B16, "bf16 H2s: ≤ 16-node tiles only (NodeSum16X6)");
         const int h = lane >> 5;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -890,6 +908,8 @@ struct NodeSum16X6 {
                         ao, as_bf16x8(make_uint4(P[u][p][0], P[u][p][1], P[u][p][2], P[u][p][3])), acc[2 * t + u], 0, 0, 0);
         }
     }
+    // B16: bf16 at the element index (bf16 math: H2s only ever feeds bf16 MFMA operands, §3g)
+    template <bool B16 = false>
     __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -898,7 +918,10 @@ struct NodeSum16X6 {
 #pragma unroll
                 for (int u = 0; u < 10; ++u) {
                     const int f = 16 * u + (lane & 15);
-                    if (f < 2 * kKhE) H2s[cm_index<kKhE>(n0 + node, f)] = acc[u][r];
+                    if (f < 2 * kKhE) {
+                        if constexpr (B16) store_b16(H2s, cm_index<kKhE>(n0 + node, f), acc[u][r]);
+                        else H2s[cm_index<kKhE>(n0 + node, f)] = acc[u][r];
+                    }
                 }
             }
         }
@@ -911,6 +934,15 @@ struct NodeSum16X6 {
 #ifndef SPWGNN_EFWD_PF
 #define SPWGNN_EFWD_PF 1
 #endif
+#ifndef SPWGNN_EFWD_VMASK   // A/B (diagnosis builds): round 3's per-element h2 validity mask
+#define SPWGNN_EFWD_VMASK 1
+#endif
+#ifndef SPWGNN_EFWD_VF
+#define SPWGNN_EFWD_VF 1
+#endif
+#ifndef SPWGNN_EFWD_NT
+#define SPWGNN_EFWD_NT 0
+#endif
 #ifndef SPWGNN_EFWD_PF_B16
 #define SPWGNN_EFWD_PF_B16 2
 #endif
@@ -919,7 +951,8 @@ struct NodeSum16X6 {
 #endif
 // W8 (≤ 32-node tiles): 8 waves at two per SIMD (256 registers: the 32-node sum and a short ring)
 // instead of 4 at one per SIMD with a 5-k-block ring
-template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false, bool W8 = false>   // AB16: A stored as bf16 (§3g)
+// N16: H2s stored as bf16 (bf16 math, §3g node side)
+template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false, bool W8 = false, bool N16 = false>   // AB16: A stored as bf16 (§3g)
 __global__ __launch_bounds__((NW16 || W8) ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu((NW16 || W8) ? 2 : 1, (NW16 || W8) ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     // bf16 math (NP = 1): a k-block is 5 MFMAs, too short to cover a load one k-block ahead
@@ -951,10 +984,15 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int q = min(2 * kb + c, kKhE / 4 - 1);
-            if constexpr (AB16)
-                r.a[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q));
-            else
-                r.a[c] = *reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
+            // A is read once per step: non-temporal (streaming) loads keep it from evicting the
+            // gathered U/V node rows the tower's other blocks re-read from L2 (SPWGNN_EFWD_NT)
+            if constexpr (AB16) {
+                const uint2* pa = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q);
+                r.a[c] = unpack4_bf16(SPWGNN_EFWD_NT ? ld_nt(pa) : *pa);
+            } else {
+                const float4* pa = reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
+                r.a[c] = SPWGNN_EFWD_NT ? ld_nt(pa) : *pa;
+            }
             r.u[c] = sr.U[64 * q];
             r.v[c] = sr.V[64 * q];
         }
@@ -982,7 +1020,11 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         const int s = cur_sd.x, d = cur_sd.y;
         const bool valid = s >= 0;
         const uint64_t vmask = __ballot(valid);
-        const float vf = valid ? 1.f : 0.f;
+#if SPWGNN_EFWD_VF   // A/B (diagnosis builds): round 3's validity multiply of h1
+        const float kVf = valid ? 1.f : 0.f;
+#else
+        constexpr float kVf = 1.f;
+#endif
         uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         Src nxt;
@@ -994,10 +1036,11 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             float xv[8];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
-                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
-                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
-                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
+                // a padding edge's A rows are kPadA (the encoders): relu gives 0 there
+                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * kVf;
+                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * kVf;
+                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * kVf;
+                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * kVf;
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
@@ -1054,7 +1097,8 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             group(std::integral_constant<int, 3>{}, 2);
         }
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
-        const uint32_t vh = (uint32_t)vmask >> (4 * h);   // bit rho(r, 0): edge rho(r, h) is real
+        // h2 of a padding edge is left as computed: the one-hot receiver sum never matches its index
+        // (−1), and its h2 > 0 bits are cleared on the scalar unit below (edge_ok), not per element
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const float b = a.b2[32 * t + i];
@@ -1062,7 +1106,10 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             for (int r = 0; r < 16; ++r) {
                 float v = relu(acc[t][r] + b);
                 if (t == 4 && i == kDegCol - 128) v = 1.f;  // degree column (multiplies b3)
-                acc[t][r] = mask_bit(v, vh, rho(r, 0));
+#if SPWGNN_EFWD_VMASK
+                v = mask_bit(v, (uint32_t)vmask >> (4 * h), rho(r, 0));
+#endif
+                acc[t][r] = v;
             }
         }
         if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
@@ -1096,6 +1143,13 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
+#if !SPWGNN_EFWD_VMASK
+            // a padding edge's h2 is not masked above: clear its words — word 64k + lane of the block
+            // belongs to edge 8k + (lane >> 3) (m2_pos), real iff that bit of vmask is set
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                mw2[k] = ((vmask >> (8 * k + (lane >> 3))) & 1ull) ? mw2[k] : 0u;
+#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = mw2[k];
         }
@@ -1103,7 +1157,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         cur_sd = nsd;
         cur = nxt;
     }
-    nsum.store(a.H2s, n0, nn, lane);
+    nsum.template store<N16>(a.H2s, n0, nn, lane);
     info = ninfo;
     }
 }
@@ -1166,7 +1220,13 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
     // small batches: a workgroup of five waves per wave-tile, one output tile per wave (kernels_team.hip)
-    if ((math == MATH_X6 || math == MATH_BF16) && a.nw_max <= 16 && team_blocks(a.n_wtiles)) return launch_edge_fwd_team(a, math, st);
+    if ((math == MATH_X6 || math == MATH_BF16) && a.nw_max <= 16 && team_blocks(a.n_wtiles))
+        return a.n16 ? hipErrorInvalidValue : launch_edge_fwd_team(a, math, st);   // team kernels: fp32 H2s
+    if (a.n16 && (math != MATH_BF16 || a.nw_max > 16 || !a.a_b16)) return hipErrorInvalidValue;
+    if (math == MATH_BF16 && a.n16) {
+        hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1, true, false, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+        return hipGetLastError();
+    }
     if (math == MATH_BF16) {
 #ifdef SPWGNN_DIAG   // 1: A rows from 8 cached blocks; 3: U, V rows of the tile's first node (wrong results)
         static const int bdbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;
@@ -1215,7 +1275,9 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st) {
-    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks((a.n_nodes + 31) / 32)) return launch_node_fwd_team(a, math, st);
+    if ((math == MATH_X6 || math == MATH_BF16) && team_blocks((a.n_nodes + 31) / 32))
+        return a.n16 ? hipErrorInvalidValue : launch_node_fwd_team(a, math, st);   // team kernels: fp32 arrays
+    if (a.n16 && math != MATH_BF16) return hipErrorInvalidValue;
     const int waves = (a.n_nodes + 31) / 32;
     if (math == MATH_X6) {
         // one 32-node column tile per wave at two waves per SIMD (measured: 0.58 vs 0.62 ms for
@@ -1227,7 +1289,8 @@ hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st) {
         return hipGetLastError();
     }
     if (math == MATH_BF16) {
-        hipLaunchKernelGGL((k_node_fwd_x6<1, 1, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        if (a.n16) hipLaunchKernelGGL((k_node_fwd_x6<1, 1, 4, true>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_node_fwd_x6<1, 1, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_node_fwd, dim3((waves + 3) / 4), dim3(256), 0, st, a);

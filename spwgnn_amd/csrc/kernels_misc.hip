@@ -1008,8 +1008,16 @@ struct WsSet4 {
 // B16 (bf16 math, §3g): X (kB16X) and/or Y (kB16Y) stored as bf16 with the fp32 element layout.
 // The body of one workgroup `bid` of a weight gradient; smem: two stage buffers of W::BUF bytes
 // (k_wgrad_ws: its own; k_wgrad_ws_batch: the largest variant's, shared by every job of the batch).
+// SPWGNN_WS_DBG (diagnosis builds, wrong results, timing only): 1 staging without global loads,
+// 2 staging without the split (raw bits into the three part images), 3 staging without LDS writes,
+// 4 matrix waves without MFMAs (fragment reads kept), 5 matrix waves without fragment reads (MFMAs on
+// constant fragments), 6 staging waves idle (barriers only)
+#ifndef SPWGNN_WS_DBG
+#define SPWGNN_WS_DBG 0
+#endif
 template <int KXP, int NYP, int YROW, bool MASK, int NP, int XD, int B16>
 __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* smem) {
+    constexpr int DBG = SPWGNN_WS_DBG;
     using W = WsStage<KXP, NYP, YROW, MASK>;
     using IX = X6Img<KXP>;
     using IY = X6Img<NYP>;
@@ -1034,26 +1042,50 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
 #pragma unroll
         for (int y = 0; y < MY; ++y) oy[y] = IY::roff(lane, MY * wy + y);
         __syncthreads();
+        // diagnosis forms: the products, or the fragment reads, taken away
+        auto mm = [&](const bf16x8 (&xf)[3], const bf16x8 (&yf)[3], f32x4 c) {
+            if constexpr (DBG == 4) {
+                c[0] += __builtin_bit_cast(f32x4, xf[0])[0] + __builtin_bit_cast(f32x4, yf[0])[1];
+                return c;
+            } else {
+                return mfma16_x6<NP>(xf, yf, c);
+            }
+        };
+        auto getx = [&](const char* Xs, int off, bf16x8 (&f)[3]) {
+            if constexpr (DBG != 5) IX::template get<NP>(Xs, off, f);
+        };
+        auto gety = [&](const char* Ys, int off, bf16x8 (&f)[3]) {
+            if constexpr (DBG != 5) IY::template get<NP>(Ys, off, f);
+        };
+        bf16x8 yb[MY][3], xa[2][3];
+        if constexpr (DBG == 5) {
+            const uint32_t k = 0x3f803f80u ^ (uint32_t)lane;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                xa[0][p] = xa[1][p] = as_bf16x8(make_uint4(k, k, k, k));
+#pragma unroll
+                for (int y = 0; y < MY; ++y) yb[y][p] = as_bf16x8(make_uint4(k, k + 1, k, k));
+            }
+        }
         for (int t = 0; t < T; ++t) {
             const char* Xs = buf(t & 1);
             const char* Ys = Xs + W::IMX;
-            bf16x8 yb[MY][3], xa[2][3];
-            IX::template get<NP>(Xs, ox[0], xa[0]);
-            IY::template get<NP>(Ys, oy[0], yb[0]);
+            getx(Xs, ox[0], xa[0]);
+            gety(Ys, oy[0], yb[0]);
 #pragma unroll
             for (int y = 0; y < MY; ++y) {
-                if (y + 1 < MY) IY::template get<NP>(Ys, oy[y + 1], yb[y + 1]);
-                else IX::template get<NP>(Xs, ox[1], xa[1]);
+                if (y + 1 < MY) gety(Ys, oy[y + 1], yb[y + 1]);
+                else getx(Xs, ox[1], xa[1]);
                 __builtin_amdgcn_sched_barrier(0);
-                acc[0][y] = mfma16_x6<NP>(xa[0], yb[y], acc[0][y]);
+                acc[0][y] = mm(xa[0], yb[y], acc[0][y]);
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int x = 1; x < MX; ++x) {
-                if (x + 1 < MX) IX::template get<NP>(Xs, ox[x + 1], xa[(x + 1) & 1]);
+                if (x + 1 < MX) getx(Xs, ox[x + 1], xa[(x + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int y = 0; y < MY; ++y) acc[x][y] = mfma16_x6<NP>(xa[x & 1], yb[y], acc[x][y]);
+                for (int y = 0; y < MY; ++y) acc[x][y] = mm(xa[x & 1], yb[y], acc[x][y]);
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
@@ -1102,6 +1134,16 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
         }
     }
     auto fetch = [&](int t, WsSet4& R) {
+        if constexpr (DBG == 1 || DBG == 6) {   // diagnosis: no global loads
+            const float c = (float)(rr + t);
+            R.nvalid = 32;
+            R.d = make_float2(c, c + 1.f);
+#pragma unroll
+            for (int k = 0; k < W::NKX; ++k) R.x[k] = make_float4(c, c + 1.f, c + 2.f, c + 3.f);
+#pragma unroll
+            for (int k = 0; k < W::NKY; ++k) R.y[k] = make_float4(c, c - 1.f, c - 2.f, c - 3.f);
+            return;
+        }
         const int64_t tg = t0 + (t < T ? t : T - 1);
         const int64_t s = tg / a.nbs, nb = tg - s * a.nbs;
         if (MASK) R.nvalid = (int)min<int64_t>(32, a.count - nb * 32);
@@ -1109,8 +1151,11 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
         const int64_t iy = YROW ? ((s * a.y_sb + nb) * 32 + yr) * 160 : (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
         const float* px = a.x + ix;
         const float* py = a.y + iy;
-        const uint16_t* hx = reinterpret_cast<const uint16_t*>(a.x) + ix;
-        const uint16_t* hy = reinterpret_cast<const uint16_t*>(a.y) + iy;
+        // bf16 storage: a per-step array's step s starts where its fp32 step starts (the producers write
+        // through per-step pointers), the element index runs within the step
+        const int64_t sx = s * a.x_sb * (W::KHX * 64), sy = YROW ? 0 : s * a.y_sb * (W::KHY * 64);
+        const uint16_t* hx = reinterpret_cast<const uint16_t*>(a.x + sx) + (ix - sx);
+        const uint16_t* hy = reinterpret_cast<const uint16_t*>(a.y + sy) + (iy - sy);
         if (XD == 1) {
             R.d = a.xd[(s * a.x_sb + nb) * 32 + rr];
         } else if (XD == 2) {
@@ -1127,7 +1172,40 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             R.y[k] = (B16 & kB16Y) ? unpack4_bf16(*reinterpret_cast<const uint2*>(hy + offy[k]))
                                    : *reinterpret_cast<const float4*>(py + offy[k]);
     };
+    uint32_t dbg_sink = 0u;
+    // diagnosis forms of the image writes: raw bits into the parts (no split), or no LDS writes
+    auto putx = [&](char* S, int row, int c4, float4 v) {
+        if constexpr (DBG == 2) {
+            char* p = S + IX::woff(row, c4);
+            const uint2 u = make_uint2(__float_as_uint(v.x) ^ __float_as_uint(v.y), __float_as_uint(v.z) ^ __float_as_uint(v.w));
+            *reinterpret_cast<uint2*>(p) = u;
+            if constexpr (NP == 3) { *reinterpret_cast<uint2*>(p + IX::PART) = u; *reinterpret_cast<uint2*>(p + 2 * IX::PART) = u; }
+        } else if constexpr (DBG == 3) {
+            uint32_t h0, m0, l0, h1, m1, l1;
+            split2(v.x, v.y, h0, m0, l0);
+            split2(v.z, v.w, h1, m1, l1);
+            dbg_sink ^= h0 ^ h1 ^ (NP == 3 ? (m0 ^ l0 ^ m1 ^ l1) : 0u);
+        } else {
+            IX::template put<NP>(S, row, c4, v);
+        }
+    };
+    auto puty = [&](char* S, int row, int c4, float4 v) {
+        if constexpr (DBG == 2) {
+            char* p = S + IY::woff(row, c4);
+            const uint2 u = make_uint2(__float_as_uint(v.x) ^ __float_as_uint(v.y), __float_as_uint(v.z) ^ __float_as_uint(v.w));
+            *reinterpret_cast<uint2*>(p) = u;
+            if constexpr (NP == 3) { *reinterpret_cast<uint2*>(p + IY::PART) = u; *reinterpret_cast<uint2*>(p + 2 * IY::PART) = u; }
+        } else if constexpr (DBG == 3) {
+            uint32_t h0, m0, l0, h1, m1, l1;
+            split2(v.x, v.y, h0, m0, l0);
+            split2(v.z, v.w, h1, m1, l1);
+            dbg_sink ^= h0 ^ h1 ^ (NP == 3 ? (m0 ^ l0 ^ m1 ^ l1) : 0u);
+        } else {
+            IY::template put<NP>(S, row, c4, v);
+        }
+    };
     auto build = [&](const WsSet4& R, char* Xs) {
+        if constexpr (DBG == 6) return;
         char* Ys = Xs + W::IMX;
         const bool xin = !MASK || rr < R.nvalid, yin = !MASK || yr < R.nvalid;
 #pragma unroll
@@ -1144,14 +1222,14 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             }
             if (MASK && !xin) v = f4zero();
             if (k == ones_k) f4set(v, ones_c, xin ? 1.f : 0.f);
-            IX::template put<NP>(Xs, rr, c0 + 8 * k, v);
+            putx(Xs, rr, c0 + 8 * k, v);
         }
 #pragma unroll
         for (int k = 0; k < W::NKY; ++k) {
             if (!yk_ok(k)) break;
             float4 v = R.y[k];
             if (MASK && !yin) v = f4zero();
-            IY::template put<NP>(Ys, yr, yc0 + 8 * k, v);
+            puty(Ys, yr, yc0 + 8 * k, v);
         }
     };
     if (T == 0) {
@@ -1203,6 +1281,9 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
         __syncthreads();
         ++t;
     }
+    if constexpr (DBG == 3) {   // keep the diagnosis split alive
+        if (dbg_sink == 0x9e3779b9u) a.slab[0] = 0.f;
+    }
     __syncthreads();
 }
 
@@ -1250,6 +1331,9 @@ void k_wgrad_ws_batch(WsBatch b) {
                     case WSV_XD_EDGE_B16Y: wgrad_ws_body<160, 160, 0, false, 1, 1, kB16Y>(job.a, bid, smem); break;
                     case WSV_160_160_ROW_B16: wgrad_ws_body<160, 160, 1, false, 1, 0, kB16X | kB16Y>(job.a, bid, smem); break;
                     case WSV_160_160_B16: wgrad_ws_body<160, 160, 0, false, 1, 0, kB16X | kB16Y>(job.a, bid, smem); break;
+                    case WSV_128_160_B16Y: wgrad_ws_body<128, 160, 0, true, 1, 0, kB16Y>(job.a, bid, smem); break;
+                    case WSV_160_128_B16: wgrad_ws_body<160, 128, 0, true, 1, 0, kB16X | kB16Y>(job.a, bid, smem); break;
+                    case WSV_128_128_B16: wgrad_ws_body<128, 128, 0, true, 1, 0, kB16X | kB16Y>(job.a, bid, smem); break;
                     default: break;
                 }
             }
@@ -1606,8 +1690,15 @@ int wgrad_ws_variant(const WgWsArgs& a, int kx_pad, int ny_pad, int yrow, int ma
         return WSV_XD_NODE;
     }
     if (b16) {   // the encoder-side edge operands of bf16 math (rm.2, rm.3: X, Y; W1a: X = c_r, Y = dA rows)
-        if (kx_pad != 160 || ny_pad != 160 || mask || b16 != (kB16X | kB16Y)) return WSV_NONE;
-        return yrow ? WSV_160_160_ROW_B16 : WSV_160_160_B16;
+        if (kx_pad == 160 && ny_pad == 160 && !mask && b16 == (kB16X | kB16Y))
+            return yrow ? WSV_160_160_ROW_B16 : WSV_160_160_B16;
+        // node side (§3g): W1b/W1c (Y = dU/dV), W3 (X = H2s, Y = g), omp.1 (X = o1, Y = dx)
+        if (!yrow && mask) {
+            if (kx_pad == 128 && ny_pad == 160 && b16 == kB16Y) return WSV_128_160_B16Y;
+            if (kx_pad == 160 && ny_pad == 128 && b16 == (kB16X | kB16Y)) return WSV_160_128_B16;
+            if (kx_pad == 128 && ny_pad == 128 && b16 == (kB16X | kB16Y)) return WSV_128_128_B16;
+        }
+        return WSV_NONE;
     }
     const bool mk = mask != 0;
     if (kx_pad == 160 && ny_pad == 160 && !mk) return yrow ? WSV_160_160_ROW : WSV_160_160;
@@ -1640,6 +1731,9 @@ hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, i
         case WSV_XD_EDGE_B16Y: hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 1, kB16Y>), g, b, 0, st, a); break;
         case WSV_160_160_ROW_B16: hipLaunchKernelGGL((k_wgrad_ws<160, 160, 1, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a); break;
         case WSV_160_160_B16: hipLaunchKernelGGL((k_wgrad_ws<160, 160, 0, false, 1, 0, kB16X | kB16Y>), g, b, 0, st, a); break;
+        case WSV_128_160_B16Y: hipLaunchKernelGGL((k_wgrad_ws<128, 160, 0, true, 1, 0, kB16Y>), g, b, 0, st, a); break;
+        case WSV_160_128_B16: hipLaunchKernelGGL((k_wgrad_ws<160, 128, 0, true, 1, 0, kB16X | kB16Y>), g, b, 0, st, a); break;
+        case WSV_128_128_B16: hipLaunchKernelGGL((k_wgrad_ws<128, 128, 0, true, 1, 0, kB16X | kB16Y>), g, b, 0, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
