@@ -110,18 +110,6 @@ __device__ __forceinline__ i16x4 lds_tr16(const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
 }
 
-// non-temporal (streaming) global loads: data read once, kept from displacing re-read rows in L2
-__device__ __forceinline__ float4 ld_nt(const float4* p) {
-    typedef float v4 __attribute__((ext_vector_type(4)));
-    const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
-    return make_float4(v[0], v[1], v[2], v[3]);
-}
-__device__ __forceinline__ uint2 ld_nt(const uint2* p) {
-    typedef unsigned v2 __attribute__((ext_vector_type(2)));
-    const v2 v = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p));
-    return make_uint2(v[0], v[1]);
-}
-
 __device__ __forceinline__ f32x16 zero16() {
     f32x16 z;
 #pragma unroll

@@ -273,12 +273,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     zero_tiles(X);
     tchain_acc<5, 5, 12, kLdE>(Y, X, a.w_w1a, lane);
     bias_act_rho<5, false>(X, a.b_w1a, h);
-    if (!valid)   // padding edge: kPadA (h1 = relu(A + U + V) = 0 without a validity multiply)
-#pragma unroll
-        for (int t = 0; t < 5; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) X[t][r] = kPadA;
-    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, true);   // chunk-major
+    store_cm<5>(a.A + (int64_t)blk * kCmBlk, X, lane, true);   // chunk-major; k_edge_fwd masks padding edges
 }
 
 // The rm encoder in split-bf16 math: NC 32-edge blocks per wave (column tiles c). Launched with
@@ -366,15 +361,8 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_x6(EncEdgeArg
     zero2(X);
     tchain_x6s<5, 10, 5, NC, kX6Ring, NP, NW>(Y, X, a.x_w1a, lane, wr);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        bias_act_rho<5, false>(X[c], a.b_w1a, h);
-        // padding edge: kPadA (h1 = relu(A + U + V) = 0 in the edge kernels without a validity multiply)
-#pragma unroll
-        for (int t = 0; t < 5; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) X[c][t][r] = src[c] >= 0 ? X[c][t][r] : kPadA;
-    }
-    save(a.A, nullptr, X, true);   // chunk-major (B16: bf16, §3g)
+    for (int c = 0; c < NC; ++c) bias_act_rho<5, false>(X[c], a.b_w1a, h);
+    save(a.A, nullptr, X, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -673,7 +661,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // tiles per wave (launched: NC = 1 at two waves per SIMD).
 // NW > 0: the workgroup's 4 waves share each weight image through an LDS ring (tgemm_x6_wg; no
 // early exit, a wave past the last node block runs on the clamped block and stores nothing).
-// N16 (bf16 math, §3g node side): H2s read and o1 stored as bf16
+// N16 (bf16 math, §3o): H2s read and o1 stored as bf16
 template <int NC, int NP = 3, int NW = 0, bool N16 = false>
 __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
@@ -908,7 +896,7 @@ struct NodeSum16X6 {
                         ao, as_bf16x8(make_uint4(P[u][p][0], P[u][p][1], P[u][p][2], P[u][p][3])), acc[2 * t + u], 0, 0, 0);
         }
     }
-    // B16: bf16 at the element index (bf16 math: H2s only ever feeds bf16 MFMA operands, §3g)
+    // B16: bf16 at the element index (bf16 math: H2s only ever feeds bf16 MFMA operands, §3o)
     template <bool B16 = false>
     __device__ __forceinline__ void store(float* H2s, int n0, int nn, int lane) const {
 #pragma unroll
@@ -934,15 +922,6 @@ struct NodeSum16X6 {
 #ifndef SPWGNN_EFWD_PF
 #define SPWGNN_EFWD_PF 1
 #endif
-#ifndef SPWGNN_EFWD_VMASK   // A/B (diagnosis builds): round 3's per-element h2 validity mask
-#define SPWGNN_EFWD_VMASK 1
-#endif
-#ifndef SPWGNN_EFWD_VF
-#define SPWGNN_EFWD_VF 1
-#endif
-#ifndef SPWGNN_EFWD_NT
-#define SPWGNN_EFWD_NT 0
-#endif
 #ifndef SPWGNN_EFWD_PF_B16
 #define SPWGNN_EFWD_PF_B16 2
 #endif
@@ -951,7 +930,7 @@ struct NodeSum16X6 {
 #endif
 // W8 (≤ 32-node tiles): 8 waves at two per SIMD (256 registers: the 32-node sum and a short ring)
 // instead of 4 at one per SIMD with a 5-k-block ring
-// N16: H2s stored as bf16 (bf16 math, §3g node side)
+// N16: H2s stored as bf16 (bf16 math, §3o)
 template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false, bool W8 = false, bool N16 = false>   // AB16: A stored as bf16 (§3g)
 __global__ __launch_bounds__((NW16 || W8) ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu((NW16 || W8) ? 2 : 1, (NW16 || W8) ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
@@ -984,15 +963,10 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int q = min(2 * kb + c, kKhE / 4 - 1);
-            // A is read once per step: non-temporal (streaming) loads keep it from evicting the
-            // gathered U/V node rows the tower's other blocks re-read from L2 (SPWGNN_EFWD_NT)
-            if constexpr (AB16) {
-                const uint2* pa = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q);
-                r.a[c] = unpack4_bf16(SPWGNN_EFWD_NT ? ld_nt(pa) : *pa);
-            } else {
-                const float4* pa = reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
-                r.a[c] = SPWGNN_EFWD_NT ? ld_nt(pa) : *pa;
-            }
+            if constexpr (AB16)
+                r.a[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q));
+            else
+                r.a[c] = *reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
             r.u[c] = sr.U[64 * q];
             r.v[c] = sr.V[64 * q];
         }
@@ -1020,11 +994,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         const int s = cur_sd.x, d = cur_sd.y;
         const bool valid = s >= 0;
         const uint64_t vmask = __ballot(valid);
-#if SPWGNN_EFWD_VF   // A/B (diagnosis builds): round 3's validity multiply of h1
-        const float kVf = valid ? 1.f : 0.f;
-#else
-        constexpr float kVf = 1.f;
-#endif
+        const float vf = valid ? 1.f : 0.f;
         uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         Src nxt;
@@ -1036,11 +1006,10 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             float xv[8];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                // a padding edge's A rows are kPadA (the encoders): relu gives 0 there
-                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * kVf;
-                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * kVf;
-                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * kVf;
-                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * kVf;
+                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
+                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
+                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
+                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
@@ -1097,8 +1066,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             group(std::integral_constant<int, 3>{}, 2);
         }
         if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
-        // h2 of a padding edge is left as computed: the one-hot receiver sum never matches its index
-        // (−1), and its h2 > 0 bits are cleared on the scalar unit below (edge_ok), not per element
+        const uint32_t vh = (uint32_t)vmask >> (4 * h);   // bit rho(r, 0): edge rho(r, h) is real
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const float b = a.b2[32 * t + i];
@@ -1106,10 +1074,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             for (int r = 0; r < 16; ++r) {
                 float v = relu(acc[t][r] + b);
                 if (t == 4 && i == kDegCol - 128) v = 1.f;  // degree column (multiplies b3)
-#if SPWGNN_EFWD_VMASK
-                v = mask_bit(v, (uint32_t)vmask >> (4 * h), rho(r, 0));
-#endif
-                acc[t][r] = v;
+                acc[t][r] = mask_bit(v, vh, rho(r, 0));
             }
         }
         if (a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
@@ -1143,13 +1108,6 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-#if !SPWGNN_EFWD_VMASK
-            // a padding edge's h2 is not masked above: clear its words — word 64k + lane of the block
-            // belongs to edge 8k + (lane >> 3) (m2_pos), real iff that bit of vmask is set
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                mw2[k] = ((vmask >> (8 * k + (lane >> 3))) & 1ull) ? mw2[k] : 0u;
-#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = mw2[k];
         }

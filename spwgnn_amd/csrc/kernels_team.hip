@@ -280,10 +280,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_team(EncEdgeArgs a)
             }
         }
         if (l == 3) {
-            if (src < 0)   // padding edge: kPadA (the wide edge forward relies on it, §3h)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) x[r] = kPadA;
-            save(a.A, -1, x, true);   // chunk-major (B16: bf16, §3g)
+            save(a.A, -1, x, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
         } else {
             if (TRAIN) save(l == 0 ? a.z2 : l == 1 ? a.z3 : a.cr, l + 1, x, true);
             act.put((l + 1) & 1, T, x, lane);

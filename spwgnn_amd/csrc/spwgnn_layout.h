@@ -15,9 +15,6 @@ constexpr int kKhE = 76;    // split-halves contraction: features [76h, 76h+76),
 constexpr int kKhN = 52;    // split-halves contraction for 100-wide inputs (104 = 100 + 4 zero)
 constexpr int kNwMaxLimit = 32;   // max nodes per wave-tile (LDS node accumulators)
 constexpr int kDegCol = 150;      // H2s column 150 holds the in-degree (multiplies the rmp.2 bias)
-// A (= c_r·W1a + b1) of a padding edge (index −1): so negative that h1 = relu(A + U + V) is 0 for any
-// finite node rows — the edge kernels need no per-element validity multiply (representable in bf16)
-constexpr float kPadA = -3.0e38f;
 
 // ---- chunk-major edge rows ("CM"): a 32-edge block of 152-wide rows stored as
 // [q < 19][h < 2][edge i < 32][4] — feature f = 76h + 4q + c. A wave's 16-byte-per-lane access in
