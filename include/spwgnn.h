@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 2
+#define SPWGNN_ABI_VERSION 3   /* 3: spwgnn_batch.flags, receiver-block plans */
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -96,14 +96,27 @@ int32_t spwgnn_plan_fill_cap(int32_t n_towers, const int32_t* tower_nodes, const
                              const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src, int32_t* edge_dst,
                              int32_t* edge_id, uint8_t* blk_csr);
 
+/* Receiver blocks: every node of a wave-tile owns ONE 32-edge block that holds its in-edges (≤ 32
+ * per node; input order within a receiver; nodes without in-edges get an all-padding block), so
+ * wtile[w] = (first block, #nodes, first node, #nodes) and block first_block + j feeds node
+ * first_node + j alone. Set SPWGNN_BATCH_RECV_BLOCKS in spwgnn_batch.flags for such a plan: the
+ * x6 edge forward then sums each block's messages as one column sum instead of a one-hot product
+ * (large fully connected towers, BASELINE config 5). Every other kernel takes either layout. */
+int32_t spwgnn_plan_size_recv(int32_t n_towers, const int32_t* tower_nodes, int32_t nw_max, spwgnn_plan_sizes* out);
+int32_t spwgnn_plan_fill_recv(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                              const int32_t* src, const int32_t* dst, int32_t nw_max, const spwgnn_plan_sizes* sizes,
+                              int32_t* wtile, int32_t* edge_src, int32_t* edge_dst, int32_t* edge_id,
+                              uint8_t* blk_csr);
+
 /* ------------------------------------------------------------------- device batch ------- */
+#define SPWGNN_BATCH_RECV_BLOCKS 1   /* spwgnn_batch.flags: the plan is a receiver-block plan */
 typedef struct spwgnn_batch {
     int32_t n_towers;
     int32_t n_nodes;        /* Σ N over towers */
     int32_t n_wtiles;
     int32_t n_eblocks;
     int32_t nw_max;
-    int32_t pad0;
+    int32_t flags;          /* SPWGNN_BATCH_* (0: a plan of spwgnn_plan_fill / _fill_cap)      */
     const float* pos;           /* [n_nodes][4]: objects (x, y, w)/170 + 0 pad (Networks.py:22)   */
     const float* prop;          /* [n_nodes][100] 'propagation' input (Networks.py:29); NULL = 0  */
     const int32_t* node_tower;  /* [n_nodes] tower id (dropout key)                                */

@@ -29,7 +29,7 @@ class PlanSizes(C.Structure):
 class BatchC(C.Structure):
     _fields_ = [
         ("n_towers", C.c_int32), ("n_nodes", C.c_int32), ("n_wtiles", C.c_int32), ("n_eblocks", C.c_int32),
-        ("nw_max", C.c_int32), ("pad0", C.c_int32),
+        ("nw_max", C.c_int32), ("flags", C.c_int32),
         ("pos", C.c_void_p), ("prop", C.c_void_p), ("node_tower", C.c_void_p), ("node_local", C.c_void_p),
         ("wtile", C.c_void_p), ("edge_src", C.c_void_p), ("edge_dst", C.c_void_p), ("blk_csr", C.c_void_p),
     ]
@@ -45,7 +45,8 @@ K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WG
 K_WGRAD_WS, K_ENC_NODE, K_ENC_NODE_BWD = 9, 10, 11
 MATH_F32, MATH_X6, MATH_BF16 = 0, 1, 2
 STEP_KEY_COUNTER, STEP_KEY_SPLITMIX = 0, 1
-ABI_VERSION = 2        # SPWGNN_ABI_VERSION this binding's structs follow
+ABI_VERSION = 3        # SPWGNN_ABI_VERSION this binding's structs follow
+BATCH_RECV_BLOCKS = 1  # spwgnn_batch.flags: a receiver-block plan (spwgnn_plan_fill_recv)
 READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 
 
@@ -64,6 +65,8 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_plan_fill": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
         "spwgnn_plan_size_cap": (i32, [i32, vp, vp, i32, C.POINTER(PlanSizes)]),
         "spwgnn_plan_fill_cap": (i32, [i32, vp, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
+        "spwgnn_plan_size_recv": (i32, [i32, vp, i32, C.POINTER(PlanSizes)]),
+        "spwgnn_plan_fill_recv": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
         "spwgnn_workspace_bytes": (i64, [i32, i32, i32, i32]),
         "spwgnn_forward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp]),
         "spwgnn_backward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp, vp, vp]),

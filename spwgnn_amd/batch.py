@@ -84,16 +84,21 @@ class HostPlan:
     node_shape: Optional[tuple]
     has_prop: bool
     arrays: list
+    flags: int = 0     # spwgnn_batch.flags (_lib.BATCH_RECV_BLOCKS: a receiver-block plan)
 
     @property
     def geometry(self) -> tuple:
-        """What a captured step bakes in: sizes and every array's shape."""
-        return (self.n_towers, self.n_nodes, self.n_wtiles, self.n_eblocks, self.nw_max, self.has_prop,
+        """What a captured step bakes in: sizes, layout flags and every array's shape."""
+        return (self.n_towers, self.n_nodes, self.n_wtiles, self.n_eblocks, self.nw_max, self.has_prop, self.flags,
                 tuple(a.shape for a in self.arrays))
 
     @staticmethod
     def build(pos, tower_nodes, src, dst, tower_edges, prop=None, nw_max=None, node_shape=None, tower_ids=None,
-              edge_cap=None) -> "HostPlan":
+              edge_cap=None, recv_blocks=None) -> "HostPlan":
+        """recv_blocks: one 32-edge block per node holding its in-edges (spwgnn_plan_fill_recv; the x6
+        edge forward then sums a node's messages as a column sum). None = automatic: for wave-tiles of
+        more than 16 nodes whose blocks would be ≥ 80 % full (large, densely connected towers —
+        BASELINE config 5), never with edge_cap."""
         L = _lib.lib()
         tower_nodes = np.ascontiguousarray(tower_nodes, dtype=np.int32)
         tower_edges = np.ascontiguousarray(tower_edges, dtype=np.int32)
@@ -111,13 +116,20 @@ class HostPlan:
             nw_max = default_nw_max(int(tower_nodes.max()) if T else 1, T)
         if T and int(tower_nodes.max()) > _NW_LIMIT:
             raise ValueError(f"towers of more than {_NW_LIMIT} nodes are not supported by this build")
+        if recv_blocks is None:
+            recv_blocks = (edge_cap is None and nw_max > 16 and len(src) > 0 and Nn * 32 <= 1.25 * len(src)
+                           and int(np.bincount(dst, minlength=Nn).max()) <= 32)
+        if recv_blocks and edge_cap is not None:
+            raise ValueError("receiver-block plans do not take edge capacities")
         cap = None
         if edge_cap is not None:
             cap = np.ascontiguousarray(np.broadcast_to(np.asarray(edge_cap, np.int32), (T,)), dtype=np.int32)
             if np.any(cap < tower_edges):
                 raise ValueError("edge_cap must be >= every tower's edge count")
         sizes = _lib.PlanSizes()
-        if cap is None:
+        if recv_blocks:
+            _lib.check(L.spwgnn_plan_size_recv(T, _ptr(tower_nodes), nw_max, C.byref(sizes)), "plan_size_recv")
+        elif cap is None:
             _lib.check(L.spwgnn_plan_size(T, _ptr(tower_nodes), _ptr(tower_edges), nw_max, C.byref(sizes)), "plan_size")
         else:
             _lib.check(L.spwgnn_plan_size_cap(T, _ptr(tower_nodes), _ptr(cap), nw_max, C.byref(sizes)), "plan_size_cap")
@@ -128,7 +140,10 @@ class HostPlan:
         csr = np.zeros((sizes.n_eblocks, 128), np.uint8)
         sp = _ptr(src) if len(src) else None
         dp = _ptr(dst) if len(dst) else None
-        if cap is None:
+        if recv_blocks:
+            _lib.check(L.spwgnn_plan_fill_recv(T, _ptr(tower_nodes), _ptr(tower_edges), sp, dp, nw_max, C.byref(sizes),
+                                               _ptr(wtile), _ptr(esrc), _ptr(edst), _ptr(eid), _ptr(csr)), "plan_fill_recv")
+        elif cap is None:
             _lib.check(L.spwgnn_plan_fill(T, _ptr(tower_nodes), _ptr(tower_edges), sp, dp, nw_max, C.byref(sizes),
                                           _ptr(wtile), _ptr(esrc), _ptr(edst), _ptr(eid), _ptr(csr)), "plan_fill")
         else:
@@ -147,7 +162,7 @@ class HostPlan:
         if prop is not None:
             host.append(np.asarray(prop, np.float32).reshape(Nn, 100))
         return HostPlan(T, Nn, tower_nodes, tower_edges, src, dst, sizes.n_wtiles, sizes.n_eblocks, sizes.nw_max,
-                        eid, node_shape, prop is not None, host)
+                        eid, node_shape, prop is not None, host, _lib.BATCH_RECV_BLOCKS if recv_blocks else 0)
 
 
 @dataclass
@@ -172,6 +187,7 @@ class TowerBatch:
     blk_csr: torch.Tensor
     edge_id: np.ndarray              # (n_eblocks*32,) original edge index or -1
     node_shape: Optional[tuple] = None   # (B, N) when built from a uniform-N dense batch
+    flags: int = 0                       # spwgnn_batch.flags (the plan's layout)
     _cstruct: Optional[_lib.BatchC] = field(default=None, repr=False)
 
     @property
@@ -191,14 +207,16 @@ class TowerBatch:
     # ------------------------------------------------------------------ constructors
     @staticmethod
     def from_edges(pos: np.ndarray, tower_nodes, src, dst, tower_edges, prop=None, device="cuda",
-                   nw_max: Optional[int] = None, node_shape=None, tower_ids=None, edge_cap=None) -> "TowerBatch":
+                   nw_max: Optional[int] = None, node_shape=None, tower_ids=None, edge_cap=None,
+                   recv_blocks=None) -> "TowerBatch":
         """pos (Nn, >=3) objects rows (already /170); towers are consecutive node ranges;
         edges tower-major with global node ids. `tower_ids` (T,): each tower's index in the batch it
         was cut from (the dropout masks are keyed by it), so a shard or micro-batch of a larger batch
         draws the masks the whole batch would; default 0..T-1. `edge_cap` (T,) ≥ tower_edges: size
         each tower's blocks for that many edges (spwgnn_plan_fill_cap) so same-shape batches share
         one plan geometry (replayed hipGraph steps); default: the actual edge counts."""
-        plan = HostPlan.build(pos, tower_nodes, src, dst, tower_edges, prop, nw_max, node_shape, tower_ids, edge_cap)
+        plan = HostPlan.build(pos, tower_nodes, src, dst, tower_edges, prop, nw_max, node_shape, tower_ids, edge_cap,
+                              recv_blocks)
         return TowerBatch.from_plan(plan, device)
 
     @staticmethod
@@ -210,7 +228,8 @@ class TowerBatch:
         m = plan
         prop_t = d[7] if m.has_prop else None
         return TowerBatch(m.n_towers, m.n_nodes, m.tower_nodes, m.tower_edges, m.src, m.dst, m.n_wtiles, m.n_eblocks,
-                          m.nw_max, dev, d[0], prop_t, d[1], d[2], d[3], d[4], d[5], d[6], m.edge_id, m.node_shape)
+                          m.nw_max, dev, d[0], prop_t, d[1], d[2], d[3], d[4], d[5], d[6], m.edge_id, m.node_shape,
+                          m.flags)
 
     @staticmethod
     def from_dense(objects, sender_relations, receiver_relations, propagation=None, device="cuda",
@@ -243,7 +262,7 @@ class TowerBatch:
 
     @staticmethod
     def fully_connected(objects: np.ndarray, propagation=None, device="cuda", nw_max=None,
-                        tower_ids=None) -> "TowerBatch":
+                        tower_ids=None, recv_blocks=None) -> "TowerBatch":
         """Fast path for (B, N, 3) towers whose relations are all active (the inference relation
         set of JengaBuilder.py:309-326 and the benchmark configs)."""
         obj = np.asarray(objects, np.float32)
@@ -255,7 +274,7 @@ class TowerBatch:
         prop = None if propagation is None else np.asarray(propagation, np.float32).reshape(B * N, 100)
         return TowerBatch.from_edges(obj.reshape(B * N, 3), np.full(B, N, np.int32), src, dst,
                                      np.full(B, N * (N - 1), np.int32), prop, device, nw_max, node_shape=(B, N),
-                                     tower_ids=tower_ids)
+                                     tower_ids=tower_ids, recv_blocks=recv_blocks)
 
     @staticmethod
     def ragged(objects_list, relation_threshold: Optional[float] = None, device="cuda", nw_max=None,
@@ -289,6 +308,7 @@ class TowerBatch:
             b = _lib.BatchC()
             b.n_towers, b.n_nodes = self.n_towers, self.n_nodes
             b.n_wtiles, b.n_eblocks, b.nw_max = self.n_wtiles, self.n_eblocks, self.nw_max
+            b.flags = self.flags
             b.pos = self.pos.data_ptr()
             b.prop = self.prop.data_ptr() if self.prop is not None else None
             b.node_tower = self.node_tower.data_ptr()

@@ -446,6 +446,9 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
         ef.a_b16 = store_b16(r, b);
         ef.n16 = store_b16_node(r, b);
+        ef.n_nodes = b->n_nodes;
+        ef.recv_blocks = (b->flags & SPWGNN_BATCH_RECV_BLOCKS) && kmath(r, kX6EdgeFwd) == MATH_X6 &&
+                         b->n_eblocks == b->n_nodes && !getenv_flag("SPWGNN_RB_ONEHOT");
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
         SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
         SPW_CHECK(launch_edge_fwd(ef, kmath(r, kX6EdgeFwd), st));

@@ -250,6 +250,103 @@ static int32_t plan_fill_impl(int32_t n_towers, const int32_t* tower_nodes, cons
     return SPWGNN_OK;
 }
 
+// Receiver blocks: each node of a wave-tile owns one 32-edge block holding its in-edges (the tile's
+// edges bucketed by receiver, input order kept within a receiver; ≤ 32 in-edges per node), so block
+// bb of tile w feeds node wtile[w].first_node + bb alone and its receiver sum is a column sum
+// (k_edge_fwd_rb_x6). Nodes without in-edges get an all-padding block (their sum row is zero).
+static int32_t plan_fill_recv_impl(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                                   const int32_t* src, const int32_t* dst, int32_t nw_max,
+                                   const spwgnn_plan_sizes* sizes, int32_t* wtile, int32_t* edge_src,
+                                   int32_t* edge_dst, int32_t* edge_id, uint8_t* blk_csr) {
+    if (!sizes || !wtile || !edge_src || !edge_dst || !blk_csr || !tower_edges) return SPWGNN_E_ARG;
+    std::vector<int32_t> first;
+    int32_t nb = 0, used = 0;
+    int32_t st = plan_pack(n_towers, tower_nodes, tower_nodes, nw_max, &first, &nb, &used);
+    if (st) return st;
+    const int32_t ntiles = (int32_t)first.size() - 1;
+    std::vector<int64_t> node_off(n_towers + 1, 0), edge_off(n_towers + 1, 0);
+    for (int32_t t = 0; t < n_towers; ++t) {
+        if (tower_edges[t] < 0) return SPWGNN_E_ARG;
+        node_off[t + 1] = node_off[t] + tower_nodes[t];
+        edge_off[t + 1] = edge_off[t] + tower_edges[t];
+    }
+    int64_t nblocks = 0;
+    for (int32_t w = 0; w < ntiles; ++w) nblocks += node_off[first[w + 1]] - node_off[first[w]];
+    if (ntiles != sizes->n_wtiles || nblocks != sizes->n_eblocks) return SPWGNN_E_ARG;
+    if (edge_off[n_towers] > 0 && (!src || !dst)) return SPWGNN_E_ARG;
+    int32_t blk = 0;
+    std::vector<int32_t> fill;
+    for (int32_t w = 0; w < ntiles; ++w) {
+        const int32_t t0 = first[w], t1 = first[w + 1];
+        const int64_t n0 = node_off[t0], n1 = node_off[t1];
+        const int32_t nn = (int32_t)(n1 - n0);
+        wtile[4 * w + 0] = blk;
+        wtile[4 * w + 1] = nn;
+        wtile[4 * w + 2] = (int32_t)n0;
+        wtile[4 * w + 3] = nn;
+        for (int64_t o = (int64_t)blk * 32; o < (int64_t)(blk + nn) * 32; ++o) {
+            edge_src[o] = edge_dst[o] = -1;
+            if (edge_id) edge_id[o] = -1;
+        }
+        fill.assign(nn, 0);
+        for (int32_t t = t0; t < t1; ++t)
+            for (int64_t e = edge_off[t]; e < edge_off[t + 1]; ++e) {
+                const int32_t s = src[e], d = dst[e];
+                if (s < node_off[t] || s >= node_off[t + 1] || d < node_off[t] || d >= node_off[t + 1])
+                    return SPWGNN_E_RELATION;
+                const int32_t b = (int32_t)(d - n0);
+                if (fill[b] >= 32) return SPWGNN_E_SHAPE;   // > 32 in-edges: not a receiver-block batch
+                const int64_t o = (int64_t)(blk + b) * 32 + fill[b]++;
+                edge_src[o] = s;
+                edge_dst[o] = d;
+                if (edge_id) edge_id[o] = (int32_t)e;
+            }
+        for (int32_t b = 0; b < nn; ++b, ++blk) {
+            uint8_t* csr = blk_csr + (int64_t)blk * 128;
+            int32_t lsrc[32], ldst[32];
+            for (int i = 0; i < 32; ++i) {
+                const int64_t o = (int64_t)blk * 32 + i;
+                lsrc[i] = i < fill[b] ? (int32_t)(edge_src[o] - n0) : 255;
+                ldst[i] = i < fill[b] ? (int32_t)(edge_dst[o] - n0) : 255;
+            }
+            for (int pass = 0; pass < 2; ++pass) {
+                const int32_t* key = pass == 0 ? ldst : lsrc;
+                int order[32];
+                for (int i = 0; i < 32; ++i) order[i] = i;
+                std::stable_sort(order, order + 32, [&](int a, int c) { return key[a] < key[c]; });
+                uint8_t* o = csr + pass * 64;
+                for (int i = 0; i < 32; ++i) {
+                    o[i] = (uint8_t)order[i];
+                    o[32 + i] = (uint8_t)(i < fill[b] ? key[order[i]] : 255);
+                }
+            }
+        }
+    }
+    return SPWGNN_OK;
+}
+
+int32_t spwgnn_plan_size_recv(int32_t n_towers, const int32_t* tower_nodes, int32_t nw_max, spwgnn_plan_sizes* out) {
+    if (!out) return SPWGNN_E_ARG;
+    std::vector<int32_t> first;
+    int32_t nb = 0, used = 0;
+    const int32_t st = plan_pack(n_towers, tower_nodes, tower_nodes, nw_max, &first, &nb, &used);
+    if (st) return st;
+    int64_t nodes = 0;
+    for (int32_t t = 0; t < n_towers; ++t) nodes += tower_nodes[t];
+    out->n_wtiles = (int32_t)first.size() - 1;
+    out->n_eblocks = (int32_t)nodes;
+    out->nw_max = used;
+    return SPWGNN_OK;
+}
+
+int32_t spwgnn_plan_fill_recv(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                              const int32_t* src, const int32_t* dst, int32_t nw_max, const spwgnn_plan_sizes* sizes,
+                              int32_t* wtile, int32_t* edge_src, int32_t* edge_dst, int32_t* edge_id,
+                              uint8_t* blk_csr) {
+    return plan_fill_recv_impl(n_towers, tower_nodes, tower_edges, src, dst, nw_max, sizes, wtile, edge_src, edge_dst,
+                               edge_id, blk_csr);
+}
+
 int32_t spwgnn_plan_size(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
                          int32_t nw_max, spwgnn_plan_sizes* out) {
     return plan_size_impl(n_towers, tower_nodes, tower_edges, nw_max, out);

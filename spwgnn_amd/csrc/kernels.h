@@ -105,6 +105,8 @@ __device__ __forceinline__ uint64_t run_seed(const Args& a) {
 
 struct EdgeFwdArgs {
     int n_wtiles, nw_max, wpg;
+    int n_nodes;       // receiver blocks: one block per node
+    int recv_blocks;   // SPWGNN_BATCH_RECV_BLOCKS plan: k_edge_fwd_rb_x6 (x6 math)
     const int32_t *wtile, *esrc, *edst;
     const uint32_t* csr;
     const float *A, *U, *V, *w2, *b2;

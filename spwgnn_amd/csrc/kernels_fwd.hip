@@ -1120,6 +1120,194 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     }
 }
 
+// Receiver blocks (spwgnn_plan_fill_recv, SPWGNN_BATCH_RECV_BLOCKS): block b holds the in-edges of
+// node b alone (one block per node, in node order), so the receiver sum of a block is the COLUMN SUM
+// of its h2 tile — 15 adds per register column and one v_permlane32_swap — instead of k_edge_fwd_x6's
+// one-hot products (three bf16 parts of every h2 register and 30 MFMAs per block) and its node
+// accumulators carried across a wave-tile's blocks. V[r] is one row per block (broadcast); U[s] are
+// the tower's sender rows, which the 8 waves of a workgroup share from L1/L2: a workgroup walks a
+// contiguous block range, wave w taking blocks w, w + 8, … of it (neighbouring receivers of one tower
+// at a time). Products, k order and the h1/h2 bit masks are k_edge_fwd_x6's; the sum over a node's
+// messages runs in a different (fixed) order: registers 0..15 of each half pairwise, then the halves.
+// MASKS: training (h1/h2 bit masks stored); the inference instantiation carries none of that code
+#ifndef SPWGNN_RB_PF
+#define SPWGNN_RB_PF 2
+#endif
+template <int NP = 3, bool MASKS = true>
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_edge_fwd_rb_x6(EdgeFwdArgs a) {
+    constexpr int kWaves = 8, kPf = SPWGNN_RB_PF;
+    static_assert(10 % kPf == 0, "ring slots carry over between blocks");
+    __shared__ uint4 wl[50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
+    for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const WlBases wlb(wl + lane);
+    const int nblk = a.n_nodes;   // one block per node
+    const int per = ((nblk + gridDim.x - 1) / gridDim.x + kWaves - 1) / kWaves * kWaves;
+    const int b0 = blockIdx.x * per, b1 = min(b0 + per, nblk);
+    int blk = b0 + wave;
+    if (blk >= b1) return;
+    struct Src { int64_t ai; const float4 *U, *V; };
+    auto src_of = [&](int b, int s) {
+        const int sc = s >= 0 ? s : b;
+        return Src{(int64_t)b * kCmBlk + h * 128 + i * 4,
+                   reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128),
+                   reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(b, 0) + h * 128)};
+    };
+    struct KB { float4 a[2], u[2], v[2]; };
+    auto ld = [&](const Src& sr, int kb, KB& r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int q = min(2 * kb + c, kKhE / 4 - 1);
+            r.a[c] = *reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
+            r.u[c] = sr.U[64 * q];
+            r.v[c] = sr.V[64 * q];
+        }
+    };
+    int cur_s = a.esrc[(int64_t)blk * 32 + i];
+    Src cur = src_of(blk, cur_s);
+    KB ring[kPf];
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) ld(cur, k, ring[k]);
+    for (; blk < b1; blk += kWaves) {
+        const int nb = min(blk + kWaves, b1 - 1);   // the next block (clamped at the end)
+        const int nxt_s = a.esrc[(int64_t)nb * 32 + i];
+        const bool valid = cur_s >= 0;
+        const uint64_t vmask = __ballot(valid);
+        const float vf = valid ? 1.f : 0.f;
+        uint32_t* mrow = MASKS && a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
+        const int m1off = lane < 4 ? lane : kKhE + lane - 4;
+        Src nxt;
+        f32x16 acc[5];
+        zero_tiles(acc);
+#pragma unroll
+        for (int kb = 0; kb < 10; ++kb) {
+            KB& cr = ring[kb % kPf];
+            float xv[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
+                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
+                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
+                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
+            }
+            uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            if (kb + kPf < 10) {
+                ld(cur, kb + kPf, cr);
+            } else {
+                if (kb + kPf == 10) nxt = src_of(nb, nxt_s);
+                ld(nxt, kb + kPf - 10, cr);
+            }
+            bf16x8 ap[3];
+            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
+            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+            if constexpr (!MASKS) __builtin_amdgcn_sched_barrier(0);   // keep the k-block order (as the mask code does)
+            if (MASKS && mrow) {   // h1 > 0 bits of the block's real chunks (k_edge_fwd_x6's layout)
+                uint64_t bal[2][4];
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) bal[c][f] = __ballot(xv[4 * c + f] > 0.f);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int q = 2 * kb + c;
+                    if (q < kKhE / 4) {
+                        uint32_t v[8];
+                        int ln[8];
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) {
+                            v[2 * f] = (uint32_t)bal[c][f];
+                            ln[2 * f] = f;
+                            v[2 * f + 1] = (uint32_t)(bal[c][f] >> 32);
+                            ln[2 * f + 1] = 4 + f;
+                        }
+                        const uint32_t stg = writelane8_batched(0u, v, ln);
+                        if (lane < 8) mrow[m1off + 4 * q] = stg;
+                    }
+                }
+            }
+            auto group = [&](auto NTc, int T0) {
+                constexpr int NT = decltype(NTc)::value;
+                bf16x8 bp[NT][3];
+#pragma unroll
+                for (int v = 0; v < NT; ++v) {
+                    const int u = (kb * 5 + T0 + v) * 3 * 64;
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) bp[v][q] = as_bf16x8(wlb.at(u + 64 * q));
+                }
+                mfma32_x6_group<NP, NT>(ap, bp, acc + T0);
+            };
+            group(std::integral_constant<int, 2>{}, 0);
+            group(std::integral_constant<int, 3>{}, 2);
+        }
+        if (MASKS && mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;  // features 152..159 (padding)
+        const uint32_t vh = (uint32_t)vmask >> (4 * h);   // bit rho(r, 0): edge rho(r, h) is real
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const float b = a.b2[32 * t + i];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = relu(acc[t][r] + b);
+                if (t == 4 && i == kDegCol - 128) v = 1.f;  // degree column (multiplies b3)
+                acc[t][r] = mask_bit(v, vh, rho(r, 0));
+            }
+        }
+        if (MASKS && a.mask2) {  // h2 > 0 bits, word per (block, tile, edge): bit = feature within tile
+            uint32_t* m2row = a.mask2 + (int64_t)blk * kM2Blk;
+            uint32_t mw2[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r0 = 0; r0 < 16; r0 += 8) {
+                    uint64_t bal[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) bal[r] = __ballot(acc[t][r0 + r] > 0.f);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int g = 0; g < 2; ++g) {
+                        uint32_t v[8];
+                        int ln[8];
+                        const int reg = (r0 >> 2) + g;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int r = 4 * g + e;
+                            const int w0 = m2_pos(rho(r0 + r, 0), t), w1 = m2_pos(rho(r0 + r, 1), t);
+                            v[2 * e] = (uint32_t)bal[r];
+                            ln[2 * e] = w0 & 63;
+                            v[2 * e + 1] = (uint32_t)(bal[r] >> 32);
+                            ln[2 * e + 1] = w1 & 63;
+                        }
+                        mw2[reg] = writelane8_batched(mw2[reg], v, ln);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = mw2[k];
+        }
+        // receiver sum of node blk = column sum of the block's h2 (padding rows are +0)
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            float p8[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) p8[q] = acc[t][2 * q] + acc[t][2 * q + 1];
+            const float s4a = (p8[0] + p8[1]) + (p8[2] + p8[3]), s4b = (p8[4] + p8[5]) + (p8[6] + p8[7]);
+            const float sh = s4a + s4b;
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(sh), __float_as_uint(sh), false, false);
+            const float tot = sh + __uint_as_float(sw[1]);   // lanes 0-31: + the other half's edges
+            const int f = 32 * t + i;
+            if (h == 0 && f < 2 * kKhE) a.H2s[cm_index<kKhE>(blk, f)] = tot;
+        }
+        cur_s = nxt_s;
+        cur = nxt;
+    }
+}
+
 int edge_grid(int n_wtiles, int waves) {
     static int cus = 0;  // compute units of the device (all devices of a node are alike)
     if (cus <= 0) {
@@ -1205,6 +1393,16 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
             hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((k_edge_fwd_x6<false, 0, 1>), dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
+    if (math == MATH_X6 && a.recv_blocks) {   // receiver blocks: column sums (spwgnn_plan_fill_recv)
+        int cus = 0, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        const int need = (a.n_nodes + 8 * 16 - 1) / (8 * 16);   // ≥ 16 blocks per wave
+        const dim3 g(std::max(1, std::min(cus, need))), b(512);
+        if (a.mask1 || a.mask2) hipLaunchKernelGGL((k_edge_fwd_rb_x6<3, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_edge_fwd_rb_x6<3, false>), g, b, 0, st, a);
         return hipGetLastError();
     }
     if (math == MATH_X6) {

@@ -157,3 +157,36 @@ def test_backward_writes_every_gradient(math, n_towers):
     torch.cuda.synchronize()
     assert torch.isfinite(g_nan).all(), int((~torch.isfinite(g_nan)).sum())
     assert torch.equal(g_nan, g_zero)
+
+
+@pytest.mark.parametrize("math", ["x6", "f32"])
+@pytest.mark.parametrize("T,N,fully", [(3, 32, True), (4, 24, False), (9, 6, True)])
+def test_receiver_block_plan_parity(T, N, fully, math):
+    """Receiver-block plans (spwgnn_plan_fill_recv: one block per node; the x6 edge forward's column
+    sums, k_edge_fwd_rb_x6): logits, loss and every gradient against the fp64 oracle at the fp32
+    tolerance, training with S = 5, and the same towers through the default plan agree."""
+    params = O.random_params(seed=17)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(T, N, seed=5, fully_connected=fully)
+    S = 5
+    loss_ref, z_ref, g_ref = O.loss_and_grads(params, obj, Rs, Rr, prop, tgt, S)
+    dense = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    rb = TowerBatch.from_edges(obj.reshape(-1, 3), dense.tower_nodes, dense.src, dense.dst, dense.tower_edges,
+                               prop.reshape(-1, 100), device="cuda", recv_blocks=True)
+    assert rb.flags == 1 and rb.n_eblocks == rb.n_nodes
+    zs = []
+    for batch in (rb, dense):
+        flat, ws, z = _gpu_forward(params, batch, S, training=True, math=math)
+        out3, dz = E.bce(z, torch.tensor(tgt, device="cuda").reshape(-1), E.BceScratch("cuda"))
+        grads, _ = E.backward(flat, batch, E.RunConfig(S, training=True, math=math), ws, dz)
+        torch.cuda.synchronize()
+        zc = z.cpu().numpy().reshape(z_ref.shape)
+        assert np.all(np.abs(zc - z_ref) <= 1e-5 + 1e-5 * np.abs(z_ref)), np.abs(zc - z_ref).max()
+        assert abs(float(out3[0]) - loss_ref) < 1e-5
+        got = P.from_flat(grads)
+        for name, ref in g_ref.items():
+            assert np.abs(got[name] - ref).max() <= 1e-5 * np.abs(ref).max() + 1e-7, name
+        zs.append(zc)
+        # inference forward of the same plan
+        zi = _gpu_forward(params, batch, S, training=False, math=math)[2].cpu().numpy().reshape(z_ref.shape)
+        assert np.all(np.abs(zi - z_ref) <= 1e-5 + 1e-5 * np.abs(z_ref))
+    assert np.abs(zs[0] - zs[1]).max() <= 2e-6

@@ -423,3 +423,38 @@ def test_input_validation_errors():
     off[1][0, :, 2] = 0.0
     b = TowerBatch.from_dense(obj, off[0], off[1], device="cpu")
     assert b.n_edges == 2 * 12 - 1
+
+
+@pytest.mark.parametrize("N,thr", [(32, None), (27, None), (20, 170.0), (6, 170.0)])
+def test_receiver_block_plan_invariants(N, thr):
+    """spwgnn_plan_fill_recv: one 32-edge block per node holding exactly that node's in-edges (input
+    order kept within a receiver), padding after them, every edge once, the csr sorted per block; the
+    automatic choice takes it for dense towers of more than 16 nodes only."""
+    B = 5
+    raw = D.synthetic_towers(B, N, seed=N + 1)
+    Rs, Rr = O.relation_matrices(raw, thr)
+    dense = TowerBatch.from_dense((raw / 170).astype(np.float32), Rs, Rr, device="cpu")
+    b = TowerBatch.from_edges(dense.pos.numpy()[:, :3], dense.tower_nodes, dense.src, dense.dst, dense.tower_edges,
+                              device="cpu", recv_blocks=True)
+    assert b.flags == _lib.BATCH_RECV_BLOCKS and b.n_eblocks == b.n_nodes
+    esrc, edst, csr, wt = b.edge_src.numpy(), b.edge_dst.numpy(), b.blk_csr.numpy(), b.wtile.numpy()
+    assert np.array_equal(wt[:, 1], wt[:, 3]) and wt[:, 1].sum() == b.n_nodes
+    seen = []
+    for fb, nb, n0, nn in wt:
+        for j in range(nb):
+            blk = fb + j
+            s, d = esrc[blk * 32:(blk + 1) * 32], edst[blk * 32:(blk + 1) * 32]
+            valid = s >= 0
+            nv = int(valid.sum())
+            assert np.all(valid[:nv]) and np.all(d[valid] == n0 + j)        # node n0 + j's in-edges only
+            ref = [(x, y) for x, y in zip(dense.src, dense.dst) if y == n0 + j]   # input order kept
+            assert list(zip(s[:nv], d[:nv])) == ref
+            seen += ref
+            for base, key in ((0, d), (64, s)):
+                order, nodes = csr[blk, base:base + 32], csr[blk, base + 32:base + 64]
+                assert sorted(order) == list(range(32)) and np.all(nodes[nv:] == 255)
+                assert np.all(nodes[:nv] == key[order[:nv]] - n0)
+    assert sorted(seen) == sorted(zip(dense.src, dense.dst))
+    auto = TowerBatch.from_edges(dense.pos.numpy()[:, :3], dense.tower_nodes, dense.src, dense.dst, dense.tower_edges,
+                                 device="cpu")
+    assert (auto.flags == _lib.BATCH_RECV_BLOCKS) == (N > 16 and thr is None and N >= 27)
