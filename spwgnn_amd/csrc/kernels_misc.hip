@@ -1015,6 +1015,9 @@ struct WsSet4 {
 #ifndef SPWGNN_WS_DBG
 #define SPWGNN_WS_DBG 0
 #endif
+#ifndef SPWGNN_WS_NSET   // stage sets the staging waves keep in flight (k_wgrad_ws)
+#define SPWGNN_WS_NSET 3
+#endif
 template <int KXP, int NYP, int YROW, bool MASK, int NP, int XD, int B16>
 __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* smem) {
     constexpr int DBG = SPWGNN_WS_DBG;
@@ -1252,34 +1255,32 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             }
         }
     }
-    WsSet4 R0, R1, R2;
-    fetch(0, R0);
-    fetch(1, R1);
-    fetch(2, R2);
-    build(R0, buf(0));
+    // NS stage sets in flight: at (sub-)iteration u the staging waves stream stage u + NS into set
+    // u % NS (its stage u was built one iteration ago) and build stage u + 1 into buffer (u + 1) & 1,
+    // so a stage's loads are issued NS − 1 iterations before their split (static set names: the
+    // loop is unrolled by NS)
+    constexpr int NS = SPWGNN_WS_NSET;
+    WsSet4 R[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) fetch(k, R[k]);
+    build(R[0], buf(0));
     __syncthreads();
-    // iteration t: stream stage t+3 into set t%3, build stage t+1 (set (t+1)%3) into buffer (t+1)&1
     int t = 0;
-    for (; t + 3 <= T - 1; t += 3) {
-        fetch(t + 3, R0);
-        build(R1, buf((t + 1) & 1));
-        __syncthreads();
-        fetch(t + 4, R1);
-        build(R2, buf(t & 1));
-        __syncthreads();
-        fetch(t + 5, R2);
-        build(R0, buf((t + 1) & 1));
-        __syncthreads();
+    for (; t + NS <= T - 1; t += NS) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            fetch(t + k + NS, R[k]);
+            build(R[(k + 1) % NS], buf((t + k + 1) & 1));
+            __syncthreads();
+        }
     }
-    if (t < T - 1) {
-        build(R1, buf((t + 1) & 1));
-        __syncthreads();
-        ++t;
-    }
-    if (t < T - 1) {
-        build(R2, buf((t + 1) & 1));
-        __syncthreads();
-        ++t;
+#pragma unroll
+    for (int k = 1; k < NS; ++k) {   // t ≡ 0 (mod NS) here: stage t + k sits in set k
+        if (t < T - 1) {
+            build(R[k], buf((t + 1) & 1));
+            __syncthreads();
+            ++t;
+        }
     }
     if constexpr (DBG == 3) {   // keep the diagnosis split alive
         if (dbg_sink == 0x9e3779b9u) a.slab[0] = 0.f;
