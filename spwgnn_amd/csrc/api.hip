@@ -3,6 +3,7 @@
 #include <cstring>
 #include <cstdlib>
 #include "kernels.h"
+#include <vector>
 #include "../../include/spwgnn.h"
 static_assert(SPWGNN_MATH_F32 == spw::MATH_F32 && SPWGNN_MATH_X6 == spw::MATH_X6 && SPWGNN_MATH_BF16 == spw::MATH_BF16,
               "math ids");
@@ -374,12 +375,6 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.scale = scale;
     en.seed = r->seed;
     en.seed_dev = r->seed_dev;
-    {
-        Prof pn{r, st};
-        SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
-        SPW_CHECK(launch_enc_node(en, r->math, st));
-        SPW_CHECK(pn.after(SPWGNN_K_ENC_NODE));
-    }
 
     EncEdgeArgs ee{};
     ee.n_eblocks = b->n_eblocks;
@@ -417,7 +412,20 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.scale = scale;
     ee.seed = r->seed;
     ee.seed_dev = r->seed_dev;
-    {
+    if (r->math == kmath(r, kX6EncEdge) && enc_pair_team(b->n_eblocks, b->n_nodes, r->math) &&
+        !getenv_flag("SPWGNN_NO_ENC_PAIR")) {
+        // small batch: both encoders in one launch (timed as the relation encoder)
+        Prof p0{r, st};
+        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
+        SPW_CHECK(launch_enc_pair_team(ee, en, r->math, ee.z1 || ee.ed, st));
+        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
+    } else {
+        {
+            Prof pn{r, st};
+            SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
+            SPW_CHECK(launch_enc_node(en, r->math, st));
+            SPW_CHECK(pn.after(SPWGNN_K_ENC_NODE));
+        }
         Prof p0{r, st};
         SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
         SPW_CHECK(launch_enc_edge(ee, kmath(r, kX6EncEdge), st));
@@ -689,10 +697,10 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     const bool n16 = store_b16_node(r, b);
     const int64_t nN = b->n_nodes;
     const float scale = (r->dropout > 0.f) ? 1.0f / (1.0f - r->dropout) : 1.0f;
-    // grads is cleared first: the reductions write the 22 Keras tensors' elements, not every float of the
-    // flat buffer (measured: without the clear 739 floats of a NaN-filled buffer stay NaN —
-    // tests/test_gpu_parity.py::test_backward_writes_every_gradient)
-    SPW_CHECK(hipMemsetAsync(grads, 0, param_table().total * sizeof(float), st));
+    // the reductions write the 22 Keras tensors' elements, not every float of the flat buffer: the
+    // remaining ranges (alignment gaps; tensors no job of this batch writes) are zeroed by the same
+    // reduction launch (tests/test_gpu_parity.py::test_backward_writes_every_gradient; a NaN-filled
+    // buffer comes out equal to a zero-filled one)
     Prof prof{r, st};
 
     for (int s = S - 1; s >= 0; --s) {
@@ -966,6 +974,40 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         SPW_CHECK(prof.before(SPWGNN_K_WGRAD_WS));
         SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st));
         SPW_CHECK(prof.after(SPWGNN_K_WGRAD_WS));
+    }
+    {   // the float ranges no reduction of this batch writes: alignment gaps, uncovered tensor rows
+        const ParamTable& pt = param_table();
+        rb.nzero = 0;
+        auto zero = [&](int64_t off, int64_t len) {
+            if (len <= 0) return true;
+            if (rb.nzero > 0 && rb.zoff[rb.nzero - 1] + rb.zlen[rb.nzero - 1] == off) {   // merge
+                rb.zlen[rb.nzero - 1] += (int32_t)len;
+                return true;
+            }
+            if (rb.nzero >= kMaxZero) return false;
+            rb.zoff[rb.nzero] = off;
+            rb.zlen[rb.nzero++] = (int32_t)len;
+            return true;
+        };
+        for (int t = 0; t < kNumTensors; ++t) {
+            const TensorDesc& d = pt.t[t];
+            const int64_t end = t + 1 < kNumTensors ? pt.t[t + 1].offset : pt.total;
+            std::vector<char> row(d.rows, 0);   // rows (kernels) or the one bias row written by some job
+            for (int k = 0; k < rb.n; ++k) {
+                const ReduceArgs& ra = rb.r[k];
+                if (d.rows > 1 && ra.kernel_off == d.offset)
+                    for (int q = 0; q < ra.kernel_rows; ++q)
+                        if (ra.kernel_row0 + q < d.rows) row[ra.kernel_row0 + q] = 1;
+                if (d.rows == 1 && ra.bias_off == d.offset) row[0] = 1;
+            }
+            for (int q = 0; q < d.rows; ++q)
+                if (!row[q] && !zero(d.offset + (int64_t)q * d.cols, d.cols)) return SPWGNN_E_ARG;
+            if (!zero(d.offset + (int64_t)d.rows * d.cols, end - d.offset - (int64_t)d.rows * d.cols)) return SPWGNN_E_ARG;
+        }
+        if (rb.n == 0 && rb.nzero > 0) {   // nothing reduced at all: the whole buffer is zero
+            SPW_CHECK(hipMemsetAsync(grads, 0, pt.total * sizeof(float), st));
+            rb.nzero = 0;
+        }
     }
     SPW_CHECK(launch_wgrad_reduce_all(rb, st));
     return SPWGNN_OK;

@@ -279,9 +279,16 @@ struct WsBatch {           // the k_wgrad_ws gradients of one backward (k_wgrad_
 };
 
 constexpr int kMaxReduce = 16;
+constexpr int kMaxZero = 48;
 struct ReduceBatch {       // the weight gradients of one backward, reduced in one launch (blockIdx.y)
     ReduceArgs r[kMaxReduce];
     int n;
+    // float ranges of the flat gradient buffer no reduction writes (the 64-float alignment gaps between
+    // tensors, tensors without rows in this batch): zeroed by the extra row blockIdx.y == n of the
+    // same launch (was a separate hipMemsetAsync of the whole buffer before the backward)
+    int nzero;
+    int64_t zoff[kMaxZero];
+    int32_t zlen[kMaxZero];
 };
 struct BceArgs {
     const float *logits, *targets;
@@ -356,6 +363,9 @@ hipError_t launch_enc_node_bwd_team(const EncNodeBwdArgs& a, int math, hipStream
 hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_node_bwd_team(const NodeBwdArgs& a, int math, hipStream_t st);
 hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipStream_t st);
+// both encoders of a small batch in one launch (when both would take their team form)
+bool enc_pair_team(int n_eblocks, int n_nodes, int math);
+hipError_t launch_enc_pair_team(const EncEdgeArgs& e, const EncNodeArgs& n, int math, bool train, hipStream_t st);
 hipError_t launch_enc_edge_bwd_team(const EncEdgeBwdArgs& a, int math, hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)

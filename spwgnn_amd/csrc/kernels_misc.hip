@@ -1016,7 +1016,7 @@ struct WsSet4 {
 #define SPWGNN_WS_DBG 0
 #endif
 #ifndef SPWGNN_WS_NSET   // stage sets the staging waves keep in flight (k_wgrad_ws)
-#define SPWGNN_WS_NSET 3
+#define SPWGNN_WS_NSET 4
 #endif
 template <int KXP, int NYP, int YROW, bool MASK, int NP, int XD, int B16>
 __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* smem) {
@@ -1349,6 +1349,11 @@ void k_wgrad_ws_batch(WsBatch b) {
 // thread instead of 64 (the reduction was latency-bound: 66 µs at config 2, 74 µs at the headline).
 __global__ __launch_bounds__(256) void k_wgrad_reduce_all(ReduceBatch rb) {
     __shared__ float part[8][32];
+    if ((int)blockIdx.y == rb.n) {   // the ranges no reduction writes: zeros
+        for (int z = 0; z < rb.nzero; ++z)
+            for (int e = blockIdx.x * 256 + threadIdx.x; e < rb.zlen[z]; e += gridDim.x * 256) rb.r[0].out[rb.zoff[z] + e] = 0.f;
+        return;
+    }
     const ReduceArgs& a = rb.r[blockIdx.y];
     const int e = threadIdx.x & 31, g = threadIdx.x >> 5;
     const int idx = blockIdx.x * 32 + e;
@@ -1747,8 +1752,8 @@ hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {
-    if (rb.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_wgrad_reduce_all, dim3((160 * 160 + 31) / 32, rb.n), dim3(256), 0, st, rb);
+    if (rb.n <= 0) return rb.nzero > 0 ? hipErrorInvalidValue : hipSuccess;   // the zero row writes through r[0].out
+    hipLaunchKernelGGL(k_wgrad_reduce_all, dim3((160 * 160 + 31) / 32, rb.n + (rb.nzero > 0 ? 1 : 0)), dim3(256), 0, st, rb);
     return hipGetLastError();
 }
 hipError_t launch_bce(const BceArgs& a, hipStream_t st) {

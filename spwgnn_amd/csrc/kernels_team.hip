@@ -212,12 +212,11 @@ __device__ __forceinline__ void bias_act_tile(f32x16& x, const float (&bv)[16]) 
 // rm encoder (k_enc_edge_x6's chain, Networks.py:75,77): d → relu(rm.0) → 3 × (150×150 + relu) →
 // dropout = c_r → A = c_r·W1a + b1, one 32-edge block per 5-wave workgroup.
 template <bool TRAIN, int NP, bool B16>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_team(EncEdgeArgs a) {
+__device__ __forceinline__ void enc_edge_team_body(const EncEdgeArgs& a, int blk) {
     __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];   // ≤ 60 KiB
     const TeamAct<kTeamEdge, NP> act{act_s};
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int blk = blockIdx.x;
     const int64_t e = (int64_t)blk * 32 + j;
     TEAM_STAMP(0);
     TeamFrags<10, NP> F;
@@ -290,6 +289,10 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_team(EncEdgeArgs a)
     }
     TEAM_STAMP(10);
 }
+template <bool TRAIN, int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_team(EncEdgeArgs a) {
+    enc_edge_team_body<TRAIN, NP, B16>(a, blockIdx.x);
+}
 
 // ------------------------------------------------------------------------------------------------
 // rm encoder backward (k_enc_edge_bwd_x6's chain): dc_r = dA·W1aᵀ (B from the dA half rows, read by
@@ -348,10 +351,9 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_bwd_team(EncEdgeBwd
 // z1 = relu(om.0(y, w)) and of P0 (the 'propagation' input) in registers — cheap VALU and loads — so
 // no layer output crosses waves: wave T < 4 owns tile T of c_o, waves 0..4 tile T of U0 and V0.
 template <int NP>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_node_team(EncNodeArgs a) {
+__device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, int nb) {
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nb = blockIdx.x;
     const int n = nb * 32 + j;
     const bool valid = n < a.n_nodes;
     const int nc = valid ? n : a.n_nodes - 1;
@@ -412,6 +414,19 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_node_team(EncNodeArgs a)
     store_cm_tile<kKhE>(a.U0 + bE, U, T, lane, valid);
     U = team_gemm(F, TeamRegs<4>{P}, [&](int) {});
     store_cm_tile<kKhE>(a.V0 + bE, U, T, lane, valid);
+}
+template <int NP>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_node_team(EncNodeArgs a) {
+    enc_node_team_body<NP>(a, blockIdx.x);
+}
+// Both encoders of a small batch in ONE launch (they are independent): workgroups [0, n_eblocks) run
+// the relation encoder's blocks, the rest the object encoder's node blocks — one dependent launch and
+// one ramp-up fewer in the replayed step of the reference's batch 32 (the object encoder's ≈ 10 µs
+// run beside the relation encoder's 16 instead of before it).
+template <bool TRAIN, int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_pair_team(EncEdgeArgs e, EncNodeArgs n) {
+    if ((int)blockIdx.x < e.n_eblocks) enc_edge_team_body<TRAIN, NP, B16>(e, blockIdx.x);
+    else enc_node_team_body<NP>(n, (int)blockIdx.x - e.n_eblocks);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1091,6 +1106,23 @@ hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st) 
     if (math == MATH_BF16) hipLaunchKernelGGL((k_enc_node_team<1>), g, b, 0, st, a);
     else if (math == MATH_X6) hipLaunchKernelGGL((k_enc_node_team<3>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+bool enc_pair_team(int n_eblocks, int n_nodes, int math) {
+    return (math == MATH_X6 || math == MATH_BF16) && team_blocks(n_eblocks) && team_blocks((n_nodes + 31) / 32);
+}
+hipError_t launch_enc_pair_team(const EncEdgeArgs& e, const EncNodeArgs& n, int math, bool train, hipStream_t st) {
+    if (!enc_pair_team(e.n_eblocks, n.n_nodes, math)) return hipErrorInvalidValue;
+    const dim3 g(e.n_eblocks + (n.n_nodes + 31) / 32), b(64 * kTeamEdge);
+    if (math == MATH_BF16) {
+        if (train && e.b16) hipLaunchKernelGGL((k_enc_pair_team<true, 1, true>), g, b, 0, st, e, n);
+        else if (train) hipLaunchKernelGGL((k_enc_pair_team<true, 1, false>), g, b, 0, st, e, n);
+        else hipLaunchKernelGGL((k_enc_pair_team<false, 1, false>), g, b, 0, st, e, n);
+    } else if (train) {
+        hipLaunchKernelGGL((k_enc_pair_team<true, 3, false>), g, b, 0, st, e, n);
+    } else {
+        hipLaunchKernelGGL((k_enc_pair_team<false, 3, false>), g, b, 0, st, e, n);
+    }
     return hipGetLastError();
 }
 hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st) {
