@@ -682,6 +682,9 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 #ifndef SPWGNN_DA_PF_B16
 #define SPWGNN_DA_PF_B16 5
 #endif
+#ifndef SPWGNN_DA_INTERLEAVE
+#define SPWGNN_DA_INTERLEAVE 1
+#endif
 // N16 (bf16 math, §3g node side): dU, dV stored as bf16
 template <bool ACCUM, bool NODA = false, int NP = 3, int DBG = 0, bool N16 = false>   // DBG 3 (diagnosis): G3 rows of the tile's first node
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
@@ -922,10 +925,22 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const WlBases wlb(wl + lane);
+#if SPWGNN_DA_INTERLEAVE
+    // a contiguous block range per WORKGROUP, its waves interleaved (wave w: blocks w, w + 8, …): the
+    // 8 waves of a CU work on neighbouring blocks at once, so the receiver rows of a tower whose
+    // blocks they share (N ≥ 9: several blocks per tower) are gathered from L1/L2 by all of them, where
+    // a contiguous range per wave re-gathered every step's rows for each of the tower's blocks
+    // (config 3: 21 GB of traffic per launch against ≈ 7.5 GB compulsory)
+    constexpr int kStride = kWaves;
+    const int perw = ((a.n_eblocks + gridDim.x - 1) / gridDim.x + kWaves - 1) / kWaves * kWaves;
+    const int b0 = blockIdx.x * perw + wave, b1 = min(blockIdx.x * perw + perw, a.n_eblocks);
+#else
     // a contiguous range of blocks per wave: a tower's blocks (same receiver rows) stay on one CU
+    constexpr int kStride = 1;
     const int nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wave;
     const int per = (a.n_eblocks + nw - 1) / nw;
     const int b0 = gw * per, b1 = min(b0 + per, a.n_eblocks);
+#endif
     if (b0 >= b1) return;
     // one (block, step) pair: its receiver row pointer (G3 of that step) and its mask words
     struct Pair { const float4* G4; uint32_t w[5], m1w[5]; };
@@ -958,8 +973,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     for (;;) {
         // the next pair (steps S-1 .. 0 of a block, then the next block; clamped at the range end)
         const bool last_step = s == 0;
-        const bool has_next = !last_step || blk + 1 < b1;
-        const int nblk = last_step ? min(blk + 1, b1 - 1) : blk;
+        const bool has_next = !last_step || blk + kStride < b1;
+        const int nblk = last_step ? (blk + kStride < b1 ? blk + kStride : blk) : blk;
         const int ns = last_step ? a.S - 1 : s - 1;
         const int nd = last_step ? a.edst[(int64_t)nblk * 32 + i] : d;
         const Pair nxt = load_pair(nblk, max(ns, 0), nd);
