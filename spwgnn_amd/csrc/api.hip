@@ -290,13 +290,16 @@ struct Prof {
         if (e_ != hipSuccess) return (int32_t)e_;     \
     } while (0)
 
-// dA = Σ_s dh1pre_s: rebuilt once after the step loop (k_dA_x6) instead of float atomics into HBM in
-// every step's edge backward (the atomics bounded that kernel; A/B on one box: x6 step 28.11 →
-// 27.39 ms, bf16 config 3 71.5 → 69.3 ms — DESIGN.md §3f). SPWGNN_DA_ATOMIC (diagnosis builds only)
-// restores the per-step atomics for A/B.
+// dA = Σ_s dh1pre_s. x6, wide edge backward: each step's k_edge_bwd_x6 adds its dh1pre into the
+// block's dA rows (a read-add-write; the wave owns the block), in the order S−1 .. 0 — the rebuild's
+// order, so bitwise the same dA — and no second W2ᵀ product runs. bf16 math (dA
+// stored as bf16 after the fp32 sum) and the team kernels rebuild it once after the step loop
+// (k_dA_x6 / k_dA_team). The first per-step form used float atomics, which bounded the kernel.
+// SPWGNN_DA_REBUILD (diagnosis builds only) keeps the rebuild for x6 as well, for A/B.
 static bool rebuild_dA(const spwgnn_run* r, const spwgnn_batch* b) {
     const int m = kmath(r, kX6EdgeBwd);
-    return b->nw_max <= 16 && m != MATH_F32 && !getenv_flag("SPWGNN_DA_ATOMIC");
+    if (b->nw_max > 16 || m == MATH_F32) return false;
+    return m == MATH_BF16 || team_blocks(b->n_wtiles) || getenv_flag("SPWGNN_DA_REBUILD");
 }
 
 // bf16 math (training) stores the encoder-side edge arrays that only ever feed MFMA operands — z2, z3,
@@ -412,29 +415,8 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     ee.scale = scale;
     ee.seed = r->seed;
     ee.seed_dev = r->seed_dev;
-    if (r->math == kmath(r, kX6EncEdge) && enc_pair_team(b->n_eblocks, b->n_nodes, r->math) &&
-        !getenv_flag("SPWGNN_NO_ENC_PAIR")) {
-        // small batch: both encoders in one launch (timed as the relation encoder)
-        Prof p0{r, st};
-        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
-        SPW_CHECK(launch_enc_pair_team(ee, en, r->math, ee.z1 || ee.ed, st));
-        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
-    } else {
-        {
-            Prof pn{r, st};
-            SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
-            SPW_CHECK(launch_enc_node(en, r->math, st));
-            SPW_CHECK(pn.after(SPWGNN_K_ENC_NODE));
-        }
-        Prof p0{r, st};
-        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
-        SPW_CHECK(launch_enc_edge(ee, kmath(r, kX6EncEdge), st));
-        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
-    }
-
     const int S = r->mp_steps;
-    Prof prof{r, st};
-    for (int s = 0; s < S; ++s) {
+    auto edge_args = [&](int s) {
         EdgeFwdArgs ef{};
         ef.n_wtiles = b->n_wtiles;
         ef.nw_max = b->nw_max;
@@ -458,10 +440,9 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.recv_blocks = (b->flags & SPWGNN_BATCH_RECV_BLOCKS) && kmath(r, kX6EdgeFwd) == MATH_X6 &&
                          b->n_eblocks == b->n_nodes && !getenv_flag("SPWGNN_RB_ONEHOT");
         ef.mask2 = r->training ? c.u(w.m2_at(s)) : nullptr;
-        SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
-        SPW_CHECK(launch_edge_fwd(ef, kmath(r, kX6EdgeFwd), st));
-        SPW_CHECK(prof.after(SPWGNN_K_EDGE_FWD));
-
+        return ef;
+    };
+    auto node_args = [&](int s) {
         NodeFwdArgs nf{};
         nf.n_nodes = b->n_nodes;
         nf.H2s = c.f(w.H2s_at(s));
@@ -494,6 +475,58 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
             nf.x_w1c = c.x6(X6_W1C);
         }
         nf.n16 = store_b16_node(r, b);
+        return nf;
+    };
+    const bool one_math = r->math == kmath(r, kX6EncEdge) && r->math == kmath(r, kX6EdgeFwd) &&
+                          r->math == kmath(r, kX6NodeFwd);
+    if (one_math && fwd_fused_team(b->n_wtiles, b->nw_max, b->n_eblocks, b->n_nodes, r->math) &&
+        !(b->flags & SPWGNN_BATCH_RECV_BLOCKS) && !getenv_flag("SPWGNN_NO_FWD_FUSED")) {
+        // small batch: the encoders and all S steps in one launch (timed as the relation encoder)
+        FwdFusedArgs fa{};
+        fa.ee = ee;
+        fa.en = en;
+        fa.ef = edge_args(0);
+        fa.nf = node_args(0);
+        fa.S = S;
+        fa.training = r->training;
+        fa.rowsN = w.RN * kRowN;
+        fa.rowsE = w.RN * kRowE;
+        fa.m1_step = r->training ? w.m1_at(1) - w.m1_at(0) : 0;
+        fa.m2_step = r->training ? w.m2_at(1) - w.m2_at(0) : 0;
+        fa.logits = logits;
+        Prof p0{r, st};
+        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
+        SPW_CHECK(launch_fwd_fused_team(fa, r->math, ee.z1 || ee.ed, st));
+        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
+        return SPWGNN_OK;
+    }
+    if (r->math == kmath(r, kX6EncEdge) && enc_pair_team(b->n_eblocks, b->n_nodes, r->math) &&
+        !getenv_flag("SPWGNN_NO_ENC_PAIR")) {
+        // small batch: both encoders in one launch (timed as the relation encoder)
+        Prof p0{r, st};
+        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
+        SPW_CHECK(launch_enc_pair_team(ee, en, r->math, ee.z1 || ee.ed, st));
+        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
+    } else {
+        {
+            Prof pn{r, st};
+            SPW_CHECK(pn.before(SPWGNN_K_ENC_NODE));
+            SPW_CHECK(launch_enc_node(en, r->math, st));
+            SPW_CHECK(pn.after(SPWGNN_K_ENC_NODE));
+        }
+        Prof p0{r, st};
+        SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
+        SPW_CHECK(launch_enc_edge(ee, kmath(r, kX6EncEdge), st));
+        SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
+    }
+
+    Prof prof{r, st};
+    for (int s = 0; s < S; ++s) {
+        const EdgeFwdArgs ef = edge_args(s);
+        SPW_CHECK(prof.before(SPWGNN_K_EDGE_FWD));
+        SPW_CHECK(launch_edge_fwd(ef, kmath(r, kX6EdgeFwd), st));
+        SPW_CHECK(prof.after(SPWGNN_K_EDGE_FWD));
+        const NodeFwdArgs nf = node_args(s);
         SPW_CHECK(prof.before(SPWGNN_K_NODE_FWD));
         SPW_CHECK(launch_node_fwd(nf, kmath(r, kX6NodeFwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_FWD));
@@ -703,7 +736,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     // buffer comes out equal to a zero-filled one)
     Prof prof{r, st};
 
-    for (int s = S - 1; s >= 0; --s) {
+    auto node_args = [&](int s) {
         const bool first = (s == S - 1);
         NodeBwdArgs nb{};
         nb.n_nodes = b->n_nodes;
@@ -741,15 +774,14 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             nb.x_w3t = c.x6(X6_W3T);
         }
         nb.n16 = n16;
-        SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
-        SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
-        SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
-
+        return nb;
+    };
+    auto edge_args = [&](int s) {
         EdgeBwdArgs eb{};
         eb.n_wtiles = b->n_wtiles;
         eb.nw_max = b->nw_max;
         eb.wpg = b->nw_max <= 16 ? 4 : edge_wpg(edge_bwd_lds_per_wave(b->nw_max));
-        eb.dA_accumulate = !first;
+        eb.dA_accumulate = s != S - 1;
         eb.no_dA = rebuild;
         eb.wtile = b->wtile;
         eb.esrc = b->edge_src;
@@ -765,30 +797,27 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         eb.dU = c.f(w.dU_at(s));
         eb.dV = c.f(w.dV_at(s));
         eb.n16 = n16;
-        SPW_CHECK(prof.before(SPWGNN_K_EDGE_BWD));
-        SPW_CHECK(launch_edge_bwd(eb, kmath(r, kX6EdgeBwd), st));
-        SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
-    }
+        return eb;
+    };
+    NodeBwdArgs tl{};
     if (dprop) {
-        NodeBwdArgs nb{};
-        nb.n_nodes = b->n_nodes;
-        nb.first = 0;
-        nb.tail = 1;
-        nb.dPin = c.f(w.dP_at(0));
-        nb.dU = c.f(w.dU_at(0));
-        nb.dV = c.f(w.dV_at(0));
-        nb.dprop = dprop;
-        nb.w1bt = c.pk(PK_W1BT);
-        nb.w1ct = c.pk(PK_W1CT);
+        tl.n_nodes = b->n_nodes;
+        tl.first = 0;
+        tl.tail = 1;
+        tl.dPin = c.f(w.dP_at(0));
+        tl.dU = c.f(w.dU_at(0));
+        tl.dV = c.f(w.dV_at(0));
+        tl.dprop = dprop;
+        tl.w1bt = c.pk(PK_W1BT);
+        tl.w1ct = c.pk(PK_W1CT);
         if (r->math != MATH_F32) {
-            nb.x_w1bt = c.x6(X6_W1BT);
-            nb.x_w1ct = c.x6(X6_W1CT);
+            tl.x_w1bt = c.x6(X6_W1BT);
+            tl.x_w1ct = c.x6(X6_W1CT);
         }
-        nb.n16 = n16;
-        SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
+        tl.n16 = n16;
     }
+    DaArgs da{};
     if (rebuild) {
-        DaArgs da{};
         da.n_eblocks = b->n_eblocks;
         da.S = S;
         da.g3_step = w.G3_at(1) - w.G3_at(0);
@@ -801,9 +830,6 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         da.dA = c.f(w.dA);
         da.x_w2t = c.x6(X6_W2T);
         da.b16 = b16;
-        SPW_CHECK(prof.before(SPWGNN_K_DA));
-        SPW_CHECK(launch_dA(da, kmath(r, kX6EdgeBwd), st));
-        SPW_CHECK(prof.after(SPWGNN_K_DA));
     }
     EncEdgeBwdArgs eeb{};
     eeb.n_eblocks = b->n_eblocks;
@@ -825,10 +851,6 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     eeb.dz2 = c.f(w.dz2);
     eeb.dz1 = c.f(w.dz1);
     eeb.scale = scale;
-    SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
-    SPW_CHECK(launch_enc_edge_bwd(eeb, kmath(r, kX6EncEdgeBwd), st));
-    SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
-
     EncNodeBwdArgs enb{};
     enb.n_nodes = b->n_nodes;
     enb.dco = c.f(w.dco);
@@ -849,9 +871,54 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         enb.x_wo1ct = c.x6(X6_WO1CT);
         enb.x_om1t = c.x6(X6_OM1T);
     }
-    SPW_CHECK(prof.before(SPWGNN_K_ENC_NODE_BWD));
-    SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), st));
-    SPW_CHECK(prof.after(SPWGNN_K_ENC_NODE_BWD));
+
+    const bool one_math = r->math == kmath(r, kX6NodeBwd) && r->math == kmath(r, kX6EdgeBwd) &&
+                          r->math == kmath(r, kX6EncEdgeBwd);
+    if (one_math && rebuild && fwd_fused_team(b->n_wtiles, b->nw_max, b->n_eblocks, b->n_nodes, r->math) &&
+        !(b->flags & SPWGNN_BATCH_RECV_BLOCKS) && !n16 && !getenv_flag("SPWGNN_NO_BWD_FUSED")) {
+        // small batch: the step loop, dA and both encoder backwards in one launch (timed as the node backward)
+        BwdFusedArgs fa{};
+        fa.nb = node_args(0);
+        fa.nb.dU = c.f(w.dU_at(1));   // step 0's incoming dU/dV (BwdFusedArgs)
+        fa.nb.dV = c.f(w.dV_at(1));
+        fa.tail = tl;
+        fa.has_tail = dprop != nullptr;
+        fa.eb = edge_args(0);
+        fa.da = da;
+        fa.eeb = eeb;
+        fa.enb = enb;
+        fa.S = S;
+        fa.rowsN = w.RN * kRowN;
+        fa.rowsE = w.RN * kRowE;
+        fa.m1_step = w.m1_at(1) - w.m1_at(0);
+        fa.m2_step = w.m2_at(1) - w.m2_at(0);
+        SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
+        SPW_CHECK(launch_bwd_fused_team(fa, r->math, st));
+        SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
+    } else {
+        for (int s = S - 1; s >= 0; --s) {
+            const NodeBwdArgs nb = node_args(s);
+            SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
+            SPW_CHECK(launch_node_bwd(nb, kmath(r, kX6NodeBwd), st));
+            SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
+            const EdgeBwdArgs eb = edge_args(s);
+            SPW_CHECK(prof.before(SPWGNN_K_EDGE_BWD));
+            SPW_CHECK(launch_edge_bwd(eb, kmath(r, kX6EdgeBwd), st));
+            SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
+        }
+        if (dprop) SPW_CHECK(launch_node_bwd(tl, kmath(r, kX6NodeBwd), st));
+        if (rebuild) {
+            SPW_CHECK(prof.before(SPWGNN_K_DA));
+            SPW_CHECK(launch_dA(da, kmath(r, kX6EdgeBwd), st));
+            SPW_CHECK(prof.after(SPWGNN_K_DA));
+        }
+        SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
+        SPW_CHECK(launch_enc_edge_bwd(eeb, kmath(r, kX6EncEdgeBwd), st));
+        SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
+        SPW_CHECK(prof.before(SPWGNN_K_ENC_NODE_BWD));
+        SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), st));
+        SPW_CHECK(prof.after(SPWGNN_K_ENC_NODE_BWD));
+    }
 
     // ---- weight gradients ----
     const int64_t RE = w.RE, RN = w.RN;
@@ -969,10 +1036,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
-    SPW_CHECK(launch_wgrad_pos3(p3, st));
+    // a small batch's rm.0 / om.0 gradients join the batched launch (one dependent launch fewer)
+    const bool p3_in_batch = wsb.n > 0 && team_blocks(b->n_eblocks) && !getenv_flag("SPWGNN_NO_POS3_MERGE");
+    if (!p3_in_batch) SPW_CHECK(launch_wgrad_pos3(p3, st));
     if (wsb.n > 0) {
         SPW_CHECK(prof.before(SPWGNN_K_WGRAD_WS));
-        SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st));
+        SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st, p3_in_batch ? &p3 : nullptr));
         SPW_CHECK(prof.after(SPWGNN_K_WGRAD_WS));
     }
     {   // the float ranges no reduction of this batch writes: alignment gaps, uncovered tensor rows

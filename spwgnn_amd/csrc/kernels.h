@@ -326,7 +326,9 @@ hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, i
                            hipStream_t st, int b16 = 0);
 // the variant k_wgrad_ws runs for these arguments (WSV_NONE: no such kernel)
 int wgrad_ws_variant(const WgWsArgs& a, int kx_pad, int ny_pad, int yrow, int mask, int math, int b16);
-hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st);
+struct Pos3Batch;
+// p3: a small batch's k_wgrad_pos3 gradients as trailing workgroups of the same launch
+hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st, const Pos3Batch* p3 = nullptr);
 hipError_t launch_wgrad_bf16(const WgradArgs& a, int chunks, hipStream_t st, int b16 = 0);
 hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int math, hipStream_t st);
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st);
@@ -367,6 +369,37 @@ hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipS
 bool enc_pair_team(int n_eblocks, int n_nodes, int math);
 hipError_t launch_enc_pair_team(const EncEdgeArgs& e, const EncNodeArgs& n, int math, bool train, hipStream_t st);
 hipError_t launch_enc_edge_bwd_team(const EncEdgeBwdArgs& a, int math, hipStream_t st);
+// A small batch's whole forward in ONE launch: one workgroup per wave-tile runs both encoders on the
+// tile's blocks and node rows, then the S propagation steps (edge side, node side), separated by
+// workgroup barriers — a wave-tile holds whole towers, so no row it reads is written by another
+// workgroup. The step arrays are the step-0 pointers of ef/nf; step s adds the run's per-step
+// strides (Ws::*_at: per step when training, U/V/H2s shared and P alternating when not).
+struct FwdFusedArgs {
+    EncEdgeArgs ee;
+    EncNodeArgs en;
+    EdgeFwdArgs ef;       // U, V, H2s, mask1, mask2 of step 0
+    NodeFwdArgs nf;       // P, Pn, a_out, o1_out, U, V of step 0; cw_out (step 0) / cw_in (later)
+    int S, training;
+    int64_t rowsN, rowsE;     // floats per step of a 104- / 152-feature node array (RN·kRowN, RN·kRowE)
+    int64_t m1_step, m2_step; // u32 words per step of mask1 / mask2
+    float* logits;
+};
+bool fwd_fused_team(int n_wtiles, int nw_max, int n_eblocks, int n_nodes, int math);
+// ... and its backward up to the weight gradients (same batches): per wave-tile the S steps' node
+// and edge sides, d/d 'propagation', the dA rebuild, both encoder backwards. nb holds step 0's
+// pointers (Pn = P_at(1), dPout = dP_at(0), dU/dV = dU_at(1)/dV_at(1): the incoming gradients of
+// step 0); eb holds step 0's (mask1/2, G3, dU, dV); tail (has_tail) the dprop pass.
+struct BwdFusedArgs {
+    NodeBwdArgs nb, tail;
+    EdgeBwdArgs eb;
+    DaArgs da;
+    EncEdgeBwdArgs eeb;
+    EncNodeBwdArgs enb;
+    int S, has_tail;
+    int64_t rowsN, rowsE, m1_step, m2_step;
+};
+hipError_t launch_fwd_fused_team(const FwdFusedArgs& a, int math, bool train, hipStream_t st);
+hipError_t launch_bwd_fused_team(const BwdFusedArgs& a, int math, hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
 // persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)

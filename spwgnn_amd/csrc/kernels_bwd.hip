@@ -670,7 +670,8 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 // One propagation step, edge side, backward, in split-bf16 math (x6; wave-tiles of ≤ 16 nodes).
 // As k_edge_fwd_x6: lane (i, h) holds edge i, features 76h + 8kb + e of k-block kb; the A operand
 // is dh2pre = G3[receiver] ⊙ [h2 > 0] built from the G3 loads, W2ᵀ (x6 image) is the LDS B operand.
-// dh1pre = dh1 ⊙ [h1 > 0] goes to dA (plain stores on the first backward step, atomics after)
+// dh1pre = dh1 ⊙ [h1 > 0] goes to dA (stores on the first backward step S−1, read-add-writes after:
+// the sum runs s = S−1 .. 0 as k_dA_x6's does, so dA is bitwise the rebuilt one)
 // and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
 // 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
 #ifndef SPWGNN_EBWD_PF
@@ -832,7 +833,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 for (int r = 8 * s; r < 8 * s + 8; ++r) {
                     float* p = dArow + rho(r, h) * kLdE + 32 * t;
                     if constexpr (NODA) {
-                    } else if (ACCUM) unsafeAtomicAdd(p, acc[t][r]);
+                    } else if (ACCUM) *p += acc[t][r];   // the wave owns the block: plain read-add-write
                     else *p = acc[t][r];
                 }
             }
@@ -879,18 +880,11 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
             else hipLaunchKernelGGL((k_edge_bwd_x6<false, true>), g, b, 0, st, a);
             return hipGetLastError();
         }
-#ifdef SPWGNN_DIAG   // per-step dA stores + float atomics (SPWGNN_DA_ATOMIC A/B builds only)
-        if (math == MATH_BF16) {
-            if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true, false, 1>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((k_edge_bwd_x6<false, false, 1>), g, b, 0, st, a);
-        } else {
-            if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
-        }
+        // x6: dA accumulated per step in fp32 (bf16 math keeps the rebuild: its dA is stored as bf16)
+        if (math != MATH_X6) return hipErrorInvalidValue;
+        if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
         return hipGetLastError();
-#else
-        return hipErrorInvalidValue;
-#endif
     }
     if (a.nw_max <= 16) {
         if (a.dA_accumulate)

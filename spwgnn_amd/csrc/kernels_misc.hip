@@ -1300,10 +1300,24 @@ void k_wgrad_ws(WgWsArgs a) {
 // reference's batch 32 each gradient is a few workgroups of one or two stages, so eleven launches
 // cost their ramp-up eleven times; batched they overlap.
 constexpr int kWsMaxBuf = WsStage<160, 160, 0, false>::BUF;
+template <int KH, bool NODE, bool B16>
+__device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int tid);
+// A small batch's rm.0 / om.0 gradients (k_wgrad_pos3) ride in the same launch: workgroups from
+// b.wgs on run two of k_wgrad_pos3's 256-thread workgroups each (one per half), beside the jobs.
 template <int NP>
 __global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void k_wgrad_ws_batch(WsBatch b) {
+void k_wgrad_ws_batch(WsBatch b, Pos3Batch p3) {
     __shared__ __attribute__((aligned(16))) char smem[2 * kWsMaxBuf];
+    if ((int)blockIdx.x >= b.wgs) {
+        const int q = 2 * ((int)blockIdx.x - b.wgs) + (int)(threadIdx.x >> 8), tid = threadIdx.x & 255;
+        if (q < p3.ce) {
+            if (p3.b16e) wgrad_pos3_body<kKhE, false, true>(p3.e, q, tid);
+            else wgrad_pos3_body<kKhE, false, false>(p3.e, q, tid);
+        } else if (q < p3.ce + p3.cn) {
+            wgrad_pos3_body<kKhN, true, false>(p3.n, q - p3.ce, tid);
+        }
+        return;
+    }
     int k = 0;
     while (k + 1 < b.n && (int)blockIdx.x >= b.j[k + 1].wg0) ++k;
     int bid = (int)blockIdx.x - b.j[k].wg0;
@@ -1505,10 +1519,10 @@ __global__ void k_tower_readout(const float* __restrict__ z, const int32_t* __re
 // d1 / y, w and the bias row) go to this workgroup's chunk for k_wgrad_reduce_all. Pieces past the
 // row's last one (qh ≥ NQH) re-read the last piece and are never written out.
 template <int KH, bool NODE, bool B16>
-__device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid) {
+__device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int tid) {
     constexpr int NQH = KH / 2, NK = (NQH + 7) / 8, NYP = KH == kKhE ? 160 : 128, BLK = KH * 64;
     constexpr int UB = 4;   // blocks whose loads are issued together (the loop is latency-bound)
-    const int tid = threadIdx.x, i = tid & 31, g = tid >> 5;
+    const int i = tid & 31, g = tid >> 5;
     const int64_t b0 = (int64_t)bid * a.blk_per_wg, b1 = min(a.nblk, b0 + a.blk_per_wg);
     float4 s0[NK], s1[NK], s2[NK];
 #pragma unroll
@@ -1579,8 +1593,8 @@ __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid) {
 // rm.0 (edge rows) and om.0 (node rows) in one launch: workgroups [0, ce) take the edge job
 template <bool B16E>
 __global__ __launch_bounds__(256) void k_wgrad_pos3(Pos3Args e, Pos3Args n, int ce) {
-    if ((int)blockIdx.x < ce) wgrad_pos3_body<kKhE, false, B16E>(e, blockIdx.x);
-    else wgrad_pos3_body<kKhN, true, false>(n, blockIdx.x - ce);
+    if ((int)blockIdx.x < ce) wgrad_pos3_body<kKhE, false, B16E>(e, blockIdx.x, threadIdx.x);
+    else wgrad_pos3_body<kKhN, true, false>(n, blockIdx.x - ce, threadIdx.x);
 }
 hipError_t launch_wgrad_pos3(const Pos3Batch& p, hipStream_t st) {
     if (p.ce + p.cn <= 0) return hipSuccess;
@@ -1744,11 +1758,14 @@ hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, i
     }
     return hipGetLastError();
 }
-hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st) {
-    if (b.n <= 0) return hipSuccess;
+hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st, const Pos3Batch* p3) {
+    if (b.n <= 0) return p3 ? launch_wgrad_pos3(*p3, st) : hipSuccess;
     if (b.n > kMaxWsJobs || b.wgs <= 0) return hipErrorInvalidValue;
-    if (math == MATH_BF16) hipLaunchKernelGGL(k_wgrad_ws_batch<1>, dim3(b.wgs), dim3(kWsThreads), 0, st, b);
-    else hipLaunchKernelGGL(k_wgrad_ws_batch<3>, dim3(b.wgs), dim3(kWsThreads), 0, st, b);
+    Pos3Batch none{};
+    const Pos3Batch& q = p3 ? *p3 : none;
+    const dim3 g(b.wgs + (q.ce + q.cn + 1) / 2);
+    if (math == MATH_BF16) hipLaunchKernelGGL(k_wgrad_ws_batch<1>, g, dim3(kWsThreads), 0, st, b, q);
+    else hipLaunchKernelGGL(k_wgrad_ws_batch<3>, g, dim3(kWsThreads), 0, st, b, q);
     return hipGetLastError();
 }
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {

@@ -80,28 +80,33 @@ struct TeamFrags {
 #pragma unroll
         for (int p = 0; p < NP; ++p) f[kb][p] = img[((kb * nt_out + T) * 3 + p) * 64 + lane];
     }
+    template <int K = NKB>
     __device__ __forceinline__ void load(const uint4* __restrict__ img, int nt_out, int T, int lane) {
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) load_kb(img, nt_out, T, lane, kb);
+        for (int kb = 0; kb < K; ++kb) load_kb(img, nt_out, T, lane, kb);
     }
 };
 
 // acc = Σ_kb W(kb, T)ᵀ·B(kb) (tgemm_x6's per-tile sum); getsp(kb, sp) supplies k-block kb's split
 // B operand. K-block kb+1's operand is requested before kb's products issue; after k-block kb,
 // next(kb) may refill f[kb] with the next layer's fragment.
-template <int NKB, int NP, class GetSp, class Next>
+// K (default: all NKB) k-blocks: a layer of fewer k-blocks may run on the first K fragments of a
+// larger set (one fragment array serves a 10-k-block layer and the 7-k-block layers after it)
+template <int K = -1, int NKB, int NP, class GetSp, class Next>
 __device__ __forceinline__ f32x16 team_gemm(TeamFrags<NKB, NP>& F, GetSp&& getsp, Next&& next, f32x16 acc = zero16()) {
+    constexpr int NK = K < 0 ? NKB : K;
+    static_assert(NK <= NKB, "k-blocks beyond the fragment set");
     uint32_t sp[2][3][4];
     getsp(0, sp[0]);
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
+    for (int kb = 0; kb < NK; ++kb) {
         bf16x8 a[3], b[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             a[p] = as_bf16x8(p < NP ? F.f[kb][p] : make_uint4(0u, 0u, 0u, 0u));
             b[p] = as_bf16x8(make_uint4(sp[kb & 1][p][0], sp[kb & 1][p][1], sp[kb & 1][p][2], sp[kb & 1][p][3]));
         }
-        if (kb + 1 < NKB) getsp(kb + 1, sp[(kb + 1) & 1]);
+        if (kb + 1 < NK) getsp(kb + 1, sp[(kb + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         acc = mfma32_x6<NP>(a, b, acc);
         next(kb);
@@ -169,6 +174,72 @@ struct TeamRegs {
         split8(v, sp);
     }
 };
+// threadIdx.x & 63, opaque to the compiler: a body inlined into a loop (k_fwd_fused_team) would
+// otherwise have its ≈ 50 per-lane fragment offsets hoisted out of the loop and live across it
+__device__ __forceinline__ int opaque_lane() {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+// The node rows of a team node body. Lane j's column of every node tile is node n: in a 32-node
+// block launch n = 32·nb + j (lanes past the batch compute on padding rows and store zeros there, as
+// the wide kernels do); in a fused wave-tile launch n = n0 + j for j < nn, the other lanes repeat
+// row n0 and store nothing (their columns never mix with the valid ones). oN/oE are the chunk-major
+// block offsets of n's block; vl is the "lane" the cm helpers take: the lane's half, n's row in its
+// block. nc is n clamped into the batch (input arrays of n_nodes rows).
+struct TeamRows {
+    int n, nc, vl;
+    bool valid, zero_pad;
+    int64_t oN, oE;
+    __device__ __forceinline__ static TeamRows block(int nb, int n_nodes, int lane) {
+        TeamRows R;
+        R.n = nb * 32 + (lane & 31);
+        R.valid = R.n < n_nodes;
+        R.nc = R.valid ? R.n : n_nodes - 1;
+        R.zero_pad = true;
+        R.oN = (int64_t)nb * kCmBlkN;
+        R.oE = (int64_t)nb * kCmBlk;
+        R.vl = lane;
+        return R;
+    }
+    __device__ __forceinline__ static TeamRows tile(int n0, int nn, int lane) {
+        TeamRows R;
+        const int j = lane & 31;
+        R.valid = j < nn;
+        R.n = R.nc = n0 + (R.valid ? j : 0);
+        R.zero_pad = false;
+        R.oN = (int64_t)(R.n >> 5) * kCmBlkN;
+        R.oE = (int64_t)(R.n >> 5) * kCmBlk;
+        R.vl = (lane & 32) | (R.n & 31);
+        return R;
+    }
+    // the same rows, opaque to the compiler (see opaque_lane): taken once per step of a fused loop
+    __device__ __forceinline__ TeamRows opaque() const {
+        TeamRows R = *this;
+        asm volatile("" : "+v"(R.n), "+v"(R.nc), "+v"(R.vl), "+v"(R.oN), "+v"(R.oE));
+        return R;
+    }
+    // a node tile's store: valid lanes their row; padding lanes of a block launch zeros
+    template <int KH>
+    __device__ __forceinline__ void store(float* __restrict__ base, const f32x16& x, int t) const {
+        const int64_t o = KH == kKhE ? oE : oN;
+        if (valid) store_cm_tile<KH>(base + o, x, t, vl);
+        else if (zero_pad) store_cm_tile<KH>(base + o, zero16(), t, vl);
+    }
+    // a store the block kernels make for every lane (padding rows get the padding lanes' values)
+    template <int KH>
+    __device__ __forceinline__ void store_all(float* __restrict__ base, const f32x16& x, int t) const {
+        if (valid || zero_pad) store_cm_tile<KH>(base + (KH == kKhE ? oE : oN), x, t, vl);
+    }
+    template <int KH>
+    __device__ __forceinline__ f32x16 load(const float* __restrict__ base, int t) const {
+        return load_cm_tile<KH>(base + (KH == kKhE ? oE : oN), t, vl);
+    }
+    template <int KH>
+    __device__ __forceinline__ void half(TeamHalf<KH>& hr, const float* __restrict__ base) const {
+        hr.load(base + (KH == kKhE ? oE : oN), vl);
+    }
+};
 template <int KH>
 __device__ __forceinline__ void store_cm_tile_b16(uint16_t* __restrict__ blk, const f32x16& x, int t, int lane) {
     const int j = lane & 31, h = lane >> 5;
@@ -212,8 +283,7 @@ __device__ __forceinline__ void bias_act_tile(f32x16& x, const float (&bv)[16]) 
 // rm encoder (k_enc_edge_x6's chain, Networks.py:75,77): d → relu(rm.0) → 3 × (150×150 + relu) →
 // dropout = c_r → A = c_r·W1a + b1, one 32-edge block per 5-wave workgroup.
 template <bool TRAIN, int NP, bool B16>
-__device__ __forceinline__ void enc_edge_team_body(const EncEdgeArgs& a, int blk) {
-    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];   // ≤ 60 KiB
+__device__ __forceinline__ void enc_edge_team_body(const EncEdgeArgs& a, int blk, uint4* act_s) {
     const TeamAct<kTeamEdge, NP> act{act_s};
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -291,19 +361,18 @@ __device__ __forceinline__ void enc_edge_team_body(const EncEdgeArgs& a, int blk
 }
 template <bool TRAIN, int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_team(EncEdgeArgs a) {
-    enc_edge_team_body<TRAIN, NP, B16>(a, blockIdx.x);
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];   // ≤ 60 KiB
+    enc_edge_team_body<TRAIN, NP, B16>(a, blockIdx.x, act_s);
 }
 
 // ------------------------------------------------------------------------------------------------
 // rm encoder backward (k_enc_edge_bwd_x6's chain): dc_r = dA·W1aᵀ (B from the dA half rows, read by
 // every wave), then dz4 .. dz1 through the rm layers' transposed images.
 template <int NP, bool B16>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_bwd_team(EncEdgeBwdArgs a) {
-    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+__device__ __forceinline__ void enc_edge_bwd_team_body(const EncEdgeBwdArgs& a, int blk, uint4* act_s) {
     const TeamAct<kTeamEdge, NP> act{act_s};
-    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5, j = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int blk = blockIdx.x;
     const int64_t e = (int64_t)blk * 32 + j;
     TeamFrags<10, NP> F;
     F.load(a.x_w1at, 5, T, lane);
@@ -345,22 +414,25 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_bwd_team(EncEdgeBwd
             });
     }
 }
+template <int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_enc_edge_bwd_team(EncEdgeBwdArgs a) {
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    enc_edge_bwd_team_body<NP, B16>(a, blockIdx.x, act_s);
+}
 
 // ------------------------------------------------------------------------------------------------
 // om encoder (k_enc_node_x6's chain, Networks.py:76,78): every wave rebuilds the four tiles of
 // z1 = relu(om.0(y, w)) and of P0 (the 'propagation' input) in registers — cheap VALU and loads — so
 // no layer output crosses waves: wave T < 4 owns tile T of c_o, waves 0..4 tile T of U0 and V0.
 template <int NP>
-__device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, int nb) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+__device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, const TeamRows& R) {
+    const int lane = threadIdx.x & 63, h = lane >> 5;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int n = nb * 32 + j;
-    const bool valid = n < a.n_nodes;
-    const int nc = valid ? n : a.n_nodes - 1;
+    const int n = R.n, nc = R.nc;
+    const bool valid = R.valid;
     TeamFrags<7, NP> F;
     if (T < 4) F.load(a.x_om1, 4, T, lane);
     else F.load(a.x_w1b, 5, T, lane);
-    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;
     if (T < 4) {
         const float4 p = reinterpret_cast<const float4*>(a.pos)[nc];
         f32x16 Z[4];
@@ -376,7 +448,7 @@ __device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, int nb)
 #pragma unroll
             for (int t = 1; t < 4; ++t)
                 if (T == t) zt = Z[t];
-            store_cm_tile<kKhN>(a.zo1 + bN, zt, T, lane, valid);
+            R.store<kKhN>(a.zo1, zt, T);
         }
         float bv[16];
         bias_tile(bv, a.b_om1, T, h);
@@ -390,7 +462,7 @@ __device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, int nb)
                 C[r] = drop_keep(key, (uint32_t)f, a.thresh) ? C[r] * a.scale : 0.f;
             }
         }
-        store_cm_tile<kKhN>(a.co + bN, C, T, lane, valid);
+        R.store<kKhN>(a.co, C, T);
     }
     // P0: the 'propagation' input (Networks.py:29,79), ld 100 → workspace ld 128
     f32x16 P[4];
@@ -408,16 +480,16 @@ __device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, int nb)
 #pragma unroll
         for (int t = 1; t < 4; ++t)
             if (T == t) pt = P[t];
-        store_cm_tile<kKhN>(a.P0 + bN, pt, T, lane, valid);
+        R.store<kKhN>(a.P0, pt, T);
     }
     f32x16 U = team_gemm(F, TeamRegs<4>{P}, [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
-    store_cm_tile<kKhE>(a.U0 + bE, U, T, lane, valid);
+    R.store<kKhE>(a.U0, U, T);
     U = team_gemm(F, TeamRegs<4>{P}, [&](int) {});
-    store_cm_tile<kKhE>(a.V0 + bE, U, T, lane, valid);
+    R.store<kKhE>(a.V0, U, T);
 }
 template <int NP>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_node_team(EncNodeArgs a) {
-    enc_node_team_body<NP>(a, blockIdx.x);
+    enc_node_team_body<NP>(a, TeamRows::block(blockIdx.x, a.n_nodes, threadIdx.x & 63));
 }
 // Both encoders of a small batch in ONE launch (they are independent): workgroups [0, n_eblocks) run
 // the relation encoder's blocks, the rest the object encoder's node blocks — one dependent launch and
@@ -425,35 +497,33 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_node_team(EncNodeArgs a)
 // run beside the relation encoder's 16 instead of before it).
 template <bool TRAIN, int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_pair_team(EncEdgeArgs e, EncNodeArgs n) {
-    if ((int)blockIdx.x < e.n_eblocks) enc_edge_team_body<TRAIN, NP, B16>(e, blockIdx.x);
-    else enc_node_team_body<NP>(n, (int)blockIdx.x - e.n_eblocks);
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    if ((int)blockIdx.x < e.n_eblocks) enc_edge_team_body<TRAIN, NP, B16>(e, blockIdx.x, act_s);
+    else enc_node_team_body<NP>(n, TeamRows::block((int)blockIdx.x - e.n_eblocks, n.n_nodes, threadIdx.x & 63));
 }
 
 // ------------------------------------------------------------------------------------------------
 // node side of one step (k_node_fwd_x6's chain, Networks.py:88-96): waves 0..3 own the four node
 // tiles of a, o1, x' and P' (three LDS exchanges), all five waves one tile each of U', V'.
 template <int NP>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_node_fwd_team(NodeFwdArgs a) {
-    __shared__ uint4 act_s[2 * 4 * 2 * NP * 64];
+__device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const TeamRows& R, uint4* act_s) {
     const TeamAct<4, NP> act{act_s};
-    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nb = blockIdx.x;
-    const bool valid = nb * 32 + j < a.n_nodes;
-    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;
+    const bool valid = R.valid;
     const bool nw = T < 4;   // node-tile wave
-    TeamFrags<10, NP> F10;
-    TeamFrags<7, NP> F;
+    // one fragment set: W3a's ten k-blocks, refilled k-block by k-block with the 7-k-block layers
+    TeamFrags<10, NP> F;
     const uint4* const first7 = a.cw_in ? a.x_wo1a : a.x_wo1c;
-    if (nw) F10.load(a.x_w3a, 4, T, lane);
+    if (nw) F.load(a.x_w3a, 4, T, lane);
     f32x16 O;
     if (nw) {
         // a = tanh([H2s | deg]·[W3; b3])   (Networks.py:88, layer 3 after the sum)
         f32x16 E;
         {
             TeamHalf<kKhE> hr;
-            hr.load(a.H2s + bE, lane);
-            E = team_gemm(F10, hr, [&](int kb) {
+            R.half(hr, a.H2s);
+            E = team_gemm(F, hr, [&](int kb) {
                 if (kb < 7) F.load_kb(first7, 4, T, lane, kb);
             });
         }
@@ -462,31 +532,31 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_node_fwd_team(NodeFwdArgs a)
             const int f = rho(r, 0) + 4 * h + 32 * T;
             E[r] = f < kFN ? fast_tanh(E[r]) : 0.f;
         }
-        if (a.a_out) store_cm_tile<kKhN>(a.a_out + bN, E, T, lane, valid);
+        if (a.a_out) R.store<kKhN>(a.a_out, E, T);
         act.put(0, T, E, lane);
         // o1 = relu([c_o | a | P]·Wo1 + bo1): c_o·Wo1c (or step 0's stored accumulator) first
         if (a.cw_in) {
-            O = load_cm_tile<kKhN>(a.cw_in + bN, T, lane);
+            O = R.load<kKhN>(a.cw_in, T);
         } else {
             TeamHalf<kKhN> hr;
-            hr.load(a.co + bN, lane);
-            O = team_gemm(F, hr, [&](int kb) { F.load_kb(a.x_wo1a, 4, T, lane, kb); });
-            if (a.cw_out) store_cm_tile<kKhN>(a.cw_out + bN, O, T, lane);
+            R.half(hr, a.co);
+            O = team_gemm<7>(F, hr, [&](int kb) { F.load_kb(a.x_wo1a, 4, T, lane, kb); });
+            if (a.cw_out) R.store_all<kKhN>(a.cw_out, O, T);
         }
     }
     team_sync();
     if (nw) {
-        O = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
+        O = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
                       [&](int kb) { F.load_kb(a.x_wo1p, 4, T, lane, kb); }, O);
         {
             TeamHalf<kKhN> hr;
-            hr.load(a.P + bN, lane);
+            R.half(hr, a.P);
             float bv[16];
             bias_tile(bv, a.bo1, T, h);
-            O = team_gemm(F, hr, [&](int kb) { F.load_kb(a.x_wo2, 4, T, lane, kb); }, O);
+            O = team_gemm<7>(F, hr, [&](int kb) { F.load_kb(a.x_wo2, 4, T, lane, kb); }, O);
             bias_act_tile<true>(O, bv);
         }
-        if (a.o1_out) store_cm_tile<kKhN>(a.o1_out + bN, O, T, lane, valid);
+        if (a.o1_out) R.store<kKhN>(a.o1_out, O, T);
         act.put(1, T, O, lane);
     }
     team_sync();
@@ -494,123 +564,134 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_node_fwd_team(NodeFwdArgs a)
         // x' = o1·Wo2' + bo2'; P' = tanh(x'[0:100] + P); logit = x'[100]  (Networks.py:91, 94)
         float bv[16];
         bias_tile(bv, a.bo2p, T, h);
-        const f32x16 P = load_cm_tile<kKhN>(a.P + bN, T, lane);
-        f32x16 X = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
+        const f32x16 P = R.load<kKhN>(a.P, T);
+        f32x16 X = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
                              [&](int kb) {
                                  if (a.U) F.load_kb(a.x_w1b, 5, T, lane, kb);
                              });
         bias_act_tile<false>(X, bv);
-        if (T == 3 && a.logits && h == 1 && valid) a.logits[nb * 32 + j] = X[0];   // x' row 100 = rho(0, 1) + 96
+        if (T == 3 && a.logits && h == 1 && valid) a.logits[R.n] = X[0];   // x' row 100 = rho(0, 1) + 96
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * T;
             X[r] = f < kFN ? fast_tanh(X[r] + P[r]) : 0.f;   // X := P'
         }
-        store_cm_tile<kKhN>(a.Pn + bN, X, T, lane, valid);
+        R.store<kKhN>(a.Pn, X, T);
         act.put(0, T, X, lane);
     } else if (a.U) {
-        F.load(a.x_w1b, 5, T, lane);
+        F.template load<7>(a.x_w1b, 5, T, lane);
     }
     team_sync();
     if (a.U) {   // U' = P'·W1b, V' = P'·W1c for the next step
-        f32x16 U = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
+        f32x16 U = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
                              [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
-        store_cm_tile<kKhE>(a.U + bE, U, T, lane, valid);
-        U = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
-        store_cm_tile<kKhE>(a.V + bE, U, T, lane, valid);
+        R.store<kKhE>(a.U, U, T);
+        U = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
+        R.store<kKhE>(a.V, U, T);
     }
+}
+
+template <int NP>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_node_fwd_team(NodeFwdArgs a) {
+    __shared__ uint4 act_s[2 * 4 * 2 * NP * 64];
+    node_fwd_team_body<NP>(a, TeamRows::block(blockIdx.x, a.n_nodes, threadIdx.x & 63), act_s);
 }
 
 // ------------------------------------------------------------------------------------------------
 // node side of one backward step (k_node_bwd_x6's chain, x6/bf16 math with dco_sum): waves 0..3 own
-// the node tiles of dP, dx, do1, dP_out and g (two LDS exchanges), all five waves one tile of G3.
-template <int NP>
-__global__ __launch_bounds__(256, 1) void k_node_bwd_team(NodeBwdArgs a) {
-    __shared__ uint4 act_s[2 * 4 * 2 * NP * 64];
+// the node tiles of dP, dx, do1, dP_out and g (two LDS exchanges), then one tile each of G3 — the
+// fifth tile by wave 0 (NW = 4: one wave per SIMD, the block launch) or by wave 4 (NW = 5: the fused
+// backward's five-wave workgroup; wave 4 only takes the barriers until then).
+template <int NP, int NW>
+__device__ __forceinline__ void node_bwd_team_body(const NodeBwdArgs& a, const TeamRows& R, uint4* act_s) {
     const TeamAct<4, NP> act{act_s};
-    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nb = blockIdx.x;
-    const bool valid = nb * 32 + j < a.n_nodes;
-    const int64_t bN = (int64_t)nb * kCmBlkN, bE = (int64_t)nb * kCmBlk;
-    constexpr bool nw = true;   // four waves, one per SIMD (the full register file: 512 per lane)
-    TeamFrags<10, NP> F10;
-    TeamFrags<7, NP> F;
-    if (nw && !a.first) F10.load(a.x_w1bt, 4, T, lane);
-    else if (nw && !a.tail) F.load(a.x_wo2t, 4, T, lane);
+    const bool valid = R.valid;
+    const bool nw = NW == 4 || T < 4;   // node-tile wave
+    // one fragment set: W1bᵀ/W1cᵀ's ten k-blocks, then the 7-k-block layers
+    TeamFrags<10, NP> F;
+    if (nw && !a.first) F.load(a.x_w1bt, 4, T, lane);
+    else if (nw && !a.tail) F.template load<7>(a.x_wo2t, 4, T, lane);
+    else if (!nw && !a.tail) F.template load<7>(a.x_w3t, 5, 4, lane);   // wave 4: G3 tile 4
     f32x16 D = zero16();
     if (nw && !a.first) {   // dP = dPin + dU·W1bᵀ + dV·W1cᵀ
-        D = load_cm_tile<kKhN>(a.dPin + bN, T, lane);
+        D = R.load<kKhN>(a.dPin, T);
         TeamHalf<kKhE> hr;
-        hr.load(a.dU + bE, lane);
-        D = team_gemm(F10, hr, [&](int kb) { F10.load_kb(a.x_w1ct, 4, T, lane, kb); }, D);
-        hr.load(a.dV + bE, lane);
-        D = team_gemm(F10, hr, [&](int) {}, D);
-        if (!a.tail) F.load(a.x_wo2t, 4, T, lane);
+        R.half(hr, a.dU);
+        D = team_gemm(F, hr, [&](int kb) { F.load_kb(a.x_w1ct, 4, T, lane, kb); }, D);
+        R.half(hr, a.dV);
+        D = team_gemm(F, hr, [&](int kb) {
+            if (!a.tail && kb < 7) F.load_kb(a.x_wo2t, 4, T, lane, kb);
+        }, D);
     }
     if (a.tail) {   // dP0 = d/d 'propagation' (ld 100)
         if (nw && valid) {
-            const int64_t n = (int64_t)nb * 32 + j;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int f0 = 32 * T + 8 * q + 4 * h;
-                if (f0 < kFN) *reinterpret_cast<float4*>(a.dprop + n * kFN + f0) = make_float4(D[4 * q], D[4 * q + 1], D[4 * q + 2], D[4 * q + 3]);
+                if (f0 < kFN) *reinterpret_cast<float4*>(a.dprop + (int64_t)R.n * kFN + f0) = make_float4(D[4 * q], D[4 * q + 1], D[4 * q + 2], D[4 * q + 3]);
             }
         }
         return;
     }
     f32x16 dP;
     if (nw) {
-        const f32x16 Pn = load_cm_tile<kKhN>(a.Pn + bN, T, lane);
+        const f32x16 Pn = R.load<kKhN>(a.Pn, T);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * T;
             D[r] = f < kFN ? D[r] * (1.f - Pn[r] * Pn[r]) : 0.f;   // tanh' (Networks.py:91)
         }
         // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
-        store_cm_tile<kKhN>(a.dPout + bN, D, T, lane, valid);
+        R.store<kKhN>(a.dPout, D, T);
         dP = D;
-        if (a.first && T == 3 && h == 1) D[0] = valid ? a.dlogits[nb * 32 + j] : 0.f;   // x' row 100 = logit
-        store_cm_tile<kKhN>(a.dx + bN, D, T, lane, valid);
+        if (a.first && T == 3 && h == 1) D[0] = valid ? a.dlogits[R.n] : 0.f;   // x' row 100 = logit
+        R.store<kKhN>(a.dx, D, T);
         act.put(0, T, D, lane);
     }
     team_sync();
     if (nw) {   // do1 = dx'·Wo2'ᵀ ⊙ [o1 > 0]
-        const f32x16 O1 = load_cm_tile<kKhN>(a.o1 + bN, T, lane);
-        f32x16 G = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
-                             [&](int kb) { F.load_kb(a.x_wo1pt, 4, T, lane, kb); });
+        const f32x16 O1 = R.load<kKhN>(a.o1, T);
+        f32x16 G = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
+                                [&](int kb) { F.load_kb(a.x_wo1pt, 4, T, lane, kb); });
 #pragma unroll
         for (int r = 0; r < 16; ++r) G[r] = O1[r] > 0.f ? G[r] : 0.f;
-        store_cm_tile<kKhN>(a.do1 + bN, G, T, lane, valid);
+        R.store<kKhN>(a.do1, G, T);
         act.put(1, T, G, lane);
     }
     team_sync();
     if (nw) {
         // P part of omp's input → dP_s
-        D = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
-                      [&](int kb) { F.load_kb(a.x_wo1at, 4, T, lane, kb); });
+        D = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
+                         [&](int kb) { F.load_kb(a.x_wo1at, 4, T, lane, kb); });
 #pragma unroll
         for (int r = 0; r < 16; ++r) D[r] += dP[r];
-        store_cm_tile<kKhN>(a.dPout + bN, D, T, lane, valid);
+        R.store<kKhN>(a.dPout, D, T);
         // effect part → g = da ⊙ (1 − a²)
-        const f32x16 Aa = load_cm_tile<kKhN>(a.a + bN, T, lane);
-        D = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
-                      [&](int kb) { F.load_kb(a.x_w3t, 5, T, lane, kb); });
+        const f32x16 Aa = R.load<kKhN>(a.a, T);
+        D = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(1, kb, sp, lane); },
+                         [&](int kb) { F.load_kb(a.x_w3t, 5, T, lane, kb); });
 #pragma unroll
         for (int r = 0; r < 16; ++r) D[r] = D[r] * (1.f - Aa[r] * Aa[r]);
-        store_cm_tile<kKhN>(a.g + bN, D, T, lane, valid);
+        R.store<kKhN>(a.g, D, T);
         act.put(0, T, D, lane);
     }
     team_sync();
-    // G3 = g·W3ᵀ (the per-edge dh2 is G3[receiver]): tile T, and wave 0 also tile 4
-    f32x16 H = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int kb) {
-        if (T == 0) F.load_kb(a.x_w3t, 5, 4, lane, kb);
+    // G3 = g·W3ᵀ (the per-edge dh2 is G3[receiver]): tile T (wave 4: tile 4), and NW = 4's wave 0 tile 4
+    f32x16 H = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int kb) {
+        if (NW == 4 && T == 0) F.load_kb(a.x_w3t, 5, 4, lane, kb);
     });
-    store_cm_tile<kKhE>(a.G3 + bE, H, T, lane, valid);
-    if (T == 0) {
-        H = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
-        store_cm_tile<kKhE>(a.G3 + bE, H, 4, lane, valid);
+    R.store<kKhE>(a.G3, H, T);
+    if (NW == 4 && T == 0) {
+        H = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
+        R.store<kKhE>(a.G3, H, 4);
     }
+}
+template <int NP>
+__global__ __launch_bounds__(256, 1) void k_node_bwd_team(NodeBwdArgs a) {
+    __shared__ uint4 act_s[2 * 4 * 2 * NP * 64];
+    node_bwd_team_body<NP, 4>(a, TeamRows::block(blockIdx.x, a.n_nodes, threadIdx.x & 63), act_s);
 }
 
 // ---- edge side of one propagation step (k_edge_fwd_x6 for ≤ 16-node wave-tiles), team form ----
@@ -622,12 +703,10 @@ __global__ __launch_bounds__(256, 1) void k_node_bwd_team(NodeBwdArgs a) {
 // H2s and both masks are bit-identical. Wave 0 writes the h1 > 0 words, wave T the h2 > 0 word of
 // tile T (wave 0 also the zero padding words 5-7).
 template <int NP, bool AB16>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a) {
+__device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt) {
     constexpr int PF = 2;   // A/U/V k-blocks in flight
-    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int wt = blockIdx.x;
-    if (wt >= a.n_wtiles) return;
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     uint4 wf[10][NP];   // tile T's W2 fragments, all ten k-blocks
@@ -799,18 +878,83 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a)
     }
 }
 
+template <int NP, bool AB16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a) {
+    if ((int)blockIdx.x < a.n_wtiles) edge_fwd_team_body<NP, AB16>(a, blockIdx.x);
+}
+
+// ---- a small batch's forward in one launch (FwdFusedArgs, kernels.h) ----
+// One workgroup of five waves per wave-tile: the relation encoder on each of the tile's blocks, the
+// object encoder on the tile's node rows, then per step the edge side (H2s of the tile's nodes) and
+// the node side (P', U', V' of the same rows). The phases are the team kernels' bodies unchanged —
+// same products in the same order, so every output is bit-identical to the launch-per-phase chain
+// (tests/test_gpu_team.py) — and are separated by workgroup barriers instead of kernel boundaries:
+// a wave-tile holds whole towers, so every row a phase reads was written by this workgroup.
+// a pointer the compiler must treat as new in every step: keeps the bodies' per-lane fragment
+// addresses from being hoisted out of the step loop (they would stay live across it and spill)
+template <class T>
+__device__ __forceinline__ void opaque(T*& p) {
+    asm volatile("" : "+s"(p));
+}
+template <bool TRAIN, int NP, bool AB16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs a) {
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    const int wt = blockIdx.x;
+    const int4 info = reinterpret_cast<const int4*>(a.ef.wtile)[wt];
+    for (int b = 0; b < info.y; ++b) enc_edge_team_body<TRAIN, NP, AB16>(a.ee, info.x + b, act_s);
+    const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
+    enc_node_team_body<NP>(a.en, R);
+    __syncthreads();   // A, U0, V0 of the tile
+    for (int s = 0; s < a.S; ++s) {
+        const int64_t sE = (int64_t)(a.training ? s : 0) * a.rowsE;   // Ws::U_at / V_at / H2s_at
+        EdgeFwdArgs ef = a.ef;
+        opaque(ef.x_w2);
+        opaque(ef.b2);
+        opaque(ef.A);
+        ef.U += sE;
+        ef.V += sE;
+        ef.H2s += sE;
+        if (ef.mask1) ef.mask1 += s * a.m1_step;
+        if (ef.mask2) ef.mask2 += s * a.m2_step;
+        edge_fwd_team_body<NP, AB16>(ef, wt);
+        __syncthreads();   // H2s of step s
+        NodeFwdArgs nf = a.nf;
+        opaque(nf.x_w3a);
+        opaque(nf.x_wo1c);
+        opaque(nf.x_wo1a);
+        opaque(nf.x_wo1p);
+        opaque(nf.x_wo2);
+        opaque(nf.x_w1b);
+        opaque(nf.x_w1c);
+        opaque(nf.bo1);
+        opaque(nf.bo2p);
+        opaque(nf.co);
+        nf.H2s = ef.H2s;
+        nf.P += (int64_t)(a.training ? s : (s & 1)) * a.rowsN;                 // Ws::P_at(s)
+        nf.Pn = const_cast<float*>(a.nf.P) + (int64_t)(a.training ? s + 1 : ((s + 1) & 1)) * a.rowsN;
+        if (nf.a_out) nf.a_out += (int64_t)s * a.rowsN;
+        if (nf.o1_out) nf.o1_out += (int64_t)s * a.rowsN;
+        nf.cw_out = s == 0 ? a.nf.cw_out : nullptr;
+        nf.cw_in = s > 0 ? a.nf.cw_out : nullptr;
+        nf.logits = s == a.S - 1 ? a.logits : nullptr;
+        const int64_t sE1 = (int64_t)(a.training ? s + 1 : 0) * a.rowsE;
+        nf.U = s + 1 < a.S ? const_cast<float*>(a.ef.U) + sE1 : nullptr;   // the same workspace arrays
+        nf.V = s + 1 < a.S ? const_cast<float*>(a.ef.V) + sE1 : nullptr;
+        node_fwd_team_body<NP>(nf, R.opaque(), act_s);
+        __syncthreads();   // P', U', V' of step s + 1
+    }
+}
+
 // ---- edge side of one backward step (k_edge_bwd_x6 without dA: x6/bf16 rebuild it), team form ----
 // Five waves per wave-tile; wave T owns feature tile T of dh1 = dh2pre·W2ᵀ: every wave builds the
 // whole dh2pre = G3[receiver] ⊙ [h2 > 0] operand k-block by k-block, multiplies it by its tile's W2ᵀ
 // fragments (from the x6 image in L2), masks with [h1 > 0] and runs tile T's one-hot receiver/sender
 // sums — k_edge_bwd_x6's products in its per-accumulator order, so dU and dV are bit-identical.
 template <int NP>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_edge_bwd_team(EdgeBwdArgs a) {
+__device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt) {
     constexpr int PF = 2;
-    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int wt = blockIdx.x;
-    if (wt >= a.n_wtiles) return;
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     uint4 wf[10][NP];   // tile T's W2ᵀ fragments
@@ -912,16 +1056,18 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_edge_bwd_team(EdgeBwdArgs a)
         }
     }
 }
+template <int NP>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_edge_bwd_team(EdgeBwdArgs a) {
+    if ((int)blockIdx.x < a.n_wtiles) edge_bwd_team_body<NP>(a, blockIdx.x);
+}
 
 // ---- dA = Σ_s dh1pre_s (k_dA_x6), team form: five waves per 32-edge block, wave T owns feature
 // tile T; the same products, per-accumulator order and step order (S−1 first) as k_dA_x6.
 template <int NP, bool B16>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_dA_team(DaArgs a) {
+__device__ __forceinline__ void dA_team_body(const DaArgs& a, int blk) {
     constexpr int PF = 2;
-    const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int blk = blockIdx.x;
-    if (blk >= a.n_eblocks) return;
     uint4 wf[10][NP];   // tile T's W2ᵀ fragments
 #pragma unroll
     for (int kb = 0; kb < 10; ++kb)
@@ -988,27 +1134,31 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_dA_team(DaArgs a) {
         for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * T] = dacc[r];
     }
 }
+template <int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_dA_team(DaArgs a) {
+    if ((int)blockIdx.x < a.n_eblocks) dA_team_body<NP, B16>(a, blockIdx.x);
+}
 
 // ---- object-encoder backward (k_enc_node_bwd_x6), team form: four waves per 32-node block, wave T
 // owns feature tile T of dc_o = (Σ_s do1_s)·Wo1cᵀ and of the om.1ᵀ product; the layer input is
 // exchanged through LDS in its split C layout. Same products and order: bit-identical.
-template <int NP>
-__global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
-    __shared__ uint4 act_s[4 * 2 * NP * 64];
+// NW = 5 (the fused backward): wave 4 takes the barrier only
+template <int NP, int NW>
+__device__ __forceinline__ void enc_node_bwd_team_body(const EncNodeBwdArgs& a, const TeamRows& R, uint4* act_s) {
     const TeamAct<4, NP> act{act_s};
-    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+    const int lane = opaque_lane(), h = lane >> 5;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nb = blockIdx.x;
-    const int n = nb * 32 + j;
-    const bool valid = n < a.n_nodes;
-    const int64_t bN = (int64_t)nb * kCmBlkN;
+    if (NW == 5 && T == 4) {
+        team_sync();
+        return;
+    }
     TeamFrags<7, NP> F;
     F.load(a.x_wo1ct, 4, T, lane);
     // Σ_s do1_s in backward step order S-1..0 (the Y of the Wo1c weight gradient), every tile
     f32x16 E[4], Z[4];
-    load_cm<4>(a.do1 + (int64_t)(a.S - 1) * a.do1_step + bN, E, lane);
+    load_cm<4>(a.do1 + (int64_t)(a.S - 1) * a.do1_step + R.oN, E, R.vl);
     for (int s = a.S - 2; s >= 0; --s) {
-        load_cm<4>(a.do1 + (int64_t)s * a.do1_step + bN, Z, lane);
+        load_cm<4>(a.do1 + (int64_t)s * a.do1_step + R.oN, Z, R.vl);
 #pragma unroll
         for (int t = 0; t < 4; ++t) E[t] += Z[t];
     }
@@ -1017,21 +1167,21 @@ __global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
 #pragma unroll
         for (int t = 1; t < 4; ++t)
             if (T == t) et = E[t];
-        store_cm_tile<kKhN>(a.dco + bN, et, T, lane, valid);
+        R.store<kKhN>(a.dco, et, T);
     }
     f32x16 D = team_gemm(F, TeamRegs<4>{E}, [&](int kb) { F.load_kb(a.x_om1t, 4, T, lane, kb); });   // dc_o
-    const f32x16 C = load_cm_tile<kKhN>(a.co + bN, T, lane);
+    const f32x16 C = R.load<kKhN>(a.co, T);
 #pragma unroll
     for (int r = 0; r < 16; ++r) D[r] = C[r] > 0.f ? D[r] * a.scale : 0.f;
-    store_cm_tile<kKhN>(a.dzo2 + bN, D, T, lane, valid);
+    R.store<kKhN>(a.dzo2, D, T);
     act.put(0, T, D, lane);
     team_sync();
     f32x16 G = team_gemm(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
     f32x16 Zt;
     if (a.zo1) {
-        Zt = load_cm_tile<kKhN>(a.zo1 + bN, T, lane);
+        Zt = R.load<kKhN>(a.zo1, T);
     } else {   // the forward's own first-layer arithmetic (k_enc_node_x6), not a stored row
-        const float4 p = reinterpret_cast<const float4*>(a.pos)[valid ? n : a.n_nodes - 1];
+        const float4 p = reinterpret_cast<const float4*>(a.pos)[R.nc];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * T;
@@ -1040,7 +1190,68 @@ __global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) G[r] = Zt[r] > 0.f ? G[r] : 0.f;
-    store_cm_tile<kKhN>(a.dzo1 + bN, G, T, lane, valid);
+    R.store<kKhN>(a.dzo1, G, T);
+}
+template <int NP>
+__global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
+    __shared__ uint4 act_s[4 * 2 * NP * 64];
+    enc_node_bwd_team_body<NP, 4>(a, TeamRows::block(blockIdx.x, a.n_nodes, threadIdx.x & 63), act_s);
+}
+
+// ---- a small batch's backward (before the weight gradients) in one launch (BwdFusedArgs) ----
+// One five-wave workgroup per wave-tile: per step S−1 .. 0 the node side (dx, do1, g, G3 and dP of
+// the tile's rows) and the edge side (dU, dV), then d/d 'propagation', the dA rebuild and the
+// relation-encoder backward on the tile's blocks, the object-encoder backward on its rows. Bodies
+// and products are the team kernels' (bit-identical results); phases meet at workgroup barriers.
+template <int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs a) {
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    const int wt = blockIdx.x;
+    const int4 info = reinterpret_cast<const int4*>(a.eb.wtile)[wt];
+    const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
+    const float* const dP0 = a.nb.dPout;   // Ws::dP_at(0); dP_at(k) alternates
+    for (int s = a.S - 1; s >= 0; --s) {
+        const bool first = s == a.S - 1;
+        const int64_t sN = (int64_t)s * a.rowsN, sE = (int64_t)s * a.rowsE;
+        NodeBwdArgs nb = a.nb;
+        opaque(nb.x_w1bt);
+        opaque(nb.x_w1ct);
+        opaque(nb.x_wo2t);
+        opaque(nb.x_wo1pt);
+        opaque(nb.x_wo1at);
+        opaque(nb.x_w3t);
+        nb.first = first;
+        nb.dPin = first ? nullptr : dP0 + ((s + 1) & 1) * a.rowsN;
+        nb.dU = first ? nullptr : a.nb.dU + sE;   // the host passes dU_at(1) / dV_at(1)
+        nb.dV = first ? nullptr : a.nb.dV + sE;
+        nb.Pn += sN;
+        nb.o1 += sN;
+        nb.a += sN;
+        nb.dx += sN;
+        nb.do1 += sN;
+        nb.g += sN;
+        nb.G3 += sE;
+        nb.dPout = const_cast<float*>(dP0) + (s & 1) * a.rowsN;
+        node_bwd_team_body<NP, 5>(nb, R.opaque(), act_s);
+        __syncthreads();   // G3 of step s
+        EdgeBwdArgs eb = a.eb;
+        opaque(eb.x_w2t);
+        eb.mask1 += s * a.m1_step;
+        eb.mask2 += s * a.m2_step;
+        eb.G3 = nb.G3;
+        eb.dU += sE;
+        eb.dV += sE;
+        edge_bwd_team_body<NP>(eb, wt);
+        __syncthreads();   // dU, dV of step s
+    }
+    if (a.has_tail) node_bwd_team_body<NP, 5>(a.tail, R, act_s);   // dP0 (reads only)
+    for (int b = 0; b < info.y; ++b) dA_team_body<NP, B16>(a.da, info.x + b);
+    __syncthreads();   // dA of the tile's blocks
+    for (int b = 0; b < info.y; ++b) {
+        enc_edge_bwd_team_body<NP, B16>(a.eeb, info.x + b, act_s);
+        __syncthreads();   // its last exchange buffer is the next body's first
+    }
+    enc_node_bwd_team_body<NP, 5>(a.enb, R, act_s);
 }
 
 bool team_blocks(int n_blocks) {
@@ -1123,6 +1334,38 @@ hipError_t launch_enc_pair_team(const EncEdgeArgs& e, const EncNodeArgs& n, int 
     } else {
         hipLaunchKernelGGL((k_enc_pair_team<false, 3, false>), g, b, 0, st, e, n);
     }
+    return hipGetLastError();
+}
+bool fwd_fused_team(int n_wtiles, int nw_max, int n_eblocks, int n_nodes, int math) {
+    return nw_max <= 16 && team_blocks(n_wtiles) && enc_pair_team(n_eblocks, n_nodes, math);
+}
+hipError_t launch_fwd_fused_team(const FwdFusedArgs& a, int math, bool train, hipStream_t st) {
+    if (!fwd_fused_team(a.ef.n_wtiles, a.ef.nw_max, a.ee.n_eblocks, a.en.n_nodes, math) || a.S < 1 || a.ef.n16 ||
+        a.nf.n16 || a.ef.recv_blocks || a.ee.b16 != a.ef.a_b16 || !a.nf.cw_out)
+        return hipErrorInvalidValue;
+    const dim3 g(a.ef.n_wtiles), b(64 * kTeamEdge);
+    if (math == MATH_BF16) {
+        if (train && a.ee.b16) hipLaunchKernelGGL((k_fwd_fused_team<true, 1, true>), g, b, 0, st, a);
+        else if (train) hipLaunchKernelGGL((k_fwd_fused_team<true, 1, false>), g, b, 0, st, a);
+        else if (!a.ee.b16) hipLaunchKernelGGL((k_fwd_fused_team<false, 1, false>), g, b, 0, st, a);
+        else return hipErrorInvalidValue;
+    } else if (math == MATH_X6 && !a.ee.b16) {
+        if (train) hipLaunchKernelGGL((k_fwd_fused_team<true, 3, false>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_fwd_fused_team<false, 3, false>), g, b, 0, st, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_bwd_fused_team(const BwdFusedArgs& a, int math, hipStream_t st) {
+    if (!fwd_fused_team(a.eb.n_wtiles, a.eb.nw_max, a.da.n_eblocks, a.nb.n_nodes, math) || a.S < 1 || !a.eb.no_dA ||
+        !a.nb.dco_sum || a.nb.n16 || a.eb.n16 || a.da.b16 != a.eeb.b16)
+        return hipErrorInvalidValue;
+    const dim3 g(a.eb.n_wtiles), b(64 * kTeamEdge);
+    if (math == MATH_BF16 && a.da.b16) hipLaunchKernelGGL((k_bwd_fused_team<1, true>), g, b, 0, st, a);
+    else if (math == MATH_BF16) hipLaunchKernelGGL((k_bwd_fused_team<1, false>), g, b, 0, st, a);
+    else if (math == MATH_X6 && !a.da.b16) hipLaunchKernelGGL((k_bwd_fused_team<3, false>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st) {

@@ -1,5 +1,7 @@
-"""Dump logits + every gradient of one bf16-math training fwd/bwd (library from SPWGNN_LIB) so two
-builds can be compared bitwise: usage python tools/b16_dump.py OUT.npz"""
+"""Dump logits + every gradient of one training fwd/bwd per batch shape and math (library from
+SPWGNN_LIB) so two builds can be compared bitwise (tools/cmp_npz.py): small batches (≤ 512 wave-tiles:
+the fused small-batch kernels), wide ones (n6w, n12w) and a ragged bf16 one.
+usage python tools/b16_dump.py OUT.npz"""
 import sys
 import os
 import numpy as np
@@ -11,7 +13,8 @@ from spwgnn_amd import TowerBatch, data as D, engine as E, params as P
 out = {}
 params = O.random_params(7)
 flat = P.to_flat(params, device="cuda")
-for name, (B, N, fully) in {"n12": (512, 12, True), "n6": (1024, 6, False)}.items():
+shapes = {"n12": (512, 12, True), "n6": (1024, 6, False), "n6w": (4096, 6, True), "n12w": (2048, 12, True)}
+for name, (B, N, fully) in shapes.items():
     obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, N, seed=3, fully_connected=fully)
     batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
     for math in ("bf16", "x6"):
