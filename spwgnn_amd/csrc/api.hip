@@ -672,8 +672,14 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         bpw = (nblk + wgs - 1) / wgs;
         chunks = (nblk + bpw - 1) / bpw;
     }
-    if (prof && g.recompute) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
-    if (ws)
+    // a small x6 batch: the W2 gradient runs inside the batched weight-gradient launch
+    const bool w2_in_batch = ws && math == MATH_X6 && wsb && team_blocks(b->n_eblocks) && !getenv_flag("SPWGNN_NO_W2_MERGE");
+    if (prof && g.recompute && !w2_in_batch) SPW_CHECK(prof->before(SPWGNN_K_WGRAD_W2));
+    if (w2_in_batch) {
+        wsb->w2 = a;
+        wsb->w2_bpw = bpw;
+        wsb->w2_wgs = (int)chunks;
+    } else if (ws)
         SPW_CHECK(launch_w2grad_ws(a, (int)chunks, bpw, math, st));
     else if (math == MATH_BF16)
         SPW_CHECK(launch_wgrad_bf16(a, (int)chunks, st, g.b16));
@@ -681,7 +687,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         return SPWGNN_E_ARG;
     else
         SPW_CHECK(launch_wgrad(a, (int)chunks, math, st));
-    if (prof && g.recompute) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
+    if (prof && g.recompute && !w2_in_batch) SPW_CHECK(prof->after(SPWGNN_K_WGRAD_W2));
     }
     const ParamTable& pt = param_table();
     ReduceArgs& ra = rb.r[rb.n++];
@@ -1037,9 +1043,9 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
     }
     // a small batch's rm.0 / om.0 gradients join the batched launch (one dependent launch fewer)
-    const bool p3_in_batch = wsb.n > 0 && team_blocks(b->n_eblocks) && !getenv_flag("SPWGNN_NO_POS3_MERGE");
+    const bool p3_in_batch = (wsb.n > 0 || wsb.w2_wgs > 0) && team_blocks(b->n_eblocks) && !getenv_flag("SPWGNN_NO_POS3_MERGE");
     if (!p3_in_batch) SPW_CHECK(launch_wgrad_pos3(p3, st));
-    if (wsb.n > 0) {
+    if (wsb.n > 0 || wsb.w2_wgs > 0) {
         SPW_CHECK(prof.before(SPWGNN_K_WGRAD_WS));
         SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st, p3_in_batch ? &p3 : nullptr));
         SPW_CHECK(prof.after(SPWGNN_K_WGRAD_WS));

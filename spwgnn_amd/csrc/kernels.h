@@ -276,6 +276,10 @@ constexpr int kMaxWsJobs = 16;
 struct WsBatch {           // the k_wgrad_ws gradients of one backward (k_wgrad_ws_batch)
     WsJob j[kMaxWsJobs];
     int n, wgs;
+    // a small batch's x6 W2 gradient (k_w2grad_ws) as the launch's last w2_wgs workgroups (0: none)
+    WgradArgs w2;
+    int64_t w2_bpw;
+    int w2_wgs;
 };
 
 constexpr int kMaxReduce = 16;

@@ -554,14 +554,13 @@ struct W2gSet {
 // DBG (diagnosis builds, SPWGNN_W2G_DBG): 1 no MFMAs, 2 gathers from stage 0, 4 no staging
 // arithmetic, 8 matrix waves at s_setprio 1, 32 no gathers
 template <int dbg, int NP = 3, bool AB16 = false>   // AB16: A stored as bf16 (bf16 math, §3g)
-__global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
+__device__ __forceinline__ void w2grad_ws_body(const WgradArgs& a, int64_t blk_per_wg, int bid,
+                                               char (*buf)[2 * kW2gImg]) {   // [stage parity][X | Y]
     using IM = X6Img<160>;
-    __shared__ __attribute__((aligned(16))) char buf[2][2 * kW2gImg];   // [stage parity][X | Y]
     const int tid = threadIdx.x;
     const int S = a.S;
     const int64_t nblk = a.RE >> 5;
-    const int64_t b0 = (int64_t)blockIdx.x * blk_per_wg;
+    const int64_t b0 = (int64_t)bid * blk_per_wg;
     const int64_t b1 = min(nblk, b0 + blk_per_wg);
     const int T = b1 > b0 ? (int)(b1 - b0) * S : 0;   // stages of this workgroup (< 2^31)
     if (tid < 256) {
@@ -608,7 +607,7 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
             }
             __syncthreads();
         }
-        float* out = a.slab + (int64_t)blockIdx.x * 160 * 160;
+        float* out = a.slab + (int64_t)bid * 160 * 160;
 #pragma unroll
         for (int x = 0; x < 5; ++x)
 #pragma unroll
@@ -725,6 +724,12 @@ void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
         ++t;
     }
     __syncthreads();   // the matrix waves' last stage
+}
+template <int dbg, int NP = 3, bool AB16 = false>
+__global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_w2grad_ws(WgradArgs a, int64_t blk_per_wg) {
+    __shared__ __attribute__((aligned(16))) char buf[2][2 * kW2gImg];
+    w2grad_ws_body<dbg, NP, AB16>(a, blk_per_wg, blockIdx.x, buf);
 }
 
 // W2 gradient with the node rows staged in LDS per (wave-tile, step) — bf16 math. The per-edge
@@ -1304,10 +1309,17 @@ template <int KH, bool NODE, bool B16>
 __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int tid);
 // A small batch's rm.0 / om.0 gradients (k_wgrad_pos3) ride in the same launch: workgroups from
 // b.wgs on run two of k_wgrad_pos3's 256-thread workgroups each (one per half), beside the jobs.
+// ... and so does its W2 gradient (k_w2grad_ws, x6): the last b.w2_wgs workgroups.
+static_assert(2 * kWsMaxBuf >= 2 * 2 * kW2gImg && kWsThreads == kW2gThreads, "W2 gradient in the batched launch");
 template <int NP>
 __global__ __launch_bounds__(kWsThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_wgrad_ws_batch(WsBatch b, Pos3Batch p3) {
     __shared__ __attribute__((aligned(16))) char smem[2 * kWsMaxBuf];
+    const int w2_first = (int)gridDim.x - b.w2_wgs;
+    if (NP == 3 && (int)blockIdx.x >= w2_first) {
+        w2grad_ws_body<0, 3, false>(b.w2, b.w2_bpw, (int)blockIdx.x - w2_first, reinterpret_cast<char (*)[2 * kW2gImg]>(smem));
+        return;
+    }
     if ((int)blockIdx.x >= b.wgs) {
         const int q = 2 * ((int)blockIdx.x - b.wgs) + (int)(threadIdx.x >> 8), tid = threadIdx.x & 255;
         if (q < p3.ce) {
@@ -1535,14 +1547,15 @@ __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int 
             const bool in = bg + u < b1;
             const int64_t b = in ? bg + u : b1 - 1;
             const int64_t row = b * 32 + i;
+            bool ok;
             if constexpr (NODE) {
-                const bool ok = in && row < a.count;
+                ok = in && row < a.count;
                 const float4 p = a.pos[ok ? row : 0];
                 x0[u] = ok ? p.y : 0.f;
                 x1[u] = ok ? p.z : 0.f;
                 x2[u] = ok ? 1.f : 0.f;
             } else {   // d from the encoder's stored per-edge (dx, dy): no dependent gathers
-                const bool ok = in && a.esrc[row] >= 0;
+                ok = in && a.esrc[row] >= 0;
                 const float2 d = a.ed[row];
                 x0[u] = ok ? d.x : 0.f;
                 x1[u] = ok ? d.y : 0.f;
@@ -1554,6 +1567,9 @@ __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int 
                 const int64_t el = b * BLK + (qh * 32 + i) * 4;
                 y[u][k] = B16 ? unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.y) + el))
                               : *reinterpret_cast<const float4*>(a.y + el);
+                // rows past the batch are not written by every producer (the fused small-batch
+                // kernels store only their towers' rows): 0·NaN must not reach the sums
+                if (!ok) y[u][k] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
 #pragma unroll
@@ -1759,11 +1775,12 @@ hipError_t launch_wgrad_ws(const WgWsArgs& a, int wgs, int kx_pad, int ny_pad, i
     return hipGetLastError();
 }
 hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st, const Pos3Batch* p3) {
-    if (b.n <= 0) return p3 ? launch_wgrad_pos3(*p3, st) : hipSuccess;
-    if (b.n > kMaxWsJobs || b.wgs <= 0) return hipErrorInvalidValue;
+    if (b.n <= 0 && b.w2_wgs <= 0) return p3 ? launch_wgrad_pos3(*p3, st) : hipSuccess;
+    if (b.n > kMaxWsJobs || b.wgs < 0 || (b.n > 0 && b.wgs == 0) || b.w2_wgs < 0) return hipErrorInvalidValue;
     Pos3Batch none{};
     const Pos3Batch& q = p3 ? *p3 : none;
-    const dim3 g(b.wgs + (q.ce + q.cn + 1) / 2);
+    if (b.w2_wgs && math != MATH_X6) return hipErrorInvalidValue;
+    const dim3 g(b.wgs + (q.ce + q.cn + 1) / 2 + b.w2_wgs);
     if (math == MATH_BF16) hipLaunchKernelGGL(k_wgrad_ws_batch<1>, g, dim3(kWsThreads), 0, st, b, q);
     else hipLaunchKernelGGL(k_wgrad_ws_batch<3>, g, dim3(kWsThreads), 0, st, b, q);
     return hipGetLastError();
