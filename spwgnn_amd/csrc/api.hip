@@ -494,10 +494,17 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         fa.m1_step = r->training ? w.m1_at(1) - w.m1_at(0) : 0;
         fa.m2_step = r->training ? w.m2_at(1) - w.m2_at(0) : 0;
         fa.logits = logits;
+        // the encoders side by side in their own launch (a workgroup per block / node block) beat
+        // running them one after the other inside each tile's workgroup
+        fa.encoders = getenv_flag("SPWGNN_FUSED_ENC");
         Prof p0{r, st};
         SPW_CHECK(p0.before(SPWGNN_K_ENC_EDGE));
-        SPW_CHECK(launch_fwd_fused_team(fa, r->math, ee.z1 || ee.ed, st));
+        if (!fa.encoders) SPW_CHECK(launch_enc_pair_team(ee, en, r->math, ee.z1 || ee.ed, st));
         SPW_CHECK(p0.after(SPWGNN_K_ENC_EDGE));
+        Prof p1{r, st};
+        SPW_CHECK(p1.before(SPWGNN_K_EDGE_FWD));
+        SPW_CHECK(launch_fwd_fused_team(fa, r->math, ee.z1 || ee.ed, st));
+        SPW_CHECK(p1.after(SPWGNN_K_EDGE_FWD));
         return SPWGNN_OK;
     }
     if (r->math == kmath(r, kX6EncEdge) && enc_pair_team(b->n_eblocks, b->n_nodes, r->math) &&
@@ -898,9 +905,15 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         fa.rowsE = w.RN * kRowE;
         fa.m1_step = w.m1_at(1) - w.m1_at(0);
         fa.m2_step = w.m2_at(1) - w.m2_at(0);
+        fa.encoders = getenv_flag("SPWGNN_FUSED_ENC");
         SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
         SPW_CHECK(launch_bwd_fused_team(fa, r->math, st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
+        if (!fa.encoders) {
+            SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
+            SPW_CHECK(launch_bwd_enc_pair_team(da, eeb, enb, r->math, st));
+            SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
+        }
     } else {
         for (int s = S - 1; s >= 0; --s) {
             const NodeBwdArgs nb = node_args(s);

@@ -384,6 +384,7 @@ struct FwdFusedArgs {
     EdgeFwdArgs ef;       // U, V, H2s, mask1, mask2 of step 0
     NodeFwdArgs nf;       // P, Pn, a_out, o1_out, U, V of step 0; cw_out (step 0) / cw_in (later)
     int S, training;
+    int encoders;             // 1: both encoders first, in this launch; 0: they ran before (k_enc_pair_team)
     int64_t rowsN, rowsE;     // floats per step of a 104- / 152-feature node array (RN·kRowN, RN·kRowE)
     int64_t m1_step, m2_step; // u32 words per step of mask1 / mask2
     float* logits;
@@ -400,10 +401,13 @@ struct BwdFusedArgs {
     EncEdgeBwdArgs eeb;
     EncNodeBwdArgs enb;
     int S, has_tail;
+    int encoders;   // 1: dA rebuild and both encoder backwards in this launch; 0: k_bwd_enc_pair_team after it
     int64_t rowsN, rowsE, m1_step, m2_step;
 };
 hipError_t launch_fwd_fused_team(const FwdFusedArgs& a, int math, bool train, hipStream_t st);
 hipError_t launch_bwd_fused_team(const BwdFusedArgs& a, int math, hipStream_t st);
+hipError_t launch_bwd_enc_pair_team(const DaArgs& da, const EncEdgeBwdArgs& eeb, const EncNodeBwdArgs& enb, int math,
+                                    hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
 // persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)

@@ -901,10 +901,12 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
     __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
     const int wt = blockIdx.x;
     const int4 info = reinterpret_cast<const int4*>(a.ef.wtile)[wt];
-    for (int b = 0; b < info.y; ++b) enc_edge_team_body<TRAIN, NP, AB16>(a.ee, info.x + b, act_s);
     const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
-    enc_node_team_body<NP>(a.en, R);
-    __syncthreads();   // A, U0, V0 of the tile
+    if (a.encoders) {   // else both encoders ran before, side by side (k_enc_pair_team)
+        for (int b = 0; b < info.y; ++b) enc_edge_team_body<TRAIN, NP, AB16>(a.ee, info.x + b, act_s);
+        enc_node_team_body<NP>(a.en, R);
+        __syncthreads();   // A, U0, V0 of the tile
+    }
     for (int s = 0; s < a.S; ++s) {
         const int64_t sE = (int64_t)(a.training ? s : 0) * a.rowsE;   // Ws::U_at / V_at / H2s_at
         EdgeFwdArgs ef = a.ef;
@@ -1245,6 +1247,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs 
         __syncthreads();   // dU, dV of step s
     }
     if (a.has_tail) node_bwd_team_body<NP, 5>(a.tail, R, act_s);   // dP0 (reads only)
+    if (!a.encoders) return;   // else k_bwd_enc_pair_team runs the rest, edge and node side by side
     for (int b = 0; b < info.y; ++b) dA_team_body<NP, B16>(a.da, info.x + b);
     __syncthreads();   // dA of the tile's blocks
     for (int b = 0; b < info.y; ++b) {
@@ -1252,6 +1255,21 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs 
         __syncthreads();   // its last exchange buffer is the next body's first
     }
     enc_node_bwd_team_body<NP, 5>(a.enb, R, act_s);
+}
+// After the fused step loop: workgroups [0, n_eblocks) rebuild dA of their block and run the
+// relation-encoder backward on it, the others the object-encoder backward of a 32-node block —
+// independent, so side by side (as the forward's k_enc_pair_team) instead of one after the other.
+template <int NP, bool B16>
+__global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_enc_pair_team(DaArgs da, EncEdgeBwdArgs eeb, EncNodeBwdArgs enb) {
+    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    const int blk = blockIdx.x;
+    if (blk < da.n_eblocks) {
+        dA_team_body<NP, B16>(da, blk);
+        __syncthreads();   // the block's dA rows, written feature tile by feature tile
+        enc_edge_bwd_team_body<NP, B16>(eeb, blk, act_s);
+    } else {
+        enc_node_bwd_team_body<NP, 5>(enb, TeamRows::block(blk - da.n_eblocks, enb.n_nodes, threadIdx.x & 63), act_s);
+    }
 }
 
 bool team_blocks(int n_blocks) {
@@ -1365,6 +1383,17 @@ hipError_t launch_bwd_fused_team(const BwdFusedArgs& a, int math, hipStream_t st
     if (math == MATH_BF16 && a.da.b16) hipLaunchKernelGGL((k_bwd_fused_team<1, true>), g, b, 0, st, a);
     else if (math == MATH_BF16) hipLaunchKernelGGL((k_bwd_fused_team<1, false>), g, b, 0, st, a);
     else if (math == MATH_X6 && !a.da.b16) hipLaunchKernelGGL((k_bwd_fused_team<3, false>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_bwd_enc_pair_team(const DaArgs& da, const EncEdgeBwdArgs& eeb, const EncNodeBwdArgs& enb, int math,
+                                    hipStream_t st) {
+    if (!team_blocks(da.n_eblocks) || !team_blocks((enb.n_nodes + 31) / 32) || da.b16 != eeb.b16 || !enb.wo1ct)
+        return hipErrorInvalidValue;
+    const dim3 g(da.n_eblocks + (enb.n_nodes + 31) / 32), b(64 * kTeamEdge);
+    if (math == MATH_BF16 && da.b16) hipLaunchKernelGGL((k_bwd_enc_pair_team<1, true>), g, b, 0, st, da, eeb, enb);
+    else if (math == MATH_BF16) hipLaunchKernelGGL((k_bwd_enc_pair_team<1, false>), g, b, 0, st, da, eeb, enb);
+    else if (math == MATH_X6 && !da.b16) hipLaunchKernelGGL((k_bwd_enc_pair_team<3, false>), g, b, 0, st, da, eeb, enb);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
