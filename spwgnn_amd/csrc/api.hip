@@ -290,16 +290,14 @@ struct Prof {
         if (e_ != hipSuccess) return (int32_t)e_;     \
     } while (0)
 
-// dA = Σ_s dh1pre_s. x6, wide edge backward: each step's k_edge_bwd_x6 adds its dh1pre into the
-// block's dA rows (a read-add-write; the wave owns the block), in the order S−1 .. 0 — the rebuild's
-// order, so bitwise the same dA — and no second W2ᵀ product runs. bf16 math (dA
-// stored as bf16 after the fp32 sum) and the team kernels rebuild it once after the step loop
-// (k_dA_x6 / k_dA_team). The first per-step form used float atomics, which bounded the kernel.
-// SPWGNN_DA_REBUILD (diagnosis builds only) keeps the rebuild for x6 as well, for A/B.
+// dA = Σ_s dh1pre_s: rebuilt once after the step loop (k_dA_x6 / k_dA_team) instead of being
+// accumulated into HBM by every step's edge backward — float atomics bounded that kernel (A/B on one
+// box: x6 step 28.11 → 27.39 ms, bf16 config 3 71.5 → 69.3 ms), and so do plain read-add-writes in
+// the rebuild's order (bitwise the same dA; headline 25.7 → 28.9 ms, round 4) — DESIGN.md §3f.
+// SPWGNN_DA_RMW (diagnosis builds only) selects the read-add-write form for A/B.
 static bool rebuild_dA(const spwgnn_run* r, const spwgnn_batch* b) {
     const int m = kmath(r, kX6EdgeBwd);
-    if (b->nw_max > 16 || m == MATH_F32) return false;
-    return m == MATH_BF16 || team_blocks(b->n_wtiles) || getenv_flag("SPWGNN_DA_REBUILD");
+    return b->nw_max <= 16 && m != MATH_F32 && !(m == MATH_X6 && !team_blocks(b->n_wtiles) && getenv_flag("SPWGNN_DA_RMW"));
 }
 
 // bf16 math (training) stores the encoder-side edge arrays that only ever feed MFMA operands — z2, z3,

@@ -670,10 +670,11 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 // One propagation step, edge side, backward, in split-bf16 math (x6; wave-tiles of ≤ 16 nodes).
 // As k_edge_fwd_x6: lane (i, h) holds edge i, features 76h + 8kb + e of k-block kb; the A operand
 // is dh2pre = G3[receiver] ⊙ [h2 > 0] built from the G3 loads, W2ᵀ (x6 image) is the LDS B operand.
-// dh1pre = dh1 ⊙ [h1 > 0] goes to dA (stores on the first backward step S−1, read-add-writes after:
-// the sum runs s = S−1 .. 0 as k_dA_x6's does, so dA is bitwise the rebuilt one)
-// and through one one-hot product (rows 0-15 receivers → dV, 16-31 senders → dU; 3 bf16 MFMAs per
-// 16 edges per feature tile). G3 rows run kX6Pf k-blocks ahead, carried across blocks.
+// dh1pre = dh1 ⊙ [h1 > 0] goes through one one-hot product (rows 0-15 receivers → dV, 16-31 senders
+// → dU; 3 bf16 MFMAs per 16 edges per feature tile); dA is rebuilt after the step loop (k_dA_x6).
+// Diagnosis builds keep a per-step dA form (stores on step S−1, read-add-writes after, in the
+// rebuild's order: bitwise the same dA) for A/B: it made this kernel 2.6x slower (§3f). G3 rows run
+// kX6Pf k-blocks ahead, carried across blocks.
 #ifndef SPWGNN_EBWD_PF
 #define SPWGNN_EBWD_PF 2
 #endif
@@ -880,11 +881,14 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
             else hipLaunchKernelGGL((k_edge_bwd_x6<false, true>), g, b, 0, st, a);
             return hipGetLastError();
         }
-        // x6: dA accumulated per step in fp32 (bf16 math keeps the rebuild: its dA is stored as bf16)
+#ifdef SPWGNN_DIAG   // per-step dA read-add-writes (SPWGNN_DA_RMW A/B builds only: 2.6x slower, §3f)
         if (math != MATH_X6) return hipErrorInvalidValue;
         if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd_x6<true>), g, b, 0, st, a);
         else hipLaunchKernelGGL((k_edge_bwd_x6<false>), g, b, 0, st, a);
         return hipGetLastError();
+#else
+        return hipErrorInvalidValue;
+#endif
     }
     if (a.nw_max <= 16) {
         if (a.dA_accumulate)

@@ -22,7 +22,7 @@ namespace spw {
 __device__ unsigned long long g_team_stamps[2][16];
 #define TEAM_STAMP(i)                                                                              \
     do {                                                                                           \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   /* 100 MHz */            \
         if (blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == 256)) g_team_stamps[threadIdx.x >> 8][i] = t_; \
     } while (0)
 #else
@@ -516,6 +516,7 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
     TeamFrags<10, NP> F;
     const uint4* const first7 = a.cw_in ? a.x_wo1a : a.x_wo1c;
     if (nw) F.load(a.x_w3a, 4, T, lane);
+    TEAM_STAMP(0);
     f32x16 O;
     if (nw) {
         // a = tanh([H2s | deg]·[W3; b3])   (Networks.py:88, layer 3 after the sum)
@@ -527,6 +528,7 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
                 if (kb < 7) F.load_kb(first7, 4, T, lane, kb);
             });
         }
+        TEAM_STAMP(1);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * T;
@@ -543,8 +545,10 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
             O = team_gemm<7>(F, hr, [&](int kb) { F.load_kb(a.x_wo1a, 4, T, lane, kb); });
             if (a.cw_out) R.store_all<kKhN>(a.cw_out, O, T);
         }
+        TEAM_STAMP(2);
     }
     team_sync();
+    TEAM_STAMP(3);
     if (nw) {
         O = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
                       [&](int kb) { F.load_kb(a.x_wo1p, 4, T, lane, kb); }, O);
@@ -558,8 +562,10 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
         }
         if (a.o1_out) R.store<kKhN>(a.o1_out, O, T);
         act.put(1, T, O, lane);
+        TEAM_STAMP(4);
     }
     team_sync();
+    TEAM_STAMP(5);
     if (nw) {
         // x' = o1·Wo2' + bo2'; P' = tanh(x'[0:100] + P); logit = x'[100]  (Networks.py:91, 94)
         float bv[16];
@@ -578,16 +584,20 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
         }
         R.store<kKhN>(a.Pn, X, T);
         act.put(0, T, X, lane);
+        TEAM_STAMP(6);
     } else if (a.U) {
         F.template load<7>(a.x_w1b, 5, T, lane);
     }
     team_sync();
+    TEAM_STAMP(7);
     if (a.U) {   // U' = P'·W1b, V' = P'·W1c for the next step
         f32x16 U = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
                              [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
         R.store<kKhE>(a.U, U, T);
+        TEAM_STAMP(8);
         U = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
         R.store<kKhE>(a.V, U, T);
+        TEAM_STAMP(9);
     }
 }
 
@@ -902,6 +912,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
     const int wt = blockIdx.x;
     const int4 info = reinterpret_cast<const int4*>(a.ef.wtile)[wt];
     const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
+    TEAM_STAMP(10);
     if (a.encoders) {   // else both encoders ran before, side by side (k_enc_pair_team)
         for (int b = 0; b < info.y; ++b) enc_edge_team_body<TRAIN, NP, AB16>(a.ee, info.x + b, act_s);
         enc_node_team_body<NP>(a.en, R);
@@ -918,7 +929,9 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
         ef.H2s += sE;
         if (ef.mask1) ef.mask1 += s * a.m1_step;
         if (ef.mask2) ef.mask2 += s * a.m2_step;
+        if (s == 0) TEAM_STAMP(11);
         edge_fwd_team_body<NP, AB16>(ef, wt);
+        if (s == 0) TEAM_STAMP(12);
         __syncthreads();   // H2s of step s
         NodeFwdArgs nf = a.nf;
         opaque(nf.x_w3a);
@@ -942,8 +955,11 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
         const int64_t sE1 = (int64_t)(a.training ? s + 1 : 0) * a.rowsE;
         nf.U = s + 1 < a.S ? const_cast<float*>(a.ef.U) + sE1 : nullptr;   // the same workspace arrays
         nf.V = s + 1 < a.S ? const_cast<float*>(a.ef.V) + sE1 : nullptr;
+        if (s == 0) TEAM_STAMP(13);
         node_fwd_team_body<NP>(nf, R.opaque(), act_s);
+        if (s == 0) TEAM_STAMP(14);
         __syncthreads();   // P', U', V' of step s + 1
+        if (s == 0) TEAM_STAMP(15);
     }
 }
 

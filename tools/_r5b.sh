@@ -6,3 +6,4 @@ for L in F0 F3 F6; do SPWGNN_LIB=$R/abl/lib$L.so timeout -k 10 300 python3 tools
 echo "== F0 vs F6"; python3 tools/cmp_npz.py gpurun_out/dump_F0.npz gpurun_out/dump_F6.npz
 echo "== F3 vs F6"; python3 tools/cmp_npz.py gpurun_out/dump_F3.npz gpurun_out/dump_F6.npz
 LIBS="F3 F4 F6 F3 F4 F6" CONFIGS=0 KERNELS="edge_bwd dA wgrad_ws edge_fwd" bash tools/ab.sh dacc
+SPWGNN_LIB=$R/abl/libD7.so timeout -k 10 120 python3 tools/fused_stamps.py
