@@ -86,6 +86,27 @@ KERNELS = {
     "enc_node_bwd": (_lib.K_ENC_NODE_BWD, lambda Ne, Nn, S: 2.0 * 2 * 100 * 100 * Nn),
 }
 INFER_KERNELS = ("edge_fwd", "node_fwd", "enc_edge", "enc_node")
+# Small batches (≤ kTeamMaxBlocks wave-tiles and blocks, ≤ 16-node tiles, split-bf16 math) run the
+# fused launches, each timed under one id: its FLOPs are those of the phases it holds,
+# its PMC summary rows those of the fused kernel
+FUSED_PARTS = {"edge_fwd": ("edge_fwd", "node_fwd"), "node_bwd": ("node_bwd", "edge_bwd"),
+               "enc_edge_bwd": ("dA", "enc_edge_bwd", "enc_node_bwd"), "enc_edge": ("enc_edge", "enc_node"),
+               "wgrad_ws": ("wgrad_ws", "wgrad_w2")}
+FUSED_PMC = {"edge_fwd": "k_fwd_fused", "node_bwd": "k_bwd_fused", "enc_edge_bwd": "k_bwd_enc_pair",
+             "enc_edge": "k_enc_pair", "wgrad_ws": "k_wgrad_ws"}
+_FUSED = [False]
+
+
+def fused_small(batches, math) -> bool:
+    """Whether these batches take the fused small-batch launches (api.hip fwd_fused_team)."""
+    lim = 512
+    return math != "f32" and all(b.n_wtiles <= lim and b.n_eblocks <= lim and (b.n_nodes + 31) // 32 <= lim
+                                 and b.nw_max <= 16 and not (getattr(b, "flags", 0) & 1) for b in batches)
+
+
+def kernel_flops(kernel, Ne, Nn, S):
+    parts = FUSED_PARTS.get(kernel, (kernel,)) if _FUSED[0] else (kernel,)
+    return sum(KERNELS[k][1](Ne, Nn, S) for k in parts)
 MAX_LAUNCHES = 32      # event pairs reserved per kernel per micro-batch and step (the family has 12)
 # device kernel name prefix in the rocprofv3 PMC summaries (tools/pmcsum.py)
 PMC_PREFIX = {"edge_fwd": "k_edge_fwd", "edge_bwd": "k_edge_bwd", "node_fwd": "k_node_fwd",
@@ -288,10 +309,11 @@ def load_pmc(config: int, kernel: str, math: str, workload: str):
         if meta and (meta.get("workload") != workload or meta.get("math") != math):
             return None
         tot = cnt = 0.0
+        prefix = FUSED_PMC.get(kernel, PMC_PREFIX[kernel]) if _FUSED[0] else PMC_PREFIX[kernel]
         for name, v in d.items():
             if kernel in ("enc_edge", "enc_node") and name.startswith(PMC_PREFIX[kernel] + "_bwd"):
                 continue
-            if name.startswith(PMC_PREFIX[kernel]) and "hbm_read_bytes" in v and "hbm_write_bytes" in v:
+            if name.startswith(prefix) and "hbm_read_bytes" in v and "hbm_write_bytes" in v:
                 tot += (v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["dispatches"]
                 cnt += v["dispatches"]
         return tot / cnt if cnt else None
@@ -335,7 +357,7 @@ def roofline(kernel: str, kern_ms, launches_per_step, Ne, Nn, S, math, config, w
     `traffic` = measured HBM bytes per launch from the committed PMC summary of the same workload
     (null if none)."""
     avg_ms = float(np.mean(kern_ms))
-    fl_step = KERNELS[kernel][1](Ne, Nn, S)
+    fl_step = kernel_flops(kernel, Ne, Nn, S)
     kflops = fl_step / launches_per_step
     achieved = kflops / (avg_ms * 1e-3) / 1e12
     mpeak = MATH_PEAK[math]
@@ -454,6 +476,7 @@ def run_train(args, cfg, world, rank, device):
     Nn = sum(b.n_nodes for b in batches)
     B = sum(b.n_towers for b in batches)
     wl = workload_name(cfg, world, args.dropout)
+    _FUSED[0] = fused_small(batches, math)
 
     # every timed kernel's per-step time, before the timed region (untimed steps), so the roofline
     # can name the DOMINANT kernel (largest ms per step) and time it inside the timed region
@@ -640,6 +663,8 @@ def kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, config, wl, steps=2
         table[name] = {"launches_per_step": per_step, "avg_launch_ms": r["avg_launch_ms"],
                        "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
                        "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
+        if _FUSED[0] and name in FUSED_PARTS:
+            table[name]["fused"] = "+".join(FUSED_PARTS[name])
         if name in FAMILIES:
             table[name]["batched"] = bool(per_step <= n_micro)
             table[name]["family"] = ("one launch per backward batching every weight-gradient shape (k_wgrad_ws_batch)"
