@@ -704,17 +704,89 @@ __global__ __launch_bounds__(256, 1) void k_node_bwd_team(NodeBwdArgs a) {
     node_bwd_team_body<NP, 4>(a, TeamRows::block(blockIdx.x, a.n_nodes, threadIdx.x & 63), act_s);
 }
 
+// ---- shared A operands of the team edge kernels: wave T builds k-blocks 2T, 2T+1 (chunks 4T .. 4T+3)
+// of the block's 32 × 152 operand, splits them and puts the parts in LDS ([kb][part][lane] uint4);
+// after a barrier every wave runs its output tile's ten k-blocks on it (team_lds_gemm). One memory
+// latency per block instead of one per k-block, and each operand element loaded once, not 5×.
+// dh2pre = G3[receiver] ⊙ [h2 > 0] (the edge backward and the dA rebuild), as k_edge_bwd_x6 builds it.
+template <int NP>
+__device__ __forceinline__ void team_dh2_kblocks(const float* __restrict__ G3, const uint32_t* __restrict__ m2row,
+                                                 int d, int n0, int T, int lane, uint4* buf) {
+    const int h = lane >> 5, i = lane & 31;
+    const bool valid = d >= 0;
+    uint32_t w[5];
+    load_m2(m2row, i, w);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) w[t] = valid ? w[t] : 0u;
+    // this lane's 76 feature bits (features 76h + 0..75): a 64-bit low part and a 12-bit tail
+    const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
+                                : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
+    const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
+    const float4* G4 = reinterpret_cast<const float4*>(G3 + cm_index<kKhE>(valid ? d : n0, 0) + h * 128);
+    float4 g[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) g[c] = G4[64 * min(4 * T + c, kKhE / 4 - 1)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int kb = 2 * T + k;
+        float xv[8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int q = 2 * kb + c;
+            const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
+            const float4 gv = g[2 * k + c];
+            xv[4 * c + 0] = mask_bit(gv.x, bits, 0);
+            xv[4 * c + 1] = mask_bit(gv.y, bits, 1);
+            xv[4 * c + 2] = mask_bit(gv.z, bits, 2);
+            xv[4 * c + 3] = mask_bit(gv.w, bits, 3);
+        }
+        uint32_t sp[3][4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], sp[0][m], sp[1][m], sp[2][m]);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) buf[(kb * 3 + p) * 64 + lane] = make_uint4(sp[p][0], sp[p][1], sp[p][2], sp[p][3]);
+    }
+}
+// acc = Σ_kb A(kb) · W(kb, T) over the ten k-blocks in LDS, in mfma32_x6's product order
+template <int NP>
+__device__ __forceinline__ f32x16 team_lds_gemm(const uint4* buf, const uint4 (&wf)[10][NP], int lane) {
+    f32x16 acc = zero16();
+    uint4 cur[3], nxt[3];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) cur[p] = buf[p * 64 + lane];
+#pragma unroll
+    for (int kb = 0; kb < 10; ++kb) {
+        if (kb + 1 < 10) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p) nxt[p] = buf[((kb + 1) * 3 + p) * 64 + lane];
+        }
+        bf16x8 ap[3], bp[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            ap[p] = as_bf16x8(p < NP ? cur[p] : make_uint4(0u, 0u, 0u, 0u));
+            bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc = mfma32_x6<NP>(ap, bp, acc);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) cur[p] = nxt[p];
+    }
+    return acc;
+}
+
 // ---- edge side of one propagation step (k_edge_fwd_x6 for ≤ 16-node wave-tiles), team form ----
 // A workgroup of five waves takes one wave-tile; wave T owns output feature tile T of h2 (and its
-// receiver sums): per 32-edge block it builds and splits the whole h1 = relu(A + U[s] + V[r]) k-block
-// by k-block (the A operand, as k_edge_fwd_x6 does) and runs tile T's products with W2 fragments read
-// straight from the x6 image (L2; no 150 KB LDS fill). Products, their per-accumulator order, the
-// epilogue and the one-hot receiver sum of tile T are k_edge_fwd_x6's (mfma32_x6 / NodeSum16X6), so
-// H2s and both masks are bit-identical. Wave 0 writes the h1 > 0 words, wave T the h2 > 0 word of
-// tile T (wave 0 also the zero padding words 5-7).
+// receiver sums). Per 32-edge block, wave T builds k-blocks 2T and 2T+1 of h1 = relu(A + U[s] + V[r])
+// (its loads all issued at once: one memory latency per block, not ten — the small-batch step is
+// latency-bound), splits them and puts the three bf16 parts in LDS (and their h1 > 0 words); after one
+// barrier every wave runs its tile's ten k-blocks on the shared operand with W2 fragments read straight
+// from the x6 image (L2; no 150 KB LDS fill). Products, their per-accumulator order, the epilogue and
+// the one-hot receiver sum of tile T are k_edge_fwd_x6's (mfma32_x6 / NodeSum16X6), so H2s and both
+// masks are bit-identical. Wave T writes the h2 > 0 word of tile T (wave 0 also the padding words).
+// hs: two buffers of 10 k-blocks × 3 parts × 64 lanes (uint4), 60 KiB, blocks alternate.
 template <int NP, bool AB16>
-__device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt) {
-    constexpr int PF = 2;   // A/U/V k-blocks in flight
+__device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt, uint4* hs) {
     const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
@@ -728,83 +800,77 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt)
     f32x4 nacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};   // NodeSum16X6 sub-tiles 2T, 2T+1
     const int key = n0 + (lane & 15);
     const int m1off = lane < 4 ? lane : kKhE + lane - 4;
-    struct KB { float4 a[2], u[2], v[2]; };
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
+        uint4* const buf = hs + (bb & 1) * (10 * 3 * 64);
         const int s = a.esrc[(int64_t)blk * 32 + i], d = a.edst[(int64_t)blk * 32 + i];
         const bool valid = s >= 0;
         const uint64_t vmask = __ballot(valid);
         const float vf = valid ? 1.f : 0.f;
-        const int sc = valid ? s : n0, dc = valid ? d : n0;
-        const int64_t ai = (int64_t)blk * kCmBlk + h * 128 + i * 4;
-        const float4* U4 = reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128);
-        const float4* V4 = reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128);
-        auto ld = [&](int kb, KB& r) {
+        {   // k-blocks 2T, 2T+1: chunks q = 4T .. 4T+3 (q < 19)
+            const int sc = valid ? s : n0, dc = valid ? d : n0;
+            const int64_t ai = (int64_t)blk * kCmBlk + h * 128 + i * 4;
+            const float4* U4 = reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128);
+            const float4* V4 = reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128);
+            float4 ra[4], ru[4], rv[4];
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int q = min(2 * kb + c, kKhE / 4 - 1);
+            for (int c = 0; c < 4; ++c) {
+                const int q = min(4 * T + c, kKhE / 4 - 1);
                 if constexpr (AB16)
-                    r.a[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + ai + 256 * q));
+                    ra[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + ai + 256 * q));
                 else
-                    r.a[c] = *reinterpret_cast<const float4*>(a.A + ai + 256 * q);
-                r.u[c] = U4[64 * q];
-                r.v[c] = V4[64 * q];
+                    ra[c] = *reinterpret_cast<const float4*>(a.A + ai + 256 * q);
+                ru[c] = U4[64 * q];
+                rv[c] = V4[64 * q];
             }
-        };
-        uint32_t* mrow = (a.mask1 && T == 0) ? a.mask1 + (int64_t)blk * kLdE : nullptr;
-        KB ring[PF];
+            uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
 #pragma unroll
-        for (int k = 0; k < PF; ++k) ld(k, ring[k]);
-        f32x16 acc = zero16();
-#pragma unroll
-        for (int kb = 0; kb < 10; ++kb) {
-            KB& cr = ring[kb % PF];
-            float xv[8];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
-                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
-                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
-                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
-            }
-            if (kb + PF < 10) ld(kb + PF, cr);
-            uint32_t hw[4], mw[4], lw[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
-            if (mrow) {   // h1 > 0 bits of the block's real chunks (as k_edge_fwd_x6)
-                uint64_t bal[2][4];
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-#pragma unroll
-                    for (int f = 0; f < 4; ++f) bal[c][f] = __ballot(xv[4 * c + f] > 0.f);
-                __builtin_amdgcn_sched_barrier(0);
+            for (int k = 0; k < 2; ++k) {
+                const int kb = 2 * T + k;
+                float xv[8];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const int q = 2 * kb + c;
-                    if (q < kKhE / 4) {
-                        uint32_t v[8];
-                        int ln[8];
+                    const float4 av = ra[2 * k + c], uv = ru[2 * k + c], vv = rv[2 * k + c];
+                    xv[4 * c + 0] = relu(av.x + uv.x + vv.x) * vf;
+                    xv[4 * c + 1] = relu(av.y + uv.y + vv.y) * vf;
+                    xv[4 * c + 2] = relu(av.z + uv.z + vv.z) * vf;
+                    xv[4 * c + 3] = relu(av.w + uv.w + vv.w) * vf;
+                }
+                uint32_t sp[3][4];
 #pragma unroll
-                        for (int f = 0; f < 4; ++f) {
-                            v[2 * f] = (uint32_t)bal[c][f];
-                            ln[2 * f] = f;
-                            v[2 * f + 1] = (uint32_t)(bal[c][f] >> 32);
-                            ln[2 * f + 1] = 4 + f;
+                for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], sp[0][m], sp[1][m], sp[2][m]);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) buf[(kb * 3 + p) * 64 + lane] = make_uint4(sp[p][0], sp[p][1], sp[p][2], sp[p][3]);
+                if (mrow) {   // h1 > 0 bits of the block's real chunks (as k_edge_fwd_x6)
+                    uint64_t bal[2][4];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) bal[c][f] = __ballot(xv[4 * c + f] > 0.f);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int q = 2 * kb + c;
+                        if (q < kKhE / 4) {
+                            uint32_t v[8];
+                            int ln[8];
+#pragma unroll
+                            for (int f = 0; f < 4; ++f) {
+                                v[2 * f] = (uint32_t)bal[c][f];
+                                ln[2 * f] = f;
+                                v[2 * f + 1] = (uint32_t)(bal[c][f] >> 32);
+                                ln[2 * f + 1] = 4 + f;
+                            }
+                            const uint32_t stg = writelane8_batched(0u, v, ln);
+                            if (lane < 8) mrow[m1off + 4 * q] = stg;
                         }
-                        const uint32_t stg = writelane8_batched(0u, v, ln);
-                        if (lane < 8) mrow[m1off + 4 * q] = stg;
                     }
                 }
             }
-            bf16x8 ap[3], bp[3];
-            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
-            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
-            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
-            acc = mfma32_x6<NP>(ap, bp, acc);
+            if (mrow && T == 0 && lane < 8) mrow[2 * kKhE + lane] = 0u;   // features 152..159 (padding)
         }
-        if (mrow && lane < 8) mrow[2 * kKhE + lane] = 0u;   // features 152..159 (padding)
+        team_sync();   // the block's split h1 (the other buffer is free: every wave passed this barrier)
+        f32x16 acc = team_lds_gemm<NP>(buf, wf, lane);
         const uint32_t vh = (uint32_t)vmask >> (4 * h);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -888,9 +954,14 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt)
     }
 }
 
+constexpr int kTeamHsU4 = 2 * 10 * 3 * 64;   // edge bodies' split-operand buffers (uint4), 60 KiB
+// LDS of a launch that runs edge bodies and five-tile exchanges (TeamAct<5>) one after the other
+template <int NP>
+constexpr int kTeamLdsU4 = kTeamHsU4 > 2 * kTeamEdge * 2 * NP * 64 ? kTeamHsU4 : 2 * kTeamEdge * 2 * NP * 64;
 template <int NP, bool AB16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a) {
-    if ((int)blockIdx.x < a.n_wtiles) edge_fwd_team_body<NP, AB16>(a, blockIdx.x);
+    __shared__ uint4 hs[kTeamHsU4];
+    if ((int)blockIdx.x < a.n_wtiles) edge_fwd_team_body<NP, AB16>(a, blockIdx.x, hs);
 }
 
 // ---- a small batch's forward in one launch (FwdFusedArgs, kernels.h) ----
@@ -908,7 +979,7 @@ __device__ __forceinline__ void opaque(T*& p) {
 }
 template <bool TRAIN, int NP, bool AB16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs a) {
-    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    __shared__ uint4 act_s[kTeamLdsU4<NP>];
     const int wt = blockIdx.x;
     const int4 info = reinterpret_cast<const int4*>(a.ef.wtile)[wt];
     const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
@@ -930,7 +1001,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
         if (ef.mask1) ef.mask1 += s * a.m1_step;
         if (ef.mask2) ef.mask2 += s * a.m2_step;
         if (s == 0) TEAM_STAMP(11);
-        edge_fwd_team_body<NP, AB16>(ef, wt);
+        edge_fwd_team_body<NP, AB16>(ef, wt, act_s);
         if (s == 0) TEAM_STAMP(12);
         __syncthreads();   // H2s of step s
         NodeFwdArgs nf = a.nf;
@@ -969,8 +1040,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
 // fragments (from the x6 image in L2), masks with [h1 > 0] and runs tile T's one-hot receiver/sender
 // sums — k_edge_bwd_x6's products in its per-accumulator order, so dU and dV are bit-identical.
 template <int NP>
-__device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt) {
-    constexpr int PF = 2;
+__device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt, uint4* hs) {
     const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
@@ -982,54 +1052,15 @@ __device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt)
         for (int p = 0; p < NP; ++p) wf[kb][p] = a.x_w2t[((kb * 5 + T) * 3 + p) * 64 + lane];
     const int key = i < 16 ? n0 + i : n0 + i - 16;   // one-hot rows: receivers, then senders
     f32x16 nacc = zero16();
-    struct KB { float4 g[2]; };
     for (int bb = 0; bb < nb; ++bb) {
         const int blk = fb + bb;
+        uint4* const buf = hs + (bb & 1) * (10 * 3 * 64);
         const int64_t e = (int64_t)blk * 32 + i;
         const int d = a.edst[e], s_ = a.esrc[e];
-        const bool valid = d >= 0;
-        uint32_t w[5];
-        load_m2(a.mask2 + (int64_t)blk * kM2Blk, i, w);
-#pragma unroll
-        for (int t = 0; t < 5; ++t) w[t] = valid ? w[t] : 0u;
         const uint32_t m1w = a.mask1[(int64_t)blk * kLdE + i + 32 * T];
-        const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
-                                    : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
-        const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
-        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + cm_index<kKhE>(valid ? d : n0, 0) + h * 128);
-        auto ld = [&](int kb, KB& r) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
-        };
-        KB ring[PF];
-#pragma unroll
-        for (int k = 0; k < PF; ++k) ld(k, ring[k]);
-        f32x16 acc = zero16();
-#pragma unroll
-        for (int kb = 0; kb < 10; ++kb) {
-            KB& cr = ring[kb % PF];
-            float xv[8];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int q = 2 * kb + c;
-                const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
-                xv[4 * c + 0] = mask_bit(cr.g[c].x, bits, 0);
-                xv[4 * c + 1] = mask_bit(cr.g[c].y, bits, 1);
-                xv[4 * c + 2] = mask_bit(cr.g[c].z, bits, 2);
-                xv[4 * c + 3] = mask_bit(cr.g[c].w, bits, 3);
-            }
-            if (kb + PF < 10) ld(kb + PF, cr);
-            uint32_t hw[4], mw[4], lw[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
-            bf16x8 ap[3], bp[3];
-            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
-            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
-            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
-            acc = mfma32_x6<NP>(ap, bp, acc);
-        }
+        team_dh2_kblocks<NP>(a.G3, a.mask2 + (int64_t)blk * kM2Blk, d, n0, T, lane, buf);
+        team_sync();   // the block's split dh2pre (the other buffer is free)
+        f32x16 acc = team_lds_gemm<NP>(buf, wf, lane);
         // dh1pre = dh1 ⊙ [h1 > 0]  (C layout: lane = feature 32T+i, rows = edges rho(r,h))
         const uint32_t mh = m1w >> (4 * h);
 #pragma unroll
@@ -1076,14 +1107,14 @@ __device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt)
 }
 template <int NP>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_edge_bwd_team(EdgeBwdArgs a) {
-    if ((int)blockIdx.x < a.n_wtiles) edge_bwd_team_body<NP>(a, blockIdx.x);
+    __shared__ uint4 hs[kTeamHsU4];
+    if ((int)blockIdx.x < a.n_wtiles) edge_bwd_team_body<NP>(a, blockIdx.x, hs);
 }
 
 // ---- dA = Σ_s dh1pre_s (k_dA_x6), team form: five waves per 32-edge block, wave T owns feature
 // tile T; the same products, per-accumulator order and step order (S−1 first) as k_dA_x6.
 template <int NP, bool B16>
-__device__ __forceinline__ void dA_team_body(const DaArgs& a, int blk) {
-    constexpr int PF = 2;
+__device__ __forceinline__ void dA_team_body(const DaArgs& a, int blk, uint4* hs) {
     const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     uint4 wf[10][NP];   // tile T's W2ᵀ fragments
@@ -1092,52 +1123,13 @@ __device__ __forceinline__ void dA_team_body(const DaArgs& a, int blk) {
 #pragma unroll
         for (int p = 0; p < NP; ++p) wf[kb][p] = a.x_w2t[((kb * 5 + T) * 3 + p) * 64 + lane];
     const int d = a.edst[(int64_t)blk * 32 + i];
-    const bool valid = d >= 0;
     f32x16 dacc = zero16();
-    struct KB { float4 g[2]; };
     for (int s = a.S - 1; s >= 0; --s) {
-        uint32_t w[5];
-        load_m2(a.mask2 + s * a.m2_step + (int64_t)blk * kM2Blk, i, w);
-#pragma unroll
-        for (int t = 0; t < 5; ++t) w[t] = valid ? w[t] : 0u;
+        uint4* const buf = hs + (s & 1) * (10 * 3 * 64);
         const uint32_t m1w = a.mask1[s * a.m1_step + (int64_t)blk * kLdE + i + 32 * T];
-        const uint64_t mlo = h == 0 ? ((uint64_t)w[1] << 32 | w[0])
-                                    : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
-        const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
-        const float4* G4 = reinterpret_cast<const float4*>(a.G3 + s * a.g3_step + cm_index<kKhE>(valid ? d : 0, 0) + h * 128);
-        auto ld = [&](int kb, KB& r) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) r.g[c] = G4[64 * min(2 * kb + c, kKhE / 4 - 1)];
-        };
-        KB ring[PF];
-#pragma unroll
-        for (int k = 0; k < PF; ++k) ld(k, ring[k]);
-        f32x16 acc = zero16();
-#pragma unroll
-        for (int kb = 0; kb < 10; ++kb) {
-            KB& cr = ring[kb % PF];
-            float xv[8];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int q = 2 * kb + c;
-                const uint32_t bits = q < 16 ? (uint32_t)(mlo >> (4 * q)) : (q < 19 ? mhi >> (4 * q - 64) : 0u);
-                xv[4 * c + 0] = mask_bit(cr.g[c].x, bits, 0);
-                xv[4 * c + 1] = mask_bit(cr.g[c].y, bits, 1);
-                xv[4 * c + 2] = mask_bit(cr.g[c].z, bits, 2);
-                xv[4 * c + 3] = mask_bit(cr.g[c].w, bits, 3);
-            }
-            if (kb + PF < 10) ld(kb + PF, cr);
-            uint32_t hw[4], mw[4], lw[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
-            bf16x8 ap[3], bp[3];
-            ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
-            ap[1] = as_bf16x8(make_uint4(mw[0], mw[1], mw[2], mw[3]));
-            ap[2] = as_bf16x8(make_uint4(lw[0], lw[1], lw[2], lw[3]));
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bp[p] = as_bf16x8(p < NP ? wf[kb][p] : make_uint4(0u, 0u, 0u, 0u));
-            acc = mfma32_x6<NP>(ap, bp, acc);
-        }
+        team_dh2_kblocks<NP>(a.G3 + s * a.g3_step, a.mask2 + s * a.m2_step + (int64_t)blk * kM2Blk, d, 0, T, lane, buf);
+        team_sync();   // step s's split dh2pre (the other buffer is free)
+        const f32x16 acc = team_lds_gemm<NP>(buf, wf, lane);
         const uint32_t mh = m1w >> (4 * h);
 #pragma unroll
         for (int r = 0; r < 16; ++r) dacc[r] += mask_bit(acc[r], mh, rho(r, 0));
@@ -1154,7 +1146,8 @@ __device__ __forceinline__ void dA_team_body(const DaArgs& a, int blk) {
 }
 template <int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_dA_team(DaArgs a) {
-    if ((int)blockIdx.x < a.n_eblocks) dA_team_body<NP, B16>(a, blockIdx.x);
+    __shared__ uint4 hs[kTeamHsU4];
+    if ((int)blockIdx.x < a.n_eblocks) dA_team_body<NP, B16>(a, blockIdx.x, hs);
 }
 
 // ---- object-encoder backward (k_enc_node_bwd_x6), team form: four waves per 32-node block, wave T
@@ -1223,7 +1216,7 @@ __global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
 // and products are the team kernels' (bit-identical results); phases meet at workgroup barriers.
 template <int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs a) {
-    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    __shared__ uint4 act_s[kTeamLdsU4<NP>];
     const int wt = blockIdx.x;
     const int4 info = reinterpret_cast<const int4*>(a.eb.wtile)[wt];
     const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
@@ -1259,13 +1252,15 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs 
         eb.G3 = nb.G3;
         eb.dU += sE;
         eb.dV += sE;
-        edge_bwd_team_body<NP>(eb, wt);
+        edge_bwd_team_body<NP>(eb, wt, act_s);
         __syncthreads();   // dU, dV of step s
     }
     if (a.has_tail) node_bwd_team_body<NP, 5>(a.tail, R, act_s);   // dP0 (reads only)
     if (!a.encoders) return;   // else k_bwd_enc_pair_team runs the rest, edge and node side by side
-    for (int b = 0; b < info.y; ++b) dA_team_body<NP, B16>(a.da, info.x + b);
-    __syncthreads();   // dA of the tile's blocks
+    for (int b = 0; b < info.y; ++b) {
+        dA_team_body<NP, B16>(a.da, info.x + b, act_s);
+        __syncthreads();   // the block's dA rows; its last operand buffer may be the next block's first
+    }
     for (int b = 0; b < info.y; ++b) {
         enc_edge_bwd_team_body<NP, B16>(a.eeb, info.x + b, act_s);
         __syncthreads();   // its last exchange buffer is the next body's first
@@ -1277,10 +1272,10 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs 
 // independent, so side by side (as the forward's k_enc_pair_team) instead of one after the other.
 template <int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_enc_pair_team(DaArgs da, EncEdgeBwdArgs eeb, EncNodeBwdArgs enb) {
-    __shared__ uint4 act_s[2 * kTeamEdge * 2 * NP * 64];
+    __shared__ uint4 act_s[kTeamLdsU4<NP>];
     const int blk = blockIdx.x;
     if (blk < da.n_eblocks) {
-        dA_team_body<NP, B16>(da, blk);
+        dA_team_body<NP, B16>(da, blk, act_s);
         __syncthreads();   // the block's dA rows, written feature tile by feature tile
         enc_edge_bwd_team_body<NP, B16>(eeb, blk, act_s);
     } else {
