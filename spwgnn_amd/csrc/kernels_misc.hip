@@ -1785,9 +1785,44 @@ hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st, con
     else hipLaunchKernelGGL(k_wgrad_ws_batch<3>, g, dim3(kWsThreads), 0, st, b, q);
     return hipGetLastError();
 }
+// Small batches (every gradient ≤ kReduceSmallChunks slabs): one thread per element sums its slabs in
+// order — 100 workgroups per gradient instead of 800: at the reference's batch 32 the launch's
+// workgroup dispatch, not its sums, was most of its 11 µs. Deterministic (a fixed order per element).
+constexpr int kReduceSmallChunks = 64;
+__global__ __launch_bounds__(256) void k_wgrad_reduce_small(ReduceBatch rb) {
+    if ((int)blockIdx.y == rb.n) {   // the ranges no reduction writes: zeros
+        for (int z = 0; z < rb.nzero; ++z)
+            for (int e = blockIdx.x * 256 + threadIdx.x; e < rb.zlen[z]; e += gridDim.x * 256) rb.r[0].out[rb.zoff[z] + e] = 0.f;
+        return;
+    }
+    const ReduceArgs& a = rb.r[blockIdx.y];
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    const int k = idx / a.ny_pad, n = idx - k * a.ny_pad;
+    const int col = a.perm ? wo2_perm(n) : n;
+    const bool kern = a.kernel_off >= 0 && k < a.kernel_rows, bias = a.bias_off >= 0 && k == a.bias_row;
+    if (!(idx < a.kx_pad * a.ny_pad && col >= 0 && col < a.kernel_cols && (kern || bias))) return;
+    const int64_t stride = (int64_t)a.kx_pad * a.ny_pad;
+    const float* p = a.slab + idx;
+    float s0 = 0.f, s1 = 0.f;
+    int c = 0;
+    for (; c + 1 < a.chunks; c += 2) {
+        s0 += p[c * stride];
+        s1 += p[(c + 1) * stride];
+    }
+    if (c < a.chunks) s0 += p[c * stride];
+    const float s = s0 + s1;
+    if (kern) a.out[a.kernel_off + (int64_t)(a.kernel_row0 + k) * a.kernel_cols + col] = s;
+    if (bias) a.out[a.bias_off + col] = s;
+}
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {
     if (rb.n <= 0) return rb.nzero > 0 ? hipErrorInvalidValue : hipSuccess;   // the zero row writes through r[0].out
-    hipLaunchKernelGGL(k_wgrad_reduce_all, dim3((160 * 160 + 31) / 32, rb.n + (rb.nzero > 0 ? 1 : 0)), dim3(256), 0, st, rb);
+    int maxc = 0;
+    for (int k = 0; k < rb.n; ++k) maxc = rb.r[k].chunks > maxc ? rb.r[k].chunks : maxc;
+    const int rows = rb.n + (rb.nzero > 0 ? 1 : 0);
+    if (maxc <= kReduceSmallChunks)
+        hipLaunchKernelGGL(k_wgrad_reduce_small, dim3((160 * 160 + 255) / 256, rows), dim3(256), 0, st, rb);
+    else
+        hipLaunchKernelGGL(k_wgrad_reduce_all, dim3((160 * 160 + 31) / 32, rows), dim3(256), 0, st, rb);
     return hipGetLastError();
 }
 hipError_t launch_bce(const BceArgs& a, hipStream_t st) {
