@@ -1320,8 +1320,11 @@ int edge_grid(int n_wtiles, int waves) {
     return need < 1 ? 1 : (need < cus ? need : cus);
 }
 
+#ifndef SPWGNN_PREP_GX   // workgroups per pack / image row (A/B at config 1: 8 / 16 / 32 → 0.1450 / 0.1417 / 0.1433 ms)
+#define SPWGNN_PREP_GX 16
+#endif
 hipError_t launch_prep(const PrepArgs& a, const PrepX6Args* x, hipStream_t st) {
-    hipLaunchKernelGGL(k_prep, dim3(32, PK_COUNT + (x ? X6_COUNT : 0)), dim3(256), 0, st, a, x ? *x : PrepX6Args{});
+    hipLaunchKernelGGL(k_prep, dim3(SPWGNN_PREP_GX, PK_COUNT + (x ? X6_COUNT : 0)), dim3(256), 0, st, a, x ? *x : PrepX6Args{});
     return hipGetLastError();
 }
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
