@@ -904,12 +904,13 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         fa.m1_step = w.m1_at(1) - w.m1_at(0);
         fa.m2_step = w.m2_at(1) - w.m2_at(0);
         fa.encoders = getenv_flag("SPWGNN_FUSED_ENC");
+        fa.dA_in_loop = !getenv_flag("SPWGNN_DA_PAIR");
         SPW_CHECK(prof.before(SPWGNN_K_NODE_BWD));
         SPW_CHECK(launch_bwd_fused_team(fa, r->math, st));
         SPW_CHECK(prof.after(SPWGNN_K_NODE_BWD));
         if (!fa.encoders) {
             SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
-            SPW_CHECK(launch_bwd_enc_pair_team(da, eeb, enb, r->math, st));
+            SPW_CHECK(launch_bwd_enc_pair_team(da, eeb, enb, r->math, !fa.dA_in_loop, st));
             SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
         }
     } else {

@@ -402,12 +402,13 @@ struct BwdFusedArgs {
     EncNodeBwdArgs enb;
     int S, has_tail;
     int encoders;   // 1: dA rebuild and both encoder backwards in this launch; 0: k_bwd_enc_pair_team after it
+    int dA_in_loop; // 1: this launch leaves dA (Σ_s dh1pre_s summed in LDS through the step loop)
     int64_t rowsN, rowsE, m1_step, m2_step;
 };
 hipError_t launch_fwd_fused_team(const FwdFusedArgs& a, int math, bool train, hipStream_t st);
 hipError_t launch_bwd_fused_team(const BwdFusedArgs& a, int math, hipStream_t st);
 hipError_t launch_bwd_enc_pair_team(const DaArgs& da, const EncEdgeBwdArgs& eeb, const EncNodeBwdArgs& enb, int math,
-                                    hipStream_t st);
+                                    int with_dA, hipStream_t st);
 
 // LDS bytes per wave of the edge kernels (stage [2][32][33] + node accumulators)
 // persistent edge-kernel grid: one 8-wave workgroup per CU (at most one wave-tile per wave)

@@ -1039,8 +1039,13 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
 // whole dh2pre = G3[receiver] ⊙ [h2 > 0] operand k-block by k-block, multiplies it by its tile's W2ᵀ
 // fragments (from the x6 image in L2), masks with [h1 > 0] and runs tile T's one-hot receiver/sender
 // sums — k_edge_bwd_x6's products in its per-accumulator order, so dU and dV are bit-identical.
+// dacc (fused backward, tiles of ≤ kTeamDaBlocks blocks): dA = Σ_s dh1pre_s accumulated in LDS per
+// (block, tile T, register, lane) across the steps, s = S−1 first (dacc_first) — the rebuild's order
+// and products, so the same bits as k_dA_team's
+constexpr int kTeamDaBlocks = 4;
 template <int NP>
-__device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt, uint4* hs) {
+__device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt, uint4* hs, float* dacc = nullptr,
+                                                   bool dacc_first = false) {
     const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
@@ -1065,6 +1070,11 @@ __device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt,
         const uint32_t mh = m1w >> (4 * h);
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = mask_bit(acc[r], mh, rho(r, 0));
+        if (dacc && bb < kTeamDaBlocks) {
+            float* q = dacc + (bb * 5 + T) * 16 * 64 + lane;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) q[r * 64] = (dacc_first ? 0.f : q[r * 64]) + acc[r];
+        }
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
             uint32_t oh[4];
@@ -1217,8 +1227,10 @@ __global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
 template <int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs a) {
     __shared__ uint4 act_s[kTeamLdsU4<NP>];
+    __shared__ float dacc_s[kTeamDaBlocks * 5 * 16 * 64];   // 80 KiB: dA of ≤ 4 blocks across the steps
     const int wt = blockIdx.x;
     const int4 info = reinterpret_cast<const int4*>(a.eb.wtile)[wt];
+    const bool da_loop = a.dA_in_loop && info.y <= kTeamDaBlocks;
     const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
     const float* const dP0 = a.nb.dPout;   // Ws::dP_at(0); dP_at(k) alternates
     for (int s = a.S - 1; s >= 0; --s) {
@@ -1252,15 +1264,40 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs 
         eb.G3 = nb.G3;
         eb.dU += sE;
         eb.dV += sE;
-        edge_bwd_team_body<NP>(eb, wt, act_s);
+        edge_bwd_team_body<NP>(eb, wt, act_s, da_loop ? dacc_s : nullptr, first);
         __syncthreads();   // dU, dV of step s
     }
     if (a.has_tail) node_bwd_team_body<NP, 5>(a.tail, R, act_s);   // dP0 (reads only)
-    if (!a.encoders) return;   // else k_bwd_enc_pair_team runs the rest, edge and node side by side
-    for (int b = 0; b < info.y; ++b) {
-        dA_team_body<NP, B16>(a.da, info.x + b, act_s);
-        __syncthreads();   // the block's dA rows; its last operand buffer may be the next block's first
+    if (da_loop) {   // dA rows of the tile's blocks from the LDS sums (each wave its tile T, as k_dA_team)
+        const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
+        const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        for (int bb = 0; bb < info.y; ++bb) {
+            const float* q = dacc_s + (bb * 5 + T) * 16 * 64 + lane;
+            const int64_t blk = info.x + bb;
+            if constexpr (B16) {
+                __bf16* dArow = reinterpret_cast<__bf16*>(a.da.dA) + blk * 32 * kLdE + i;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * T] = (__bf16)q[r * 64];
+            } else {
+                float* dArow = a.da.dA + blk * 32 * kLdE + i;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * T] = q[r * 64];
+            }
+        }
+    } else if (a.dA_in_loop) {   // a tile of more blocks: the rebuild, here
+        for (int b = 0; b < info.y; ++b) {
+            dA_team_body<NP, B16>(a.da, info.x + b, act_s);
+            __syncthreads();   // its last operand buffer may be the next block's first
+        }
     }
+    if (!a.encoders) return;   // else k_bwd_enc_pair_team runs the rest, edge and node side by side
+    if (!a.dA_in_loop) {
+        for (int b = 0; b < info.y; ++b) {
+            dA_team_body<NP, B16>(a.da, info.x + b, act_s);
+            __syncthreads();   // the block's dA rows; its last operand buffer may be the next block's first
+        }
+    }
+    __syncthreads();   // every wave's dA rows of the tile
     for (int b = 0; b < info.y; ++b) {
         enc_edge_bwd_team_body<NP, B16>(a.eeb, info.x + b, act_s);
         __syncthreads();   // its last exchange buffer is the next body's first
@@ -1271,12 +1308,15 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs 
 // relation-encoder backward on it, the others the object-encoder backward of a 32-node block —
 // independent, so side by side (as the forward's k_enc_pair_team) instead of one after the other.
 template <int NP, bool B16>
-__global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_enc_pair_team(DaArgs da, EncEdgeBwdArgs eeb, EncNodeBwdArgs enb) {
+__global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_enc_pair_team(DaArgs da, EncEdgeBwdArgs eeb, EncNodeBwdArgs enb,
+                                                                    int with_dA) {
     __shared__ uint4 act_s[kTeamLdsU4<NP>];
     const int blk = blockIdx.x;
     if (blk < da.n_eblocks) {
-        dA_team_body<NP, B16>(da, blk, act_s);
-        __syncthreads();   // the block's dA rows, written feature tile by feature tile
+        if (with_dA) {   // else the fused backward left dA in place
+            dA_team_body<NP, B16>(da, blk, act_s);
+            __syncthreads();   // the block's dA rows, written feature tile by feature tile
+        }
         enc_edge_bwd_team_body<NP, B16>(eeb, blk, act_s);
     } else {
         enc_node_bwd_team_body<NP, 5>(enb, TeamRows::block(blk - da.n_eblocks, enb.n_nodes, threadIdx.x & 63), act_s);
@@ -1398,13 +1438,13 @@ hipError_t launch_bwd_fused_team(const BwdFusedArgs& a, int math, hipStream_t st
     return hipGetLastError();
 }
 hipError_t launch_bwd_enc_pair_team(const DaArgs& da, const EncEdgeBwdArgs& eeb, const EncNodeBwdArgs& enb, int math,
-                                    hipStream_t st) {
+                                    int with_dA, hipStream_t st) {
     if (!team_blocks(da.n_eblocks) || !team_blocks((enb.n_nodes + 31) / 32) || da.b16 != eeb.b16 || !enb.wo1ct)
         return hipErrorInvalidValue;
     const dim3 g(da.n_eblocks + (enb.n_nodes + 31) / 32), b(64 * kTeamEdge);
-    if (math == MATH_BF16 && da.b16) hipLaunchKernelGGL((k_bwd_enc_pair_team<1, true>), g, b, 0, st, da, eeb, enb);
-    else if (math == MATH_BF16) hipLaunchKernelGGL((k_bwd_enc_pair_team<1, false>), g, b, 0, st, da, eeb, enb);
-    else if (math == MATH_X6 && !da.b16) hipLaunchKernelGGL((k_bwd_enc_pair_team<3, false>), g, b, 0, st, da, eeb, enb);
+    if (math == MATH_BF16 && da.b16) hipLaunchKernelGGL((k_bwd_enc_pair_team<1, true>), g, b, 0, st, da, eeb, enb, with_dA);
+    else if (math == MATH_BF16) hipLaunchKernelGGL((k_bwd_enc_pair_team<1, false>), g, b, 0, st, da, eeb, enb, with_dA);
+    else if (math == MATH_X6 && !da.b16) hipLaunchKernelGGL((k_bwd_enc_pair_team<3, false>), g, b, 0, st, da, eeb, enb, with_dA);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
