@@ -156,6 +156,13 @@ struct TeamHalf {
 #pragma unroll
         for (int q = 0; q < Q; ++q) raw[q] = *reinterpret_cast<const float4*>(p + 256 * q);
     }
+    // the same block held in LDS (an explicit LDS pointer: ds_read, not flat loads)
+    __device__ __forceinline__ void load_lds(const float* blk_lds, int lane) {
+        typedef __attribute__((address_space(3))) const float lds_f;
+        const lds_f* p = (const lds_f*)blk_lds + ((lane >> 5) * 32 + (lane & 31)) * 4;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) raw[q] = make_float4(p[256 * q], p[256 * q + 1], p[256 * q + 2], p[256 * q + 3]);
+    }
     __device__ __forceinline__ void operator()(int kb, uint32_t (&sp)[3][4]) const {
         const float4 x = raw[2 * kb];
         const float4 y = 2 * kb + 1 < Q ? raw[2 * kb + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -188,7 +195,7 @@ __device__ __forceinline__ int opaque_lane() {
 // block offsets of n's block; vl is the "lane" the cm helpers take: the lane's half, n's row in its
 // block. nc is n clamped into the batch (input arrays of n_nodes rows).
 struct TeamRows {
-    int n, nc, vl;
+    int n, nc, vl, jl;   // jl: the row within the wave-tile (tile mode) / the block (block mode)
     bool valid, zero_pad;
     int64_t oN, oE;
     __device__ __forceinline__ static TeamRows block(int nb, int n_nodes, int lane) {
@@ -197,6 +204,7 @@ struct TeamRows {
         R.valid = R.n < n_nodes;
         R.nc = R.valid ? R.n : n_nodes - 1;
         R.zero_pad = true;
+        R.jl = lane & 31;
         R.oN = (int64_t)nb * kCmBlkN;
         R.oE = (int64_t)nb * kCmBlk;
         R.vl = lane;
@@ -207,6 +215,7 @@ struct TeamRows {
         const int j = lane & 31;
         R.valid = j < nn;
         R.n = R.nc = n0 + (R.valid ? j : 0);
+        R.jl = R.valid ? j : 0;
         R.zero_pad = false;
         R.oN = (int64_t)(R.n >> 5) * kCmBlkN;
         R.oE = (int64_t)(R.n >> 5) * kCmBlk;
@@ -216,7 +225,7 @@ struct TeamRows {
     // the same rows, opaque to the compiler (see opaque_lane): taken once per step of a fused loop
     __device__ __forceinline__ TeamRows opaque() const {
         TeamRows R = *this;
-        asm volatile("" : "+v"(R.n), "+v"(R.nc), "+v"(R.vl), "+v"(R.oN), "+v"(R.oE));
+        asm volatile("" : "+v"(R.n), "+v"(R.nc), "+v"(R.vl), "+v"(R.jl), "+v"(R.oN), "+v"(R.oE));
         return R;
     }
     // a node tile's store: valid lanes their row; padding lanes of a block launch zeros
@@ -506,7 +515,10 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_enc_pair_team(EncEdgeArgs e,
 // node side of one step (k_node_fwd_x6's chain, Networks.py:88-96): waves 0..3 own the four node
 // tiles of a, o1, x' and P' (three LDS exchanges), all five waves one tile each of U', V'.
 template <int NP>
-__device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const TeamRows& R, uint4* act_s) {
+// h2l (the fused forward): the tile's H2s rows as one chunk-major 32-row block in LDS, rows = R.jl,
+// written by the step's edge side — read instead of the global rows (the same values)
+__device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const TeamRows& R, uint4* act_s,
+                                                   const float* h2l = nullptr) {
     const TeamAct<4, NP> act{act_s};
     const int lane = opaque_lane(), h = lane >> 5;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -523,7 +535,8 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
         f32x16 E;
         {
             TeamHalf<kKhE> hr;
-            R.half(hr, a.H2s);
+            if (h2l) hr.load_lds(h2l, (lane & 32) | R.jl);
+            else R.half(hr, a.H2s);
             E = team_gemm(F, hr, [&](int kb) {
                 if (kb < 7) F.load_kb(first7, 4, T, lane, kb);
             });
@@ -786,7 +799,7 @@ __device__ __forceinline__ f32x16 team_lds_gemm(const uint4* buf, const uint4 (&
 // masks are bit-identical. Wave T writes the h2 > 0 word of tile T (wave 0 also the padding words).
 // hs: two buffers of 10 k-blocks × 3 parts × 64 lanes (uint4), 60 KiB, blocks alternate.
 template <int NP, bool AB16>
-__device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt, uint4* hs) {
+__device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt, uint4* hs, float* h2l = nullptr) {
     const int lane = opaque_lane(), h = lane >> 5, i = lane & 31;
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
@@ -948,7 +961,10 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int f = 32 * T + 16 * u + (lane & 15);
-                if (f < 2 * kKhE) a.H2s[cm_index<kKhE>(n0 + node, f)] = nacc[u][r];
+                if (f < 2 * kKhE) {
+                    a.H2s[cm_index<kKhE>(n0 + node, f)] = nacc[u][r];
+                    if (h2l) h2l[cm_offk<kKhE>(node, f)] = nacc[u][r];
+                }
             }
         }
     }
@@ -973,13 +989,18 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a)
 // a wave-tile holds whole towers, so every row a phase reads was written by this workgroup.
 // a pointer the compiler must treat as new in every step: keeps the bodies' per-lane fragment
 // addresses from being hoisted out of the step loop (they would stay live across it and spill)
+// (laundered as a global-address-space pointer: a generic one would turn every access through it
+// into flat memory instructions, which also count against the LDS wait counter)
 template <class T>
 __device__ __forceinline__ void opaque(T*& p) {
-    asm volatile("" : "+s"(p));
+    __attribute__((address_space(1))) T* g = (__attribute__((address_space(1))) T*)p;
+    asm volatile("" : "+s"(g));
+    p = (T*)g;
 }
 template <bool TRAIN, int NP, bool AB16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs a) {
     __shared__ uint4 act_s[kTeamLdsU4<NP>];
+    __shared__ float h2l[kCmBlk];   // the step's H2s rows of the tile (≤ 16 nodes), edge side → node side
     const int wt = blockIdx.x;
     const int4 info = reinterpret_cast<const int4*>(a.ef.wtile)[wt];
     const TeamRows R = TeamRows::tile(info.z, info.w, threadIdx.x & 63);
@@ -1001,7 +1022,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
         if (ef.mask1) ef.mask1 += s * a.m1_step;
         if (ef.mask2) ef.mask2 += s * a.m2_step;
         if (s == 0) TEAM_STAMP(11);
-        edge_fwd_team_body<NP, AB16>(ef, wt, act_s);
+        edge_fwd_team_body<NP, AB16>(ef, wt, act_s, h2l);
         if (s == 0) TEAM_STAMP(12);
         __syncthreads();   // H2s of step s
         NodeFwdArgs nf = a.nf;
@@ -1027,7 +1048,7 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_fwd_fused_team(FwdFusedArgs 
         nf.U = s + 1 < a.S ? const_cast<float*>(a.ef.U) + sE1 : nullptr;   // the same workspace arrays
         nf.V = s + 1 < a.S ? const_cast<float*>(a.ef.V) + sE1 : nullptr;
         if (s == 0) TEAM_STAMP(13);
-        node_fwd_team_body<NP>(nf, R.opaque(), act_s);
+        node_fwd_team_body<NP>(nf, R.opaque(), act_s, h2l);
         if (s == 0) TEAM_STAMP(14);
         __syncthreads();   // P', U', V' of step s + 1
         if (s == 0) TEAM_STAMP(15);
