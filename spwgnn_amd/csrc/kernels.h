@@ -373,10 +373,10 @@ hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipS
 bool enc_pair_team(int n_eblocks, int n_nodes, int math);
 hipError_t launch_enc_pair_team(const EncEdgeArgs& e, const EncNodeArgs& n, int math, bool train, hipStream_t st);
 hipError_t launch_enc_edge_bwd_team(const EncEdgeBwdArgs& a, int math, hipStream_t st);
-// A small batch's whole forward in ONE launch: one workgroup per wave-tile runs both encoders on the
-// tile's blocks and node rows, then the S propagation steps (edge side, node side), separated by
-// workgroup barriers — a wave-tile holds whole towers, so no row it reads is written by another
-// workgroup. The step arrays are the step-0 pointers of ef/nf; step s adds the run's per-step
+// A small batch's S-step forward loop in ONE launch (after k_enc_pair_team; `encoders` puts both
+// encoders in front of it instead): one workgroup per wave-tile runs the S propagation steps (edge
+// side, node side), separated by workgroup barriers — a wave-tile holds whole towers, so no row it
+// reads is written by another workgroup. The step arrays are the step-0 pointers of ef/nf; step s adds the run's per-step
 // strides (Ws::*_at: per step when training, U/V/H2s shared and P alternating when not).
 struct FwdFusedArgs {
     EncEdgeArgs ee;

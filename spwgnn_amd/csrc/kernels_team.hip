@@ -980,10 +980,11 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_edge_fwd_team(EdgeFwdArgs a)
     if ((int)blockIdx.x < a.n_wtiles) edge_fwd_team_body<NP, AB16>(a, blockIdx.x, hs);
 }
 
-// ---- a small batch's forward in one launch (FwdFusedArgs, kernels.h) ----
-// One workgroup of five waves per wave-tile: the relation encoder on each of the tile's blocks, the
-// object encoder on the tile's node rows, then per step the edge side (H2s of the tile's nodes) and
-// the node side (P', U', V' of the same rows). The phases are the team kernels' bodies unchanged —
+// ---- a small batch's forward step loop in one launch (FwdFusedArgs, kernels.h) ----
+// One workgroup of five waves per wave-tile: per step the edge side (H2s of the tile's nodes, also
+// handed to the node side in LDS) and the node side (P', U', V' of the same rows); with `encoders`
+// (diagnosis builds) the relation encoder on the tile's blocks and the object encoder on its rows
+// first. The phases are the team kernels' bodies unchanged —
 // same products in the same order, so every output is bit-identical to the launch-per-phase chain
 // (tests/test_gpu_team.py) — and are separated by workgroup barriers instead of kernel boundaries:
 // a wave-tile holds whole towers, so every row a phase reads was written by this workgroup.
@@ -1242,9 +1243,10 @@ __global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
 
 // ---- a small batch's backward (before the weight gradients) in one launch (BwdFusedArgs) ----
 // One five-wave workgroup per wave-tile: per step S−1 .. 0 the node side (dx, do1, g, G3 and dP of
-// the tile's rows) and the edge side (dU, dV), then d/d 'propagation', the dA rebuild and the
-// relation-encoder backward on the tile's blocks, the object-encoder backward on its rows. Bodies
-// and products are the team kernels' (bit-identical results); phases meet at workgroup barriers.
+// the tile's rows) and the edge side (dU, dV; dh1pre summed into dA in LDS), then d/d 'propagation'
+// and the dA rows (k_bwd_enc_pair_team runs the encoder backwards next; with `encoders`, diagnosis
+// builds, they run here). Bodies and products are the team kernels' (bit-identical results); phases
+// meet at workgroup barriers.
 template <int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs a) {
     __shared__ uint4 act_s[kTeamLdsU4<NP>];
