@@ -216,6 +216,11 @@ int32_t spwgnn_adam_dev(float* params, const float* grads, float* m, float* v, i
                         const float* lr_table, int32_t table_len, float beta1, float beta2, float eps, float l2,
                         float grad_scale, spwgnn_stream_t stream);
 
+/* Epoch sums of model.fit's progress line (main.py:92-98): total3[k] += (double)out3[k] * weights3[k]
+ * for k < 3 (out3 = spwgnn_bce's [loss, correct, n]; weights (n, 1, 1) make Σ loss·n) — one launch,
+ * replayable, no host sync. */
+int32_t spwgnn_accumulate_out3(const float* out3, const double* weights3, double* total3, spwgnn_stream_t stream);
+
 /* Sigmoid readout (Networks.py:93-96) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream);
 

@@ -1215,6 +1215,12 @@ int32_t spwgnn_adam(float* params, const float* grads, float* m, float* v, int64
     return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
 }
 
+int32_t spwgnn_accumulate_out3(const float* out3, const double* weights3, double* total3, spwgnn_stream_t stream) {
+    if (!out3 || !weights3 || !total3) return SPWGNN_E_ARG;
+    hipError_t e = launch_accumulate_out3(out3, weights3, total3, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream) {
     if (!logits || !probs || n < 1) return SPWGNN_E_ARG;
     hipError_t e = launch_sigmoid(logits, probs, n, static_cast<hipStream_t>(stream));

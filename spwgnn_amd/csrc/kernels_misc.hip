@@ -1847,6 +1847,14 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
     hipLaunchKernelGGL(k_tower_readout, dim3((n_towers + 255) / 256), dim3(256), 0, st, z, off, n_towers, mode, out);
     return hipGetLastError();
 }
+__global__ void k_accumulate_out3(const float* out3, const double* w, double* tot) {
+    const int k = threadIdx.x;
+    if (k < 3) tot[k] += (double)out3[k] * w[k];
+}
+hipError_t launch_accumulate_out3(const float* out3, const double* w, double* tot, hipStream_t st) {
+    hipLaunchKernelGGL(k_accumulate_out3, dim3(1), dim3(64), 0, st, out3, w, tot);
+    return hipGetLastError();
+}
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st) {
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
     hipLaunchKernelGGL(k_sigmoid, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, st, z, p, n);

@@ -195,6 +195,13 @@ def step_advance(key_dev: torch.Tensor, step_dev: torch.Tensor, mode: int = _lib
     _lib.check(st, "spwgnn_step_advance")
 
 
+def accumulate_out3(total3: torch.Tensor, out3: torch.Tensor, weights3: torch.Tensor) -> None:
+    """total3 += out3.double() * weights3 (three float64 sums on the device) in one launch."""
+    assert total3.dtype == torch.float64 and weights3.dtype == torch.float64 and out3.dtype == torch.float32
+    st = _lib.lib().spwgnn_accumulate_out3(out3.data_ptr(), weights3.data_ptr(), total3.data_ptr(), _stream(out3.device))
+    _lib.check(st, "spwgnn_accumulate_out3")
+
+
 def sigmoid(logits: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(logits)
     st = _lib.lib().spwgnn_sigmoid(logits.data_ptr(), out.data_ptr(), logits.numel(), _stream(logits.device))

@@ -149,7 +149,7 @@ class KerasModel:
             run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key)
             E.forward(net.flat.data, batch, run, ws, logits=z)
             out3, _ = E.bce(z, target, bce, dlogits=dz)
-            self._tot.add_(out3.double() * w3)
+            E.accumulate_out3(self._tot, out3, w3)   # one launch (was three elementwise torch kernels)
             E.backward(net.flat.data, batch, run, ws, dz, grads=self._grads)
             E.adam_dev(net.flat.data, self._grads, self.m, self.v, ctr.step, ctr.lr_table, self.beta1, self.beta2,
                        self.eps, self.l2)
