@@ -190,6 +190,11 @@ int32_t spwgnn_backward(const float* params, const spwgnn_batch* batch, const sp
 int64_t spwgnn_bce_scratch_bytes(int64_t n);
 int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* out3,
                    float* dlogits, void* scratch, spwgnn_stream_t stream);
+/* spwgnn_bce plus spwgnn_accumulate_out3 in the same launch: total3[k] += (double)out3[k] *
+ * weights3[k] after out3 is written (model.fit's per-batch progress sums, main.py:92-98). */
+int32_t spwgnn_bce_accumulate(const float* logits, const float* targets, int64_t n, float* out3,
+                              float* dlogits, void* scratch, const double* weights3, double* total3,
+                              spwgnn_stream_t stream);
 
 /* Keras-2.x Adam (Networks.py:101: lr=5e-4, decay=0): in-place on the flat buffer.
  * g' = grad_scale*grad + 2*l2*param; lr_t = lr*sqrt(1-b2^t)/(1-b1^t);

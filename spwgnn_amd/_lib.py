@@ -72,6 +72,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_backward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp, vp, vp]),
         "spwgnn_bce_scratch_bytes": (i64, [i64]),
         "spwgnn_bce": (i32, [vp, vp, i64, vp, vp, vp, vp]),
+        "spwgnn_bce_accumulate": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp]),
         "spwgnn_adam": (i32, [vp, vp, vp, vp, i64, i32, f32, f32, f32, f32, f32, f32, vp]),
         "spwgnn_adam_dev": (i32, [vp, vp, vp, vp, i64, vp, vp, i32, f32, f32, f32, f32, f32, vp]),
         "spwgnn_adam_lr_table": (i32, [f32, f32, f32, i32, vp]),

@@ -1140,10 +1140,12 @@ int64_t spwgnn_bce_scratch_bytes(int64_t n) {
     return 256 * 2 * sizeof(float);
 }
 
-int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* out3, float* dlogits, void* scratch,
-                   spwgnn_stream_t stream) {
+static int32_t bce_launch(const float* logits, const float* targets, int64_t n, float* out3, float* dlogits,
+                          void* scratch, const double* weights3, double* total3, spwgnn_stream_t stream) {
     if (!logits || !targets || !out3 || !scratch || n < 1) return SPWGNN_E_ARG;
     BceArgs a{};
+    a.w3 = weights3;
+    a.tot3 = total3;
     a.logits = logits;
     a.targets = targets;
     a.n = n;
@@ -1153,6 +1155,17 @@ int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* 
     a.blocks = (int)std::min<int64_t>(256, (n + 255) / 256);
     hipError_t e = launch_bce(a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
+int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* out3, float* dlogits, void* scratch,
+                   spwgnn_stream_t stream) {
+    return bce_launch(logits, targets, n, out3, dlogits, scratch, nullptr, nullptr, stream);
+}
+
+int32_t spwgnn_bce_accumulate(const float* logits, const float* targets, int64_t n, float* out3, float* dlogits,
+                              void* scratch, const double* weights3, double* total3, spwgnn_stream_t stream) {
+    if (!weights3 || !total3) return SPWGNN_E_ARG;
+    return bce_launch(logits, targets, n, out3, dlogits, scratch, weights3, total3, stream);
 }
 
 static float adam_lr_t(float lr, float beta1, float beta2, double t) {

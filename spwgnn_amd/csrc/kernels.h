@@ -301,6 +301,8 @@ struct BceArgs {
     float* partial;   // [blocks][2]
     float* out3;
     int blocks;
+    const double* w3;   // non-null: tot3[k] += (double)out3[k] * w3[k] by the thread that writes out3
+    double* tot3;
 };
 struct AdamArgs {
     float *p, *m, *v;

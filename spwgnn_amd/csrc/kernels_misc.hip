@@ -1415,6 +1415,16 @@ constexpr float kLogitClip = 16.11809565f;
 
 // FINAL (a.blocks == 1, e.g. the reference's batch 32): the one workgroup also writes out3, the
 // same double-precision division k_bce_final does over its one partial — one launch instead of two.
+// With a.tot3 the thread that writes out3 also adds it into the epoch sums (k_accumulate_out3's
+// arithmetic on the same float values).
+__device__ inline void bce_store_out3(const BceArgs& a, float loss, float correct) {
+    const float o[3] = {loss, correct, (float)a.n};
+    for (int k = 0; k < 3; ++k) {
+        a.out3[k] = o[k];
+        if (a.tot3) a.tot3[k] += (double)o[k] * a.w3[k];
+    }
+}
+
 template <bool FINAL>
 __global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
     __shared__ float sl[256], sc[256];
@@ -1440,9 +1450,7 @@ __global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
     }
     if (threadIdx.x == 0) {
         if constexpr (FINAL) {
-            a.out3[0] = (float)((double)sl[0] / (double)a.n);
-            a.out3[1] = (float)(double)sc[0];
-            a.out3[2] = (float)a.n;
+            bce_store_out3(a, (float)((double)sl[0] / (double)a.n), (float)(double)sc[0]);
         } else {
             a.partial[2 * blockIdx.x] = sl[0];
             a.partial[2 * blockIdx.x + 1] = sc[0];
@@ -1457,9 +1465,7 @@ __global__ void k_bce_final(BceArgs a) {
         ls += a.partial[2 * b];
         cs += a.partial[2 * b + 1];
     }
-    a.out3[0] = (float)(ls / (double)a.n);
-    a.out3[1] = (float)cs;
-    a.out3[2] = (float)a.n;
+    bce_store_out3(a, (float)(ls / (double)a.n), (float)cs);
 }
 
 __global__ void k_adam(AdamArgs a) {

@@ -150,15 +150,23 @@ class BceScratch:
         self.out3 = torch.empty(3, dtype=torch.float32, device=device)
 
 
-def bce(logits: torch.Tensor, targets: torch.Tensor, scratch: BceScratch, dlogits: Optional[torch.Tensor] = None):
+def bce(logits: torch.Tensor, targets: torch.Tensor, scratch: BceScratch, dlogits: Optional[torch.Tensor] = None,
+        total3: Optional[torch.Tensor] = None, weights3: Optional[torch.Tensor] = None):
     """Keras binary_crossentropy (+ binary_accuracy numerator) and d loss / d logit on device.
-    Returns out3 = [loss, n_correct, n] (device) and dlogits."""
+    Returns out3 = [loss, n_correct, n] (device) and dlogits. With total3/weights3 (float64) the
+    same launch also does total3 += out3.double() * weights3 (spwgnn_bce_accumulate)."""
     targets = targets.reshape(-1).to(torch.float32).contiguous()
     if dlogits is None:
         dlogits = torch.empty_like(logits)
-    st = _lib.lib().spwgnn_bce(logits.data_ptr(), targets.data_ptr(), logits.numel(), scratch.out3.data_ptr(),
-                               dlogits.data_ptr(), scratch.scratch.data_ptr(), _stream(logits.device))
-    _lib.check(st, "spwgnn_bce")
+    args = (logits.data_ptr(), targets.data_ptr(), logits.numel(), scratch.out3.data_ptr(), dlogits.data_ptr(),
+            scratch.scratch.data_ptr())
+    if total3 is None:
+        st = _lib.lib().spwgnn_bce(*args, _stream(logits.device))
+        _lib.check(st, "spwgnn_bce")
+    else:
+        assert total3.dtype == torch.float64 and weights3 is not None and weights3.dtype == torch.float64
+        st = _lib.lib().spwgnn_bce_accumulate(*args, weights3.data_ptr(), total3.data_ptr(), _stream(logits.device))
+        _lib.check(st, "spwgnn_bce_accumulate")
     return scratch.out3, dlogits
 
 

@@ -148,8 +148,7 @@ class KerasModel:
             E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_COUNTER)
             run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key)
             E.forward(net.flat.data, batch, run, ws, logits=z)
-            out3, _ = E.bce(z, target, bce, dlogits=dz)
-            E.accumulate_out3(self._tot, out3, w3)   # one launch (was three elementwise torch kernels)
+            E.bce(z, target, bce, dlogits=dz, total3=self._tot, weights3=w3)   # loss + epoch sums, one launch
             E.backward(net.flat.data, batch, run, ws, dz, grads=self._grads)
             E.adam_dev(net.flat.data, self._grads, self.m, self.v, ctr.step, ctr.lr_table, self.beta1, self.beta2,
                        self.eps, self.l2)

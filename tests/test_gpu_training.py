@@ -317,3 +317,28 @@ def test_batch_upload_pinned_roundtrip():
     for a, t in zip(arrs, out):
         assert t.device.type == "cuda" and t.shape == a.shape
         assert np.array_equal(t.cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("n", [192, 70000])
+def test_bce_accumulate_equals_bce_then_accumulate(n):
+    """spwgnn_bce_accumulate (loss + the fit's epoch sums in one launch) against spwgnn_bce followed
+    by spwgnn_accumulate_out3, bit for bit, over two batches — one workgroup (the reference's batch
+    32 × 6 boxes) and the multi-block + k_bce_final path; the sums also against float64 on the host."""
+    rng = np.random.default_rng(n)
+    w3 = torch.tensor([float(n), 1.0, 1.0], dtype=torch.float64, device="cuda")
+    tot_a = torch.zeros(3, dtype=torch.float64, device="cuda")
+    tot_b = torch.zeros(3, dtype=torch.float64, device="cuda")
+    host = np.zeros(3)
+    for _ in range(2):
+        z = torch.tensor(rng.normal(scale=3.0, size=n).astype(np.float32), device="cuda")
+        t = torch.tensor(rng.integers(0, 2, n).astype(np.float32), device="cuda")
+        sa, sb = E.BceScratch("cuda"), E.BceScratch("cuda")
+        oa, da = E.bce(z, t, sa, total3=tot_a, weights3=w3)
+        ob, db = E.bce(z, t, sb)
+        E.accumulate_out3(tot_b, ob, w3)
+        torch.cuda.synchronize()
+        assert torch.equal(oa, ob) and torch.equal(da, db)
+        host += oa.double().cpu().numpy() * w3.cpu().numpy()
+    torch.cuda.synchronize()
+    assert torch.equal(tot_a, tot_b)
+    assert np.array_equal(tot_a.cpu().numpy(), host)
