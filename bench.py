@@ -97,11 +97,12 @@ FUSED_PMC = {"edge_fwd": "k_fwd_fused", "node_bwd": "k_bwd_fused", "enc_edge_bwd
 _FUSED = [False]
 
 
-def fused_small(batches, math) -> bool:
-    """Whether these batches take the fused small-batch launches (api.hip fwd_fused_team)."""
-    lim = 512
-    return math != "f32" and all(b.n_wtiles <= lim and b.n_eblocks <= lim and (b.n_nodes + 31) // 32 <= lim
-                                 and b.nw_max <= 16 and not (getattr(b, "flags", 0) & 1) for b in batches)
+def fused_small(batches, math, S, dropout=0.1) -> bool:
+    """Whether these batches' training steps take the fused small-batch launches: the
+    library's own gate (spwgnn_fused_path), so the kernel table's attribution cannot drift from it."""
+    from spwgnn_amd import engine as E
+    run = E.RunConfig(S, training=True, dropout=dropout, math=math)
+    return all(E.fused_path(b, run) == 3 for b in batches)
 
 
 def kernel_flops(kernel, Ne, Nn, S):
@@ -276,18 +277,22 @@ def cpu_time(cfg: dict, seconds: float, threads: int, form: str):
 
 
 def cpu_baseline(cfg: dict, seconds: float):
-    """SURVEY §8d / BASELINE.md CPU plan: the oracle at up to 16 host threads (the reported value: the
-    literal dense form Keras runs), its gather form, and 1 thread; timed on this host's cores."""
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    """SURVEY §8d / BASELINE.md CPU plan: the oracle on every host core this process may run on
+    (len(os.sched_getaffinity(0)); the reported value: the literal dense form Keras runs), its gather
+    form on the same cores, and beside them the dense form at 16 threads and at 1 thread."""
+    threads = max(1, len(os.sched_getaffinity(0)))
     dense, dsamp = cpu_time(cfg, seconds, threads, "dense")
     gather, gsamp = cpu_time(cfg, seconds / 2, threads, "gather")
+    t16 = min(16, threads)
+    d16, samp16 = (dense, dsamp) if t16 == threads else cpu_time(cfg, seconds / 2, t16, "dense")
     one, osamp = cpu_time(cfg, max(3.0, seconds / 4), 1, "dense")
     what = "fwd" if cfg["mode"] == "infer" else "fwd+bwd"
     return {"value": round(dense, 1), "unit": "towers/s", "cores": threads, "kind": "port",
             "sample": f"oracle.forward_dense fp32 {what} ({dsamp}), N={cfg['nodes']}, S={cfg['S']}, "
-                      f"{cfg['relations']} relations, torch CPU threads={threads}; gather form "
-                      f"{gather:.1f} towers/s ({gsamp}); dense at 1 thread {one:.1f} towers/s ({osamp})",
-            "value_gather": round(gather, 1), "value_1thread": round(one, 1)}
+                      f"{cfg['relations']} relations, torch CPU threads={threads} (the affinity set); gather "
+                      f"form {gather:.1f} towers/s ({gsamp}); dense at {t16} threads {d16:.1f} towers/s "
+                      f"({samp16}); dense at 1 thread {one:.1f} towers/s ({osamp})",
+            "value_gather": round(gather, 1), "value_16threads": round(d16, 1), "value_1thread": round(one, 1)}
 
 
 # ------------------------------------------------------------------------------ PMC traffic
@@ -476,7 +481,7 @@ def run_train(args, cfg, world, rank, device):
     Nn = sum(b.n_nodes for b in batches)
     B = sum(b.n_towers for b in batches)
     wl = workload_name(cfg, world, args.dropout)
-    _FUSED[0] = fused_small(batches, math)
+    _FUSED[0] = fused_small(batches, math, S, args.dropout)
 
     # every timed kernel's per-step time, before the timed region (untimed steps), so the roofline
     # can name the DOMINANT kernel (largest ms per step) and time it inside the timed region

@@ -171,6 +171,11 @@ typedef struct spwgnn_run {
 /* Workspace bytes for (n_nodes, n_eblocks, mp_steps, training). */
 int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training);
 
+/* Which launches a forward / backward of this batch and run takes (no device work): bit 0 = the
+ * forward's fused small-batch step loop, bit 1 = the backward's; < 0 = an error
+ * status. Profilers attribute kernel time and FLOPs by it instead of restating the library's gate. */
+int32_t spwgnn_fused_path(const spwgnn_batch* batch, const spwgnn_run* run);
+
 /* Forward: the whole graph of Networks.py:31-96 → per-node logits z (the model output is
  * sigmoid(z), Networks.py:94). logits: [n_nodes] device fp32. */
 int32_t spwgnn_forward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run,

@@ -68,6 +68,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_plan_size_recv": (i32, [i32, vp, i32, C.POINTER(PlanSizes)]),
         "spwgnn_plan_fill_recv": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
         "spwgnn_workspace_bytes": (i64, [i32, i32, i32, i32]),
+        "spwgnn_fused_path": (i32, [C.POINTER(BatchC), C.POINTER(RunC)]),
         "spwgnn_forward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp]),
         "spwgnn_backward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp, vp, vp]),
         "spwgnn_bce_scratch_bytes": (i64, [i64]),

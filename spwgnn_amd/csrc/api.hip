@@ -320,6 +320,21 @@ static bool store_b16_node(const spwgnn_run* r, const spwgnn_batch* b) {
            !team_blocks(b->n_wtiles) && !team_blocks((b->n_nodes + 31) / 32) && !getenv_flag("SPWGNN_NODE_F32");
 }
 
+// Whether a forward / backward takes the fused small-batch step loops. One place for
+// the gate: run_forward, run_backward and spwgnn_fused_path (the bench's kernel attribution) use it.
+static bool fwd_fused_taken(const spwgnn_run* r, const spwgnn_batch* b) {
+    const bool one_math = r->math == kmath(r, kX6EncEdge) && r->math == kmath(r, kX6EdgeFwd) &&
+                          r->math == kmath(r, kX6NodeFwd);
+    return one_math && fwd_fused_team(b->n_wtiles, b->nw_max, b->n_eblocks, b->n_nodes, r->math) &&
+           !(b->flags & SPWGNN_BATCH_RECV_BLOCKS) && !store_b16_node(r, b) && !getenv_flag("SPWGNN_NO_FWD_FUSED");
+}
+static bool bwd_fused_taken(const spwgnn_run* r, const spwgnn_batch* b) {
+    const bool one_math = r->math == kmath(r, kX6NodeBwd) && r->math == kmath(r, kX6EdgeBwd) &&
+                          r->math == kmath(r, kX6EncEdgeBwd);
+    return one_math && rebuild_dA(r, b) && fwd_fused_team(b->n_wtiles, b->nw_max, b->n_eblocks, b->n_nodes, r->math) &&
+           !(b->flags & SPWGNN_BATCH_RECV_BLOCKS) && !store_b16_node(r, b) && !getenv_flag("SPWGNN_NO_BWD_FUSED");
+}
+
 static int32_t run_forward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w,
                            char* base, float* logits, hipStream_t st) {
     Ctx c{w, base};
@@ -475,10 +490,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         nf.n16 = store_b16_node(r, b);
         return nf;
     };
-    const bool one_math = r->math == kmath(r, kX6EncEdge) && r->math == kmath(r, kX6EdgeFwd) &&
-                          r->math == kmath(r, kX6NodeFwd);
-    if (one_math && fwd_fused_team(b->n_wtiles, b->nw_max, b->n_eblocks, b->n_nodes, r->math) &&
-        !(b->flags & SPWGNN_BATCH_RECV_BLOCKS) && !getenv_flag("SPWGNN_NO_FWD_FUSED")) {
+    if (fwd_fused_taken(r, b)) {
         // small batch: the encoders and all S steps in one launch (timed as the relation encoder)
         FwdFusedArgs fa{};
         fa.ee = ee;
@@ -883,10 +895,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         enb.x_om1t = c.x6(X6_OM1T);
     }
 
-    const bool one_math = r->math == kmath(r, kX6NodeBwd) && r->math == kmath(r, kX6EdgeBwd) &&
-                          r->math == kmath(r, kX6EncEdgeBwd);
-    if (one_math && rebuild && fwd_fused_team(b->n_wtiles, b->nw_max, b->n_eblocks, b->n_nodes, r->math) &&
-        !(b->flags & SPWGNN_BATCH_RECV_BLOCKS) && !n16 && !getenv_flag("SPWGNN_NO_BWD_FUSED")) {
+    if (bwd_fused_taken(r, b)) {
         // small batch: the step loop, dA and both encoder backwards in one launch (timed as the node backward)
         BwdFusedArgs fa{};
         fa.nb = node_args(0);
@@ -1062,24 +1071,30 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st, p3_in_batch ? &p3 : nullptr));
         SPW_CHECK(prof.after(SPWGNN_K_WGRAD_WS));
     }
-    {   // the float ranges no reduction of this batch writes: alignment gaps, uncovered tensor rows
+    {   // the float ranges no reduction of this batch writes: alignment gaps, uncovered tensor rows.
+        // More ranges than the launch carries (kMaxZero) or no reduction at all: one memset of the
+        // whole buffer instead (stream-ordered before the reduction, which then writes its ranges)
         const ParamTable& pt = param_table();
         rb.nzero = 0;
+        bool overflow = false;
         auto zero = [&](int64_t off, int64_t len) {
-            if (len <= 0) return true;
+            if (len <= 0) return;
             if (rb.nzero > 0 && rb.zoff[rb.nzero - 1] + rb.zlen[rb.nzero - 1] == off) {   // merge
                 rb.zlen[rb.nzero - 1] += (int32_t)len;
-                return true;
+            } else if (rb.nzero < kMaxZero) {
+                rb.zoff[rb.nzero] = off;
+                rb.zlen[rb.nzero++] = (int32_t)len;
+            } else {
+                overflow = true;
             }
-            if (rb.nzero >= kMaxZero) return false;
-            rb.zoff[rb.nzero] = off;
-            rb.zlen[rb.nzero++] = (int32_t)len;
-            return true;
         };
-        for (int t = 0; t < kNumTensors; ++t) {
+        constexpr int kMaxRows = 512;   // the largest Keras tensor has 350 rows (rmp.0 kernel)
+        uint8_t row[kMaxRows];
+        for (int t = 0; t < kNumTensors && !overflow; ++t) {
             const TensorDesc& d = pt.t[t];
+            if (d.rows > kMaxRows) return SPWGNN_E_ARG;
             const int64_t end = t + 1 < kNumTensors ? pt.t[t + 1].offset : pt.total;
-            std::vector<char> row(d.rows, 0);   // rows (kernels) or the one bias row written by some job
+            memset(row, 0, d.rows);   // rows (kernels) or the one bias row written by some job
             for (int k = 0; k < rb.n; ++k) {
                 const ReduceArgs& ra = rb.r[k];
                 if (d.rows > 1 && ra.kernel_off == d.offset)
@@ -1088,10 +1103,10 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
                 if (d.rows == 1 && ra.bias_off == d.offset) row[0] = 1;
             }
             for (int q = 0; q < d.rows; ++q)
-                if (!row[q] && !zero(d.offset + (int64_t)q * d.cols, d.cols)) return SPWGNN_E_ARG;
-            if (!zero(d.offset + (int64_t)d.rows * d.cols, end - d.offset - (int64_t)d.rows * d.cols)) return SPWGNN_E_ARG;
+                if (!row[q]) zero(d.offset + (int64_t)q * d.cols, d.cols);
+            zero(d.offset + (int64_t)d.rows * d.cols, end - d.offset - (int64_t)d.rows * d.cols);
         }
-        if (rb.n == 0 && rb.nzero > 0) {   // nothing reduced at all: the whole buffer is zero
+        if (overflow || (rb.n == 0 && rb.nzero > 0)) {
             SPW_CHECK(hipMemsetAsync(grads, 0, pt.total * sizeof(float), st));
             rb.nzero = 0;
         }
@@ -1109,6 +1124,12 @@ extern "C" {
 int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_steps, int32_t training) {
     if (n_nodes < 1 || n_eblocks < 1 || mp_steps < 1) return -1;
     return make_ws(n_nodes, n_eblocks, mp_steps, training ? 1 : 0).total;
+}
+
+int32_t spwgnn_fused_path(const spwgnn_batch* batch, const spwgnn_run* run) {
+    const int32_t stt = validate(batch, run);
+    if (stt) return stt;
+    return (fwd_fused_taken(run, batch) ? 1 : 0) | (run->training && bwd_fused_taken(run, batch) ? 2 : 0);
 }
 
 int32_t spwgnn_forward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run, void* workspace,

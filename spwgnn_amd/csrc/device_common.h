@@ -45,6 +45,8 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
     return __builtin_bit_cast(uint32_t, r);
 }
 __device__ __forceinline__ float bf16_lo(uint32_t p) { return __uint_as_float(p << 16); }
+// x rounded to bf16 (RNE), as an fp32 value
+__device__ __forceinline__ float bf16_round(float x) { return __uint_as_float(pk_bf16(x, 0.f) << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 // (a, b) → three packed bf16 pairs h, m, l (element 0 = a in the low half)
 // bf16_lo of h and m as a v_perm_b32: written as a shift, the compiler rebuilds it as a second
@@ -131,13 +133,26 @@ __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 __device__ __forceinline__ float mask_bit(float g, uint32_t bits, int f) {
     return __uint_as_float(__float_as_uint(g) & (uint32_t)__builtin_amdgcn_sbfe((int)bits, f, 1));
 }
-// tanh(x) = 1 − 2/(2^(2x·log2 e) + 1) on the transcendental unit (v_exp_f32, v_rcp_f32): 5
-// instructions instead of libm tanhf's ≈ 22 (two thirds of the node forward's non-split VALU).
-// Absolute error ≤ 4.2e-7 (libm: 6e-8) — the size of the split-bf16 products' own error (§3b);
-// ±1 at ±∞, NaN propagates. Used by the split-bf16 node forward; f32 math keeps tanhf.
-__device__ __forceinline__ float fast_tanh(float x) {
+// tanh in fp32 for the split-bf16 node kernels, ≤ 1 ulp below |x| = 0.625 and ≤ 2 ulp above (libm
+// tanhf: ≤ 1). Above 0.625: 1 − 2/(2^(2x·log2 e) + 1) on the transcendental unit (v_exp_f32,
+// v_rcp_f32), exact in the limits (±1 at ±∞, NaN propagates). Below: x + x³·p(x²), p a degree-4 fit of
+// (tanh x − x)/x³ on [0, 0.625] (max 0.72 ulp in fp32) — the exp form cancels there (1 − 0.999…) and
+// loses up to 4·10⁵ ulp of relative accuracy near 0, which bf16 math then rounds into its operands
+// (it was the engine's offset from the bf16 emulator). 14 VALU instead of libm's ≈ 22.
+__device__ __forceinline__ float acc_tanh(float x) {
+    const float u = x * x;
+    float p = __builtin_fmaf(-0.005700227044831583f, u, 0.020631621187850974f);
+    p = __builtin_fmaf(p, u, -0.053736200685166706f);
+    p = __builtin_fmaf(p, u, 0.13331381511777754f);
+    p = __builtin_fmaf(p, u, -0.333332788328783f);
+    const float small = __builtin_fmaf(x * u, p, x);
     const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
-    return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+    const float big = __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+#ifdef SPWGNN_TANH_EXP_ONLY   // diagnosis A/B: the exp form everywhere (rounds 1-4's fast_tanh)
+    return big + 0.f * small;
+#else
+    return __builtin_fabsf(x) < 0.625f ? small : big;
+#endif
 }
 // The 2-input first Dense of the encoders with one explicit rounding order: left to the compiler,
 // unrolled copies of x0·w0 + x1·w1 + b were contracted / paired differently, so an edge's value

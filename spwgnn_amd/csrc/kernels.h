@@ -362,7 +362,10 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
 
 // Team kernels (kernels_team.hip): one block per workgroup of waves that split each layer's output
 // tiles — the latency-bound small batches (the reference's batch 32) up to kTeamMaxBlocks blocks
-constexpr int kTeamMaxBlocks = 512;
+#ifndef SPWGNN_TEAM_MAX_BLOCKS   // diagnosis builds lift it to time the team / fused kernels at large batches
+#define SPWGNN_TEAM_MAX_BLOCKS 512
+#endif
+constexpr int kTeamMaxBlocks = SPWGNN_TEAM_MAX_BLOCKS;
 bool team_blocks(int n_blocks);   // 32-row blocks of the launch (edge or node blocks)
 hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st);

@@ -307,7 +307,10 @@ __device__ __forceinline__ void segsum_walk_b(const float* st, float* nacc, uint
 // dA (Σ over steps of dh1pre) is written by the first backward step and accumulated by the later
 // ones with no-return float atomics (one add per element per launch, launches stream-ordered:
 // the summation order is fixed, so the result stays deterministic).
-template <bool ONEHOT, bool ACCUM>
+// B16 (bf16 math on wave-tiles of 17–32 nodes, which only this kernel serves): the products' operands
+// dh2pre and W2ᵀ rounded to bf16 and the sender/receiver sums adding bf16(dh1pre) — the bf16
+// arithmetic of the split-bf16 kernels on the fp32 matrix core; dA stays Σ fp32.
+template <bool ONEHOT, bool ACCUM, bool B16 = false>
 __global__ __launch_bounds__(ONEHOT ? 512 : 256, ONEHOT ? 1 : 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_edge_bwd(EdgeBwdArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, i = lane & 31;
@@ -387,6 +390,10 @@ void k_edge_bwd(EdgeBwdArgs a) {
             xv[2] = (bits & 4u) ? g.z : 0.f;
             xv[3] = (bits & 8u) ? g.w : 0.f;
             if (a.dh2_out) *reinterpret_cast<float4*>(dh2cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+            if (B16) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) xv[k] = bf16_round(xv[k]);
+            }
             ahead = G4[64 * min(q + 1, kKhE / 4 - 1)];  // unconditional (clamped) prefetch
             const float* wq = wrow + (ONEHOT ? 4 * q : 4 * q * kLdE);
             float4 wv = ONEHOT ? *reinterpret_cast<const float4*>(wq)
@@ -399,6 +406,7 @@ void k_edge_bwd(EdgeBwdArgs a) {
                     wn = ONEHOT ? *reinterpret_cast<const float4*>(wt1)
                                 : make_float4(wt1[0], wt1[kLdE], wt1[2 * kLdE], wt1[3 * kLdE]);
                 }
+                if (B16) wv = make_float4(bf16_round(wv.x), bf16_round(wv.y), bf16_round(wv.z), bf16_round(wv.w));
                 acc[t] = mfma32(xv[0], wv.x, acc[t]);
                 acc[t] = mfma32(xv[1], wv.y, acc[t]);
                 acc[t] = mfma32(xv[2], wv.z, acc[t]);
@@ -458,7 +466,8 @@ void k_edge_bwd(EdgeBwdArgs a) {
                     const int t = 2 * rd + slot;
                     if (t >= 5) continue;
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = acc[t][r];
+                    for (int r = 0; r < 16; ++r)
+                        st[slot * 1056 + (rho(r, 0) + 4 * h) * 33 + i] = B16 ? bf16_round(acc[t][r]) : acc[t][r];
                 }
                 wave_lds_sync();
                 const int t = 2 * rd + h;
@@ -897,10 +906,15 @@ hipError_t launch_edge_bwd(const EdgeBwdArgs& a, int math, hipStream_t st) {
             hipLaunchKernelGGL((k_edge_bwd<true, false>), dim3(edge_grid(a.n_wtiles)), dim3(64 * kEdgeWaves), 0, st, a);
     } else {
         const size_t lds = edge_bwd_lds_per_wave(a.nw_max) * a.wpg;
-        if (a.dA_accumulate)
-            hipLaunchKernelGGL((k_edge_bwd<false, true>), dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
-        else
-            hipLaunchKernelGGL((k_edge_bwd<false, false>), dim3((a.n_wtiles + a.wpg - 1) / a.wpg), dim3(64 * a.wpg), lds, st, a);
+        const dim3 g((a.n_wtiles + a.wpg - 1) / a.wpg), b(64 * a.wpg);
+        if (math == MATH_BF16) {
+            if (a.dA_accumulate) hipLaunchKernelGGL((k_edge_bwd<false, true, true>), g, b, lds, st, a);
+            else hipLaunchKernelGGL((k_edge_bwd<false, false, true>), g, b, lds, st, a);
+        } else if (a.dA_accumulate) {
+            hipLaunchKernelGGL((k_edge_bwd<false, true>), g, b, lds, st, a);
+        } else {
+            hipLaunchKernelGGL((k_edge_bwd<false, false>), g, b, lds, st, a);
+        }
     }
     return hipGetLastError();
 }

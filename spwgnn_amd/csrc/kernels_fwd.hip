@@ -362,6 +362,14 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_x6(EncEdgeArg
     tchain_x6s<5, 10, 5, NC, kX6Ring, NP, NW>(Y, X, a.x_w1a, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) bias_act_rho<5, false>(X[c], a.b_w1a, h);
+    if constexpr (TRAIN && NP == 1 && !B16) {   // bf16 math with fp32 storage (tiles of 17–32 nodes): A
+#pragma unroll                                   // rounded as the bf16-stored copy is
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) X[c][t][r] = bf16_round(X[c][t][r]);
+    }
     save(a.A, nullptr, X, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
 }
 
@@ -701,7 +709,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = rho(r, 0) + 4 * h + 32 * t;
-                E[c][t][r] = f < kFN ? fast_tanh(E[c][t][r]) : 0.f;
+                E[c][t][r] = f < kFN ? acc_tanh(E[c][t][r]) : 0.f;
             }
         if (a.a_out && has[c]) store_cm<4>(a.a_out + bN(c), E[c], lane, valid[c]);
     }
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int f = rho(r, 0) + 4 * h + 32 * t;
-                X[c][t][r] = f < kFN ? fast_tanh(X[c][t][r] + P[t][r]) : 0.f;   // X := P'
+                X[c][t][r] = f < kFN ? acc_tanh(X[c][t][r] + P[t][r]) : 0.f;   // X := P'
             }
         if (has[c]) store_cm<4>(a.Pn + bN(c), X[c], lane, valid[c]);
     }

@@ -358,6 +358,10 @@ __device__ __forceinline__ void enc_edge_team_body(const EncEdgeArgs& a, int blk
             }
         }
         if (l == 3) {
+            if constexpr (TRAIN && NP == 1 && !B16) {   // bf16 math, fp32 storage (tiles of 17–32 nodes):
+#pragma unroll                                           // A rounded as the bf16-stored copy is (§6b)
+                for (int r = 0; r < 16; ++r) x[r] = bf16_round(x[r]);
+            }
             save(a.A, -1, x, true);   // chunk-major; k_edge_fwd masks padding edges (B16: bf16, §3g)
         } else {
             if (TRAIN) save(l == 0 ? a.z2 : l == 1 ? a.z3 : a.cr, l + 1, x, true);
@@ -545,7 +549,7 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * T;
-            E[r] = f < kFN ? fast_tanh(E[r]) : 0.f;
+            E[r] = f < kFN ? acc_tanh(E[r]) : 0.f;
         }
         if (a.a_out) R.store<kKhN>(a.a_out, E, T);
         act.put(0, T, E, lane);
@@ -593,7 +597,7 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, 0) + 4 * h + 32 * T;
-            X[r] = f < kFN ? fast_tanh(X[r] + P[r]) : 0.f;   // X := P'
+            X[r] = f < kFN ? acc_tanh(X[r] + P[r]) : 0.f;   // X := P'
         }
         R.store<kKhN>(a.Pn, X, T);
         act.put(0, T, X, lane);
@@ -1247,6 +1251,14 @@ __global__ __launch_bounds__(256) void k_enc_node_bwd_team(EncNodeBwdArgs a) {
 // and the dA rows (k_bwd_enc_pair_team runs the encoder backwards next; with `encoders`, diagnosis
 // builds, they run here). Bodies and products are the team kernels' (bit-identical results); phases
 // meet at workgroup barriers.
+// The fused backward's static LDS (exchange buffers + the dA sums) needs gfx950's 160 KiB per CU; a
+// build for a smaller-LDS target stops here with this message rather than in the linker.
+constexpr size_t kLdsBytesGfx950 = 160 * 1024;
+static_assert(sizeof(uint4) * kTeamLdsU4<3> + sizeof(float) * kTeamDaBlocks * 5 * 16 * 64 <= kLdsBytesGfx950,
+              "k_bwd_fused_team: exchange buffers + dA sums exceed the 160 KiB LDS of gfx950");
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libspwgnn_hip targets gfx950 (160 KiB LDS per CU): the fused small-batch backward needs it"
+#endif
 template <int NP, bool B16>
 __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_fused_team(BwdFusedArgs a) {
     __shared__ uint4 act_s[kTeamLdsU4<NP>];

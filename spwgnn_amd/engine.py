@@ -100,6 +100,17 @@ def workspace_bytes(batch: TowerBatch, run: RunConfig) -> int:
     return n
 
 
+def fused_path(batch: TowerBatch, run: RunConfig) -> int:
+    """The library's own answer to which launches this batch and run take (spwgnn_fused_path): bit 0 =
+    the forward's fused small-batch step loop, bit 1 = the backward's. No device work."""
+    b = batch.cstruct()
+    r = run.cstruct()
+    st = _lib.lib().spwgnn_fused_path(C.byref(b), C.byref(r))
+    if st < 0:
+        _lib.check(st, "spwgnn_fused_path")
+    return int(st)
+
+
 def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Workspace,
             logits: Optional[torch.Tensor] = None) -> torch.Tensor:
     _require_gpu(flat_params, "params")

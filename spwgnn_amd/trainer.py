@@ -221,19 +221,18 @@ class Trainer:
             out3, dz = self.engine.loss(z, tg)
             # [loss, correct, n] of this micro-batch, folded in before the engine reuses its buffer:
             # Σ loss_i·n_i, Σ correct_i, Σ n_i (the engine's out3 is one persistent tensor)
-            wt = self._w3.get((b.n_nodes, out3.device))
+            key = (b.n_nodes, out3.device)
+            wt = self._w3.pop(key, None)
             if wt is None:
-                wt = self._w3[(b.n_nodes, out3.device)] = out3.new_tensor([float(b.n_nodes), 1.0, 1.0],
-                                                                           dtype=torch.float64)
+                wt = out3.new_tensor([float(b.n_nodes), 1.0, 1.0], dtype=torch.float64)
+            self._w3[key] = wt            # most recent last; ragged micro-batches keep at most 16
+            while len(self._w3) > 16:
+                self._w3.pop(next(iter(self._w3)))
             w3 = out3.double() * wt
             tot3 = w3 if tot3 is None else tot3 + w3
             g = self.engine.backward(self.params, b, run, dz)
             w = b.n_nodes / n_global
-            if len(batches) == 1:
-                acc = g
-                if w != 1.0:
-                    acc.mul_(w)
-            elif acc is None:
+            if acc is None:
                 acc = g.mul(w)            # own buffer: the engine reuses its gradient buffer
             else:
                 acc.add_(g, alpha=w)

@@ -136,6 +136,37 @@ def test_bf16_math_against_bf16_emulator(N, fully, dropout):
     _bf16_check(z.reshape(-1), g, ref, band, f"bf16 N={N} fully={fully} dropout={dropout}", loss)
 
 
+def test_bf16_thresholded_n6_band_probe_shape():
+    """The shape tools/bf16_band_probe.py found farthest from the emulator before the node kernels'
+    tanh was made fp32-accurate near 0: 64 thresholded 6-block towers, S = 5."""
+    params = O.random_params(44)
+    pos, sizes, src, dst, te, _ = D.ragged_batch(64, 6, 6, seed=3)
+    n = int(sizes.sum())
+    tgt = np.random.default_rng(12).integers(0, 2, size=n).astype(np.float32)
+    batch = TowerBatch.from_edges(pos, sizes, src, dst, te, device="cuda")
+    z, loss, g = _train(P.to_flat(params, device="cuda"), batch, tgt, 5, "bf16")
+    ref, band = OB.noise_band(params, pos, src.astype(np.int64), dst.astype(np.int64), np.zeros((n, 100)), tgt, 5)
+    _bf16_check(z.reshape(-1), g, ref, band, "bf16 N=6 thresholded (band-probe shape)", loss)
+
+
+@pytest.mark.parametrize("T,N,fully", [(4, 32, True), (6, 24, False)])
+def test_bf16_receiver_block_plan_against_emulator(T, N, fully):
+    """bf16 math on a receiver-block plan (the plan HostPlan picks by itself for dense towers of more
+    than 16 nodes; its bf16 edge kernels are the one-hot ones): logits, loss and every gradient against
+    the bf16-operand emulator, inside the band of valid implementations."""
+    params = O.random_params(17)
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(T, N, seed=5, fully_connected=fully)
+    dense = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    rb = TowerBatch.from_edges(obj.reshape(-1, 3), dense.tower_nodes, dense.src, dense.dst, dense.tower_edges,
+                               prop.reshape(-1, 100), device="cuda", recv_blocks=True)
+    assert rb.flags == 1
+    z, loss, g = _train(P.to_flat(params, device="cuda"), rb, tgt, 5, "bf16")
+    e = np.array(O.dense_to_edges(Rs, Rr), np.int64).reshape(-1, 4)      # (tower, slot, sender, receiver)
+    src, dst = e[:, 0] * N + e[:, 2], e[:, 0] * N + e[:, 3]
+    ref, band = OB.noise_band(params, obj.reshape(-1, 3), src, dst, prop.reshape(-1, 100), tgt.reshape(-1), 5)
+    _bf16_check(z.reshape(-1), g, ref, band, f"bf16 receiver blocks T={T} N={N} fully={fully}", loss)
+
+
 def test_config3_bf16_full_size_against_emulator():
     """Config 3 in bf16 (65,536 fully connected 12-block towers, S = 5, training): a sampled 16-tower
     sub-batch's logits and gradients, and the full batch's logits of those towers, against the bf16
