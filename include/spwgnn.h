@@ -234,6 +234,11 @@ int32_t spwgnn_accumulate_out3(const float* out3, const double* weights3, double
 /* Sigmoid readout (Networks.py:93-96) for predict(): probs[i] = 1/(1+exp(-logits[i])). */
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream);
 
+/* dev[0, bytes) ← host[0, bytes) by a kernel on `stream` (not a DMA copy): `host` must be pinned,
+ * device-mapped memory (hipHostMalloc), both pointers 16-byte aligned, bytes a multiple of 16. A
+ * replayed small-batch step makes it its first node, so the batch upload rides inside the graph. */
+int32_t spwgnn_copy_in(const void* host, void* dev, int64_t bytes, spwgnn_stream_t stream);
+
 /* Per-tower readout over contiguous node ranges [tower_offsets[t], tower_offsets[t+1]):
  *   SUM_PROB   out[t] = Σ sigmoid(z)  — the stability sum of JengaBuilder.remove_to_demolish /
  *              TowerCreator.drop_to_demolish (JengaBuilder.py:252-256, TowerCreator.py:298-301),

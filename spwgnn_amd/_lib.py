@@ -79,6 +79,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_adam_lr_table": (i32, [f32, f32, f32, i32, vp]),
         "spwgnn_step_advance": (i32, [vp, vp, i32, C.c_uint64, i32, vp]),
         "spwgnn_sigmoid": (i32, [vp, vp, i64, vp]),
+        "spwgnn_copy_in": (i32, [vp, vp, i64, vp]),
         "spwgnn_accumulate_out3": (i32, [vp, vp, vp, vp]),
         "spwgnn_tower_readout": (i32, [vp, vp, i32, i32, vp, vp]),
     }

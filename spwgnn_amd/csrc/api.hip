@@ -1255,6 +1255,15 @@ int32_t spwgnn_accumulate_out3(const float* out3, const double* weights3, double
     return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
 }
 
+int32_t spwgnn_copy_in(const void* host, void* dev, int64_t bytes, spwgnn_stream_t stream) {
+    if (!host || !dev || bytes < 0 || bytes % 16 || reinterpret_cast<uintptr_t>(host) % 16 ||
+        reinterpret_cast<uintptr_t>(dev) % 16)
+        return SPWGNN_E_ARG;
+    if (bytes == 0) return SPWGNN_OK;
+    hipError_t e = launch_copy_in(host, dev, bytes / 16, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? SPWGNN_OK : (int32_t)e;
+}
+
 int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stream_t stream) {
     if (!logits || !probs || n < 1) return SPWGNN_E_ARG;
     hipError_t e = launch_sigmoid(logits, probs, n, static_cast<hipStream_t>(stream));

@@ -358,6 +358,7 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank, hipStream_t st);
 hipError_t launch_sigmoid(const float* z, float* p, int64_t n, hipStream_t st);
 hipError_t launch_accumulate_out3(const float* out3, const double* w, double* tot, hipStream_t st);
+hipError_t launch_copy_in(const void* src, void* dst, int64_t n16, hipStream_t st);
 hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers, int mode, float* out, hipStream_t st);
 
 // Team kernels (kernels_team.hip): one block per workgroup of waves that split each layer's output

@@ -1853,6 +1853,19 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
     hipLaunchKernelGGL(k_tower_readout, dim3((n_towers + 255) / 256), dim3(256), 0, st, z, off, n_towers, mode, out);
     return hipGetLastError();
 }
+// A replayed small-batch step's batch arrays, pinned (device-mapped) host staging → the static device
+// buffer, as the step's first kernel: the loads cross PCIe once, all in flight together (a few µs),
+// where a DMA copy between two replays left the GPU idle for ≈ 26 µs.
+__global__ __launch_bounds__(256) void k_copy_in(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+hipError_t launch_copy_in(const void* src, void* dst, int64_t n16, hipStream_t st) {
+    const int wgs = (int)std::min<int64_t>(64, (n16 + 1023) / 1024);   // ≤ 4 pieces per thread
+    hipLaunchKernelGGL(k_copy_in, dim3(std::max(wgs, 1)), dim3(256), 0, st, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), n16);
+    return hipGetLastError();
+}
+
 __global__ void k_accumulate_out3(const float* out3, const double* w, double* tot) {
     const int k = threadIdx.x;
     if (k < 3) tot[k] += (double)out3[k] * w[k];

@@ -221,6 +221,20 @@ def accumulate_out3(total3: torch.Tensor, out3: torch.Tensor, weights3: torch.Te
     _lib.check(st, "spwgnn_accumulate_out3")
 
 
+def copy_in(host: torch.Tensor, dev: torch.Tensor, nbytes: int, src_dev_ptr: Optional[int] = None) -> None:
+    """dev[:nbytes] ← host[:nbytes] by a kernel on the current stream (spwgnn_copy_in): `host` a pinned
+    (device-mapped) tensor, read at `src_dev_ptr` (its device address) when given. Captured into a
+    graph it is one kernel node, not a DMA copy."""
+    if not host.is_pinned():
+        raise ValueError("copy_in reads pinned host memory")
+    _require_gpu(dev, "copy_in destination")
+    if nbytes > host.numel() * host.element_size() or nbytes > dev.numel() * dev.element_size():
+        raise ValueError("copy_in beyond a buffer")
+    src = src_dev_ptr if src_dev_ptr is not None else host.data_ptr()
+    st = _lib.lib().spwgnn_copy_in(src, dev.data_ptr(), int(nbytes), _stream(dev.device))
+    _lib.check(st, "spwgnn_copy_in")
+
+
 def sigmoid(logits: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(logits)
     st = _lib.lib().spwgnn_sigmoid(logits.data_ptr(), out.data_ptr(), logits.numel(), _stream(logits.device))

@@ -11,8 +11,8 @@ DESIGN.md §3k). What a capture bakes in, and how it stays valid:
   every batch of B towers of N boxes has the same wave-tiles and blocks whatever its relations
   (unused capacity is padding, index −1, which matches no node);
 * addresses — the batch arrays and targets live in static device buffers that each step refills
-  with ONE pinned host→device copy before the replay; workspace, BCE scratch, logits, dlogits and
-  gradients belong to the step object;
+  from a pinned staging slot with its own first kernel (spwgnn_copy_in); workspace, BCE scratch,
+  logits, dlogits and gradients belong to the step object;
 * per-step scalars — the dropout key and the Adam step count are device words advanced by
   spwgnn_step_advance at the start of each step; lr_t comes from a host-built table
   (spwgnn_adam_lr_table, the expression spwgnn_adam evaluates).
@@ -67,8 +67,32 @@ class DeviceCounters:
             self.hyper = hyper
 
 
+_HIP = None
+
+
+def _mapped_device_ptr(host: torch.Tensor) -> int:
+    """The device address of a pinned host tensor (hipHostGetDevicePointer): kernels read it over
+    PCIe. Raises if the allocation is not device-mapped (the kernel would fault)."""
+    global _HIP
+    import ctypes as C
+    if _HIP is None:
+        _HIP = C.CDLL("libamdhip64.so")
+    p = C.c_void_p()
+    st = _HIP.hipHostGetDevicePointer(C.byref(p), C.c_void_p(host.data_ptr()), C.c_uint(0))
+    if st != 0 or not p.value:
+        raise _lib.SpwgnnError(f"pinned staging buffer is not device-mapped (hipHostGetDevicePointer {st})")
+    return int(p.value)
+
+
 class StaticBatch:
-    """A batch geometry's device arrays at fixed addresses, refilled per step in one copy."""
+    """A batch geometry's device arrays at fixed addresses, refilled per step from pinned staging.
+
+    Two pinned (device-mapped) staging slots: the host writes the next step's arrays into one while
+    the step that reads the other runs; `copy_in(slot)` moves a slot into the device buffer with one
+    kernel (spwgnn_copy_in) on the current stream — inside a captured step it is the graph's first
+    kernel node, so no copy sits between two replays."""
+
+    SLOTS = 2
 
     def __init__(self, plan: HostPlan, device):
         self.device = torch.device(device)
@@ -79,7 +103,7 @@ class StaticBatch:
             total += (a.nbytes + 15) // 16 * 16
         self.n_target = plan.n_nodes
         self.t_off = total
-        total += plan.n_nodes * 4
+        total += (plan.n_nodes * 4 + 15) // 16 * 16
         self.total = max(total, 16)
         self.buf = torch.zeros(self.total, dtype=torch.uint8, device=self.device)
         views = []
@@ -88,46 +112,50 @@ class StaticBatch:
             views.append(self.buf[o:o + a.nbytes].view(dt).view(a.shape))
         self.target = self.buf[self.t_off:self.t_off + 4 * plan.n_nodes].view(torch.float32)
         self.batch = TowerBatch.from_plan(plan, self.device, dev_arrays=views)
-        # pinned staging ring: a slot is refilled only after the copy that last read it has run
-        # (its event), so the host never waits on the step in flight and never allocates per step
-        self.ring = [torch.empty(self.total, dtype=torch.uint8, pin_memory=True) for _ in range(self.RING)]
-        self.ring_ev = [None] * self.RING
+        self.ring = [torch.zeros(self.total, dtype=torch.uint8, pin_memory=True) for _ in range(self.SLOTS)]
+        self.ring_dev = [_mapped_device_ptr(r) for r in self.ring]
         self.loads = 0
 
-    RING = 3
-
-    def load(self, plan: HostPlan, target: np.ndarray):
-        """This step's plan arrays and targets → the static buffers (one pinned staging slot, one
-        non-blocking copy on the current stream)."""
+    def fill(self, plan: HostPlan, target: np.ndarray, slot: int):
+        """This step's plan arrays and targets → pinned staging slot `slot` (host writes only: the
+        caller has made sure no step still reads that slot)."""
         if plan.geometry != self.geometry:
             raise ValueError("batch geometry differs from the captured one")
-        slot = self.loads % self.RING
-        self.loads += 1
-        if self.ring_ev[slot] is not None:
-            self.ring_ev[slot].synchronize()
-        host = self.ring[slot]
-        hv = host.numpy()
+        hv = self.ring[slot].numpy()
         for a, o in zip(plan.arrays, self.offsets):
             hv[o:o + a.nbytes] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
         t = np.ascontiguousarray(target, np.float32).reshape(-1)
         if t.size != self.n_target:
             raise ValueError("one target per node")
         hv[self.t_off:self.t_off + t.nbytes] = t.view(np.uint8)
-        self.buf.copy_(host, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self.ring_ev[slot] = ev
+        self.loads += 1
         # host-side copies the wrappers keep for reporting (edge ids, counts) follow the new batch
         b = self.batch
         b.tower_edges, b.src, b.dst, b.edge_id = plan.tower_edges, plan.src, plan.dst, plan.edge_id
         b.tower_nodes, b.node_shape = plan.tower_nodes, plan.node_shape
+
+    def copy_in(self, slot: int):
+        E.copy_in(self.ring[slot], self.buf, self.total, src_dev_ptr=self.ring_dev[slot])
+
+    def load(self, plan: HostPlan, target: np.ndarray):
+        """fill + copy_in through slot 0, synchronously ordered on the current stream (tools/tests)."""
+        torch.cuda.current_stream(self.device).synchronize()
+        self.fill(plan, target, 0)
+        self.copy_in(0)
 
 
 class ReplayStep:
     """One batch geometry's training step (forward, BCE, backward, Adam) as a replayed hipGraph.
 
     `body(batch, target, ws, bce, z, dz)` issues the step's launches on the current stream; it is
-    run eagerly on the first call (a real step) and captured right after, then replayed."""
+    run eagerly on the first call (a real step) and captured right after, then replayed.
+
+    The batch upload is part of the step: its first kernel copies a pinned staging slot into the
+    static device buffer (StaticBatch.copy_in). Two slots, one graph each: step i reads slot i mod 2,
+    and the host fills slot i mod 2 once step i − 2, its last reader, has finished — so the host
+    prepares a batch while the previous step runs, and the GPU never waits on a DMA copy between two
+    replays (that copy left it idle ≈ 26 µs per Keras-fit step at batch 32,
+    profiles/r04_fit_step_gaps.txt)."""
 
     def __init__(self, plan: HostPlan, device, body: Callable, graph: bool = True):
         self.static = StaticBatch(plan, device)
@@ -139,26 +167,44 @@ class ReplayStep:
         self.dz = torch.empty(n, dtype=torch.float32, device=self.device)
         self.body = body
         self.use_graph = graph
-        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graphs: list = [None] * StaticBatch.SLOTS
+        self.done: list = [None] * StaticBatch.SLOTS   # per slot: event after the last step that read it
+        self.calls = 0
         self.replays = 0
 
-    def _issue(self):
-        self.body(self.static.batch, self.static.target, self.ws, self.bce, self.z, self.dz)
+    @property
+    def graph(self) -> Optional[torch.cuda.CUDAGraph]:
+        return self.graphs[0]
+
+    def _issue(self, k: int):
+        st = self.static
+        st.copy_in(k)
+        self.body(st.batch, st.target, self.ws, self.bce, self.z, self.dz)
 
     def __call__(self, plan: HostPlan, target: np.ndarray):
-        self.static.load(plan, target)
-        if self.graph is not None:
-            self.graph.replay()
+        k = self.calls % StaticBatch.SLOTS
+        self.calls += 1
+        if self.done[k] is not None:
+            self.done[k].synchronize()
+        self.static.fill(plan, target, k)
+        cur = torch.cuda.current_stream(self.device)
+        if self.graphs[k] is not None:
+            self.graphs[k].replay()
             self.replays += 1
-            return
-        self._issue()
-        if self.use_graph:
-            g = torch.cuda.CUDAGraph()
-            # capture on torch's side stream; the eager step above already sized every buffer
-            torch.cuda.current_stream(self.device).synchronize()
-            with torch.cuda.graph(g):
-                self._issue()
-            self.graph = g
+        else:
+            self._issue(k)
+            if self.use_graph:
+                # capture on torch's side stream; the eager step above already sized every buffer.
+                # Every slot's graph now: a capture issues nothing, so the next call already replays
+                cur.synchronize()
+                for j in range(StaticBatch.SLOTS):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self._issue(j)
+                    self.graphs[j] = g
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self.done[k] = ev
 
 
 class ReplayCache:

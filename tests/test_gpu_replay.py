@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from oracle import model as O
-from spwgnn_amd import data as D, params as P
+from spwgnn_amd import data as D, engine as E, params as P
 from spwgnn_amd.batch import HostPlan, TowerBatch
 from spwgnn_amd.keras_api import CompactDataset, PropagationNetwork
 from spwgnn_amd.replay import ReplayStep
@@ -176,3 +176,18 @@ def test_capacity_plan_equals_compact_plan():
     assert np.all(np.abs(za - zb) <= 1e-5 + 1e-5 * np.abs(zb))
     for name, r in gb.items():
         assert np.abs(ga[name] - r).max() <= 1e-5 * np.abs(r).max() + 1e-7, name
+
+
+def test_copy_in_kernel_moves_pinned_bytes():
+    """spwgnn_copy_in (the replayed step's batch upload, one kernel): every byte of a pinned staging
+    buffer lands in the device buffer, and misaligned sizes are rejected."""
+    from spwgnn_amd.replay import _mapped_device_ptr
+    n = 48 * 1024 + 16
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    host.copy_(torch.from_numpy(np.random.default_rng(3).integers(0, 256, n, dtype=np.uint8)))
+    dev = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    E.copy_in(host, dev, n, src_dev_ptr=_mapped_device_ptr(host))
+    torch.cuda.synchronize()
+    assert torch.equal(dev.cpu(), host)
+    with pytest.raises(Exception):
+        E.copy_in(host, dev, n - 8)

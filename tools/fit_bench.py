@@ -8,7 +8,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from spwgnn_amd import data as D  # noqa: E402
 from spwgnn_amd.keras_api import PropagationNetwork  # noqa: E402
 
