@@ -141,12 +141,12 @@ __device__ __forceinline__ void store_b16(float* base, int64_t idx, float v) {
 constexpr int kM2Blk = 256;
 __device__ __forceinline__ void load_m2(const uint32_t* __restrict__ blk_words, int edge, uint32_t (&w)[5]) {
     const uint32_t* p = blk_words + edge * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint4 v = ld_nt_u4(p);   // streamed: each step's words are read once per kernel
     w[0] = v.x;
     w[1] = v.y;
     w[2] = v.z;
     w[3] = v.w;
-    w[4] = p[4];
+    w[4] = ld_nt_u1(p + 4);
 }
 // writer side: word (edge, t) lives in register (8·edge + t) >> 6, lane (8·edge + t) & 63 of the
 // four-register image that k_edge_fwd stores with one full-wave store per register

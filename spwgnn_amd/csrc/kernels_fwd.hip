@@ -972,9 +972,9 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         for (int c = 0; c < 2; ++c) {
             const int q = min(2 * kb + c, kKhE / 4 - 1);
             if constexpr (AB16)
-                r.a[c] = unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q));
+                r.a[c] = unpack4_bf16(ld_nt_u2(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q));
             else
-                r.a[c] = *reinterpret_cast<const float4*>(a.A + sr.ai + 256 * q);
+                r.a[c] = ld_nt_f4(a.A + sr.ai + 256 * q);
             r.u[c] = sr.U[64 * q];
             r.v[c] = sr.V[64 * q];
         }
@@ -1381,6 +1381,17 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
         return a.n16 ? hipErrorInvalidValue : launch_edge_fwd_team(a, math, st);   // team kernels: fp32 H2s
     if (a.n16 && (math != MATH_BF16 || a.nw_max > 16 || !a.a_b16)) return hipErrorInvalidValue;
     if (math == MATH_BF16 && a.n16) {
+#ifdef SPWGNN_DIAG   // byte attribution (wrong results): 1 A rows from 8 cached blocks, 3 U/V rows of the tile's first node
+        static const int ndbg = getenv("SPWGNN_EFWD_DBG") ? atoi(getenv("SPWGNN_EFWD_DBG")) : 0;
+        if (ndbg == 1) {
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 1, 1, true, false, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+            return hipGetLastError();
+        }
+        if (ndbg == 3) {
+            hipLaunchKernelGGL((k_edge_fwd_x6<true, 3, 1, true, false, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
+            return hipGetLastError();
+        }
+#endif
         hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1, true, false, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
         return hipGetLastError();
     }

@@ -656,8 +656,8 @@ __device__ __forceinline__ void w2grad_ws_body(const WgradArgs& a, int64_t blk_p
         load_m2(a.mask2 + ((int64_t)s * nblk + b) * kM2Blk, rr, mw);
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(ha + off[k]);
-            else R.a[k] = *reinterpret_cast<const float4*>(pa + off[k]);
+            if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(ha + off[k]);   // re-read by the
+            else R.a[k] = *reinterpret_cast<const float4*>(pa + off[k]);                // block's next steps
             R.u[k] = *reinterpret_cast<const float4*>(pu + off[k]);
             R.v[k] = *reinterpret_cast<const float4*>(pv + off[k]);
             R.g[k] = *reinterpret_cast<const float4*>(pg + off[k]);
