@@ -276,20 +276,54 @@ def cpu_time(cfg: dict, seconds: float, threads: int, form: str):
     return n_sample * n / el, f"{n_sample} towers x {n} iters, {el:.1f}s"
 
 
+def usable_cores():
+    """(cores this process can actually run on, affinity count, cgroup CPU quota or None): the affinity
+    set (len(os.sched_getaffinity(0))) capped by the cgroup's CPU quota (cpu.max) and by
+    OMP_NUM_THREADS when the environment declares its share that way. On a shared box the affinity
+    set lists the whole machine; oversubscribing torch's thread pool there made one run of the oracle
+    take minutes instead of seconds."""
+    aff = max(1, len(os.sched_getaffinity(0)))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, -(-int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:   # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, -(-q // per))
+        except (OSError, ValueError):
+            pass
+    cores = min(aff, quota) if quota else aff
+    # the box's declared share (gpurun sets OMP_NUM_THREADS to the CPUs a one-GPU job may use)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        cores = min(cores, int(env))
+    return cores, aff, quota
+
+
 def cpu_baseline(cfg: dict, seconds: float):
-    """SURVEY §8d / BASELINE.md CPU plan: the oracle on every host core this process may run on
-    (len(os.sched_getaffinity(0)); the reported value: the literal dense form Keras runs), its gather
-    form on the same cores, and beside them the dense form at 16 threads and at 1 thread."""
-    threads = max(1, len(os.sched_getaffinity(0)))
+    """SURVEY §8d / BASELINE.md CPU plan: the oracle on every host core this process can use (the
+    affinity set, capped by the cgroup's CPU quota; the reported value: the literal dense form Keras
+    runs), its gather form on the same cores, and beside them the dense form at 16 threads and at 1."""
+    threads, aff, quota = usable_cores()
+    print(f"cpu_baseline: {threads} threads (affinity {aff}, cgroup quota {quota})", file=sys.stderr, flush=True)
     dense, dsamp = cpu_time(cfg, seconds, threads, "dense")
+    print(f"cpu_baseline: dense {dense:.1f} towers/s", file=sys.stderr, flush=True)
     gather, gsamp = cpu_time(cfg, seconds / 2, threads, "gather")
     t16 = min(16, threads)
     d16, samp16 = (dense, dsamp) if t16 == threads else cpu_time(cfg, seconds / 2, t16, "dense")
     one, osamp = cpu_time(cfg, max(3.0, seconds / 4), 1, "dense")
     what = "fwd" if cfg["mode"] == "infer" else "fwd+bwd"
-    return {"value": round(dense, 1), "unit": "towers/s", "cores": threads, "kind": "port",
+    return {"value": round(dense, 1), "unit": "towers/s", "cores": threads, "affinity_cores": aff,
+            "cgroup_cpu_quota": quota, "kind": "port",
             "sample": f"oracle.forward_dense fp32 {what} ({dsamp}), N={cfg['nodes']}, S={cfg['S']}, "
-                      f"{cfg['relations']} relations, torch CPU threads={threads} (the affinity set); gather "
+                      f"{cfg['relations']} relations, torch CPU threads={threads} (affinity {aff}, cgroup quota {quota}); gather "
                       f"form {gather:.1f} towers/s ({gsamp}); dense at {t16} threads {d16:.1f} towers/s "
                       f"({samp16}); dense at 1 thread {one:.1f} towers/s ({osamp})",
             "value_gather": round(gather, 1), "value_16threads": round(d16, 1), "value_1thread": round(one, 1)}
