@@ -389,25 +389,72 @@ def step_hbm(config: int, ms_per_step: float, math: str, workload: str):
         return None
 
 
+# Algorithmic (compulsory) HBM bytes PER STEP of each timed kernel: every array it must read or write,
+# once, real rows and real features only (150-wide edge/node-message rows, 100-wide state rows; an
+# fp32 element is 4 B, a bf16-stored operand 2 B — bf16 math's §3g/§3o arrays), h1>0 / h2>0 words 19 B
+# per edge each. Not the measured traffic (`traffic`, PMC); the roofline picks the roof whose floor
+# (bytes ÷ 8 TB/s or FLOPs ÷ matrix peak) is the larger — the kernel's arithmetic intensity against
+# the ridge point.
+def kernel_bytes(kernel, Ne, Nn, S, math):
+    F, W, WN, MK = 4.0, 150, 100, 19.0
+    B = 2.0 if math == "bf16" else F          # operand-only arrays stored as bf16 in bf16 math
+    edge = {
+        "edge_fwd": S * (Ne * (W * B + 2 * MK) + Nn * (2 * W * F + (W + 1) * B)),
+        "edge_bwd": S * (Ne * 2 * MK + Nn * (W * F + 2 * W * B)),
+        "dA": Ne * (S * 2 * MK + W * B) + S * Nn * W * F,
+        "wgrad_w2": Ne * W * B + S * (Ne * 2 * MK + Nn * 3 * W * F),
+        "node_fwd": S * Nn * ((W + 1) * B + 2 * WN * F + WN * F + WN * B + WN * F + 2 * W * F),
+        "node_bwd": S * Nn * (2 * WN * F + WN * B + 2 * W * B + WN * B + W * F + 2 * WN * F + WN * B),
+        "enc_edge": Ne * (16 + 8 + 4 * W * B + 4 * MK),
+        "enc_edge_bwd": Ne * (W * B + 4 * MK + 4 * W * B),
+        "enc_node": Nn * (16 + WN * F + 2 * W * F + 2 * MK),
+        "enc_node_bwd": Nn * (S * WN * F + 3 * WN * F),
+        # the weight gradients' X and Y operands: rm.1 (X rebuilt from the 8-B d), rm.2, rm.3, W1a per
+        # edge; W1b, W1c, omp.0 P/a parts, omp.1, W3 per node·step; omp.0 c part and om.1 per node
+        "wgrad_ws": Ne * (8 + W * B + 3 * 2 * W * B) + S * Nn * (2 * (WN * F + W * B) + 2 * (WN * F + WN * F)
+                                                                  + 2 * WN * B + (W + 1) * B + WN * B)
+                    + Nn * (2 * WN * F + 8 + WN * F),
+    }
+    return edge.get(kernel)
+
+
 def roofline(kernel: str, kern_ms, launches_per_step, Ne, Nn, S, math, config, workload):
-    """A timed kernel's roofline: its algorithmic FLOPs per step ÷ its HIP-event time per step (the
-    mean launch time × launches per step), against the matrix peak of the math it runs in; every timed
-    kernel is fused GEMM work far above the ridge point, so the bound is the matrix pipe.
+    """A timed kernel's roofline. Both floors of one launch: its algorithmic FLOPs ÷ the matrix peak of
+    the math it runs in, and its algorithmic bytes (kernel_bytes) ÷ 8 TB/s; `bound` is the roof with
+    the larger floor (the kernel's arithmetic intensity against the ridge point), `achieved` the
+    algorithmic FLOP/s or B/s at the measured mean launch time (HIP events), `frac` = achieved / peak.
+    The fused small-batch launches are latency chains over L2-resident intermediates: matrix roof only.
     `traffic` = measured HBM bytes per launch from the committed PMC summary of the same workload
     (null if none)."""
     avg_ms = float(np.mean(kern_ms))
+    t = avg_ms * 1e-3
     fl_step = kernel_flops(kernel, Ne, Nn, S)
     kflops = fl_step / launches_per_step
-    achieved = kflops / (avg_ms * 1e-3) / 1e12
     mpeak = MATH_PEAK[math]
+    m_ach = kflops / t / 1e12
+    by_step = None if (_FUSED[0] and kernel in FUSED_PARTS) else kernel_bytes(kernel, Ne, Nn, S, math)
+    kbytes = by_step / launches_per_step if by_step else None
+    b_ach = kbytes / t / 1e9 if kbytes else None
     traffic = load_pmc(config, kernel, math, workload)
-    h_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(mpeak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / mpeak, 4), "traffic": traffic, "kernel": kernel,
-            "avg_launch_ms": round(avg_ms, 4), "launches": len(kern_ms), "launches_per_step": launches_per_step,
-            "ms_per_step": round(avg_ms * launches_per_step, 4), "flop_per_launch": kflops,
-            "hbm_gbs": round(h_gbs, 1) if h_gbs else None,
-            "hbm_frac": round(h_gbs / PEAK_HBM_GBS, 4) if h_gbs else None, "peak_note": PEAK_NOTE[math]}
+    h_gbs = traffic / t / 1e9 if traffic else None
+    hbm_bound = kbytes is not None and kbytes / (PEAK_HBM_GBS * 1e9) > kflops / (mpeak * 1e12)
+    out = {"bound": "hbm" if hbm_bound else "mfma",
+           "achieved": round(b_ach, 1) if hbm_bound else round(m_ach, 2),
+           "peak": PEAK_HBM_GBS if hbm_bound else round(mpeak, 1),
+           "unit": "GB/s" if hbm_bound else "TFLOP/s",
+           "frac": round(b_ach / PEAK_HBM_GBS, 4) if hbm_bound else round(m_ach / mpeak, 4),
+           "traffic": traffic, "kernel": kernel,
+           "avg_launch_ms": round(avg_ms, 4), "launches": len(kern_ms), "launches_per_step": launches_per_step,
+           "ms_per_step": round(avg_ms * launches_per_step, 4), "flop_per_launch": kflops,
+           "alg_bytes_per_launch": round(kbytes) if kbytes else None,
+           "intensity_flop_per_byte": round(kflops / kbytes, 1) if kbytes else None,
+           "ridge_flop_per_byte": round(mpeak * 1e12 / (PEAK_HBM_GBS * 1e9), 1),
+           "mfma_achieved_tflops": round(m_ach, 2), "mfma_frac": round(m_ach / mpeak, 4),
+           "alg_hbm_gbs": round(b_ach, 1) if b_ach else None,
+           "alg_hbm_frac": round(b_ach / PEAK_HBM_GBS, 4) if b_ach else None,
+           "hbm_gbs": round(h_gbs, 1) if h_gbs else None,
+           "hbm_frac": round(h_gbs / PEAK_HBM_GBS, 4) if h_gbs else None, "peak_note": PEAK_NOTE[math]}
+    return out
 
 
 def recorded_ms(ev, npairs):
@@ -700,7 +747,8 @@ def kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, config, wl, steps=2
             continue   # kernel not launched by this configuration / math
         r = roofline(name, ms, per_step, Ne, Nn, S, math, config, wl)
         table[name] = {"launches_per_step": per_step, "avg_launch_ms": r["avg_launch_ms"],
-                       "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
+                       "ms_per_step": r["ms_per_step"], "tflops": r["mfma_achieved_tflops"], "frac": r["mfma_frac"],
+                       "bound": r["bound"], "roof_frac": r["frac"], "alg_hbm_frac": r["alg_hbm_frac"],
                        "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
         if _FUSED[0] and name in FUSED_PARTS:
             table[name]["fused"] = "+".join(FUSED_PARTS[name])
@@ -774,7 +822,8 @@ def run_infer(args, cfg, world, rank, device):
         r = roofline(name, ms, len(ms) // 3, Ne, Nn, S, math, 5, wl)
         times[name] = ms
         table[name] = {"launches_per_step": len(ms) // 3, "avg_launch_ms": r["avg_launch_ms"],
-                       "ms_per_step": r["ms_per_step"], "tflops": r["achieved"], "frac": r["frac"],
+                       "ms_per_step": r["ms_per_step"], "tflops": r["mfma_achieved_tflops"], "frac": r["mfma_frac"],
+                       "bound": r["bound"], "roof_frac": r["frac"], "alg_hbm_frac": r["alg_hbm_frac"],
                        "traffic": r["traffic"], "hbm_gbs": r["hbm_gbs"]}
     kname = args.roofline_kernel or dominant(table)
     if kname not in times:

@@ -225,6 +225,29 @@ def test_bench_dominant_kernel_rule():
     assert bench.dominant({}) == "edge_fwd"
 
 
+def test_bench_roofline_bound_follows_intensity():
+    """The roofline's bound is the roof with the larger floor: the weight-gradient kernel (34 FLOP/B
+    at x6, ridge 52) is priced against HBM, the aggregate-gradient dA (162 FLOP/B) against the matrix
+    peak; the fused small-batch launches stay on the matrix roof; frac = achieved / peak either way."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    Ne, Nn, S = 1966080, 393216, 5
+    bench._FUSED[0] = False
+    r = bench.roofline("wgrad_ws", [4.5], 1, Ne, Nn, S, "x6", 0, "t")
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.PEAK_HBM_GBS
+    assert r["intensity_flop_per_byte"] < r["ridge_flop_per_byte"]
+    assert abs(r["frac"] - r["alg_bytes_per_launch"] / 4.5e-3 / 1e9 / bench.PEAK_HBM_GBS) < 1e-3
+    r = bench.roofline("dA", [2.0], 1, Ne, Nn, S, "x6", 0, "t")
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and r["frac"] == r["mfma_frac"]
+    bench._FUSED[0] = True
+    r = bench.roofline("wgrad_ws", [0.02], 1, 4000, 400, S, "x6", 1, "t")
+    assert r["bound"] == "mfma" and r["alg_bytes_per_launch"] is None
+    bench._FUSED[0] = False
+
+
 def test_plan_without_any_edge_and_empty_batch():
     """Single-box towers: no edge list at all (NULL src/dst through the C-ABI), one padding block
     per wave-tile; an empty batch is rejected before the library is called."""
