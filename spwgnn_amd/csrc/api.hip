@@ -99,7 +99,7 @@ static Ws make_ws(int64_t n_nodes, int64_t n_eblocks, int S, int training) {
         int64_t o = 0;
         for (int id = 0; id < X6_COUNT; ++id) {
             w.x6off[id] = o;
-            o += x6_chain_uint4(kX6Specs[id].nt_out, kX6Specs[id].nkb);
+            o += x6_chain_uint4(kX6Specs[id].nt_out, x6_nkb(kX6Specs[id]));
         }
         w.x6 = take(o * 4);
     }
@@ -351,8 +351,9 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
             X6Desc& d = xa.d[id];
             d.pack = sp.pack;
             d.nt_out = sp.nt_out;
-            d.nkb = sp.nkb;
+            d.nkb = x6_nkb(sp);
             d.kh = sp.kh;
+            d.ht = sp.ht;
             d.dst = w.x6off[id];
             // an image reads pack elements (k < rows, col < cols) only
             if ((sp.kh ? 2 * sp.kh : 16 * sp.nkb) > pack_rows(sp.pack) || 32 * sp.nt_out > pack_cols(sp.pack))
@@ -378,6 +379,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.w1c = c.pk(PK_W1C);
     if (r->math != MATH_F32) {
         en.x_om1 = c.x6(X6_OM1);
+        en.xh_om1 = c.x6(X6_OM1_H);
         en.x_w1b = c.x6(X6_W1B);
         en.x_w1c = c.x6(X6_W1C);
     }
@@ -484,6 +486,11 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
             nf.x_wo1a = c.x6(X6_WO1A);
             nf.x_wo1p = c.x6(X6_WO1P);
             nf.x_wo2 = c.x6(X6_WO2);
+            nf.xh_w3a = c.x6(X6_W3A_H);
+            nf.xh_wo1c = c.x6(X6_WO1C_H);
+            nf.xh_wo1a = c.x6(X6_WO1A_H);
+            nf.xh_wo1p = c.x6(X6_WO1P_H);
+            nf.xh_wo2 = c.x6(X6_WO2_H);
             nf.x_w1b = c.x6(X6_W1B);
             nf.x_w1c = c.x6(X6_W1C);
         }
@@ -794,6 +801,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             nb.x_wo1ct = c.x6(X6_WO1CT);
             nb.x_wo1at = c.x6(X6_WO1AT);
             nb.x_wo1pt = c.x6(X6_WO1PT);
+            nb.xh_w1bt = c.x6(X6_W1BT_H);
+            nb.xh_w1ct = c.x6(X6_W1CT_H);
+            nb.xh_wo2t = c.x6(X6_WO2T_H);
+            nb.xh_wo1ct = c.x6(X6_WO1CT_H);
+            nb.xh_wo1at = c.x6(X6_WO1AT_H);
+            nb.xh_wo1pt = c.x6(X6_WO1PT_H);
             nb.x_w3t = c.x6(X6_W3T);
         }
         nb.n16 = n16;
@@ -836,6 +849,8 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         if (r->math != MATH_F32) {
             tl.x_w1bt = c.x6(X6_W1BT);
             tl.x_w1ct = c.x6(X6_W1CT);
+            tl.xh_w1bt = c.x6(X6_W1BT_H);
+            tl.xh_w1ct = c.x6(X6_W1CT_H);
         }
         tl.n16 = n16;
     }
@@ -893,6 +908,8 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     if (kmath(r, kX6NodeBwd) != MATH_F32) {
         enb.x_wo1ct = c.x6(X6_WO1CT);
         enb.x_om1t = c.x6(X6_OM1T);
+        enb.xh_wo1ct = c.x6(X6_WO1CT_H);
+        enb.xh_om1t = c.x6(X6_OM1T_H);
     }
 
     if (bwd_fused_taken(r, b)) {

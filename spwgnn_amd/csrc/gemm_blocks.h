@@ -396,7 +396,70 @@ __device__ __forceinline__ void bias_act_rho(f32x16 (&X)[NT], const float* __res
 }
 
 constexpr int kX6Ring = 3;
+// SPWGNN_PAD_DBG (diagnosis builds, wrong results): 1 skips the MFMAs of the last output tile of every
+// 4-tile (100-wide) transposed product — the time the padding rows 100..127 cost
+#ifndef SPWGNN_PAD_DBG
+#define SPWGNN_PAD_DBG 0
+#endif
 // (the x6 edge kernels pick their wave counts per variant: kernels_fwd.hip / kernels_bwd.hip)
+
+// ---- half tile (HT): a 4-tile product's last tile (output rows 96..127, of which a
+// 100-wide layer uses 96..99) runs as two 16x16x32 MFMAs per k-block PAIR over rows 96..111 — one per
+// 16-node half of the column tile — instead of one 32x32x16 MFMA per k-block over 32 rows: half the
+// matrix cycles of that tile. B operands: one v_permlane16_swap per register of the pair's split
+// parts (lane group g = (k-block 2P + (g&1), lane half g>>1), the image's ht slot order). The two
+// 16x16 accumulators convert to and from rows 0..15 of the 32x32 C tile with permlane16 + permlane32
+// swaps (both involutions), so every caller keeps the 32x32 C layout; rows 16..31 stay untouched.
+template <int NC, int NT>
+__device__ __forceinline__ void ht_enter(const f32x16 (&out)[NC][NT], f32x4 (&q)[NC][2]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(out[c][3][r]), __float_as_uint(out[c][3][4 + r]), false, false);
+            const auto y = __builtin_amdgcn_permlane16_swap(x[0], x[1], false, false);
+            q[c][0][r] = __uint_as_float(y[0]);
+            q[c][1][r] = __uint_as_float(y[1]);
+        }
+}
+template <int NC, int NT>
+__device__ __forceinline__ void ht_leave(const f32x4 (&q)[NC][2], f32x16 (&out)[NC][NT]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(q[c][0][r]), __float_as_uint(q[c][1][r]), false, false);
+            const auto y = __builtin_amdgcn_permlane32_swap(x[0], x[1], false, false);
+            out[c][3][r] = __uint_as_float(y[0]);
+            out[c][3][4 + r] = __uint_as_float(y[1]);
+        }
+}
+// k-block pair (x0 = k-block 2P, x1 = 2P + 1 or absent) of column tile c into its two half accumulators
+template <int PARTS, int NC>
+__device__ __forceinline__ void ht_mfma(const bf16x8 (&a)[3], const uint32_t (&x0)[NC][3][4], const uint32_t (&x1)[NC][3][4],
+                                        bool has1, f32x4 (&q)[NC][2]) {
+    constexpr int LP = PARTS == 1 ? 1 : 3;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        bf16x8 b0[3], b1[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            uint32_t u0[4] = {0u, 0u, 0u, 0u}, u1[4] = {0u, 0u, 0u, 0u};
+            if (p < LP) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(x0[c][p][m], has1 ? x1[c][p][m] : 0u, false, false);
+                    u0[m] = r[0];
+                    u1[m] = r[1];
+                }
+            }
+            b0[p] = as_bf16x8(make_uint4(u0[0], u0[1], u0[2], u0[3]));
+            b1[p] = as_bf16x8(make_uint4(u1[0], u1[1], u1[2], u1[3]));
+        }
+        q[c][0] = mfma16_x6<PARTS>(a, b0, q[c][0]);
+        q[c][1] = mfma16_x6<PARTS>(a, b1, q[c][1]);
+    }
+}
 
 // ---- transposed orientation in split-bf16 math (x6), NC column tiles of 32 rows per wave:
 // out[c][T] += Wᵀ·B[c] over NKB k-blocks of 16. getb(c, kb, v) supplies the 8 fp32 B values of
@@ -404,24 +467,28 @@ constexpr int kX6Ring = 3;
 // (k_prep) holds, per step u = kb·NT_OUT + T, the three matching A-operand parts of lane (i, h),
 // 16 bytes each: [u][part][lane] uint4. Steps stream through a D-deep ring of static slots (fully
 // unrolled; the loads of step u + D issue before step u's MFMAs).
-template <int NT_OUT, int NKB, int NC, int D = kX6Ring, int PARTS = 3, class GetB>
+template <int NT_OUT, int NKB, int NC, int D = kX6Ring, int PARTS = 3, bool HT = false, class GetB>
 __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
                                          int lane) {
+    static_assert(!HT || NT_OUT == 4, "half tile: 4-tile products");
     constexpr int NS = NKB * NT_OUT, NP = 4 * NC;   // pair-splits per k-block
+    constexpr int SPD = HT ? 3 : 2;                 // split slots (HT: a pair's first k-block stays live)
     const uint4* wb = img + lane;
     uint4 ring[D][3];
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
         for (int p = 0; p < 3; ++p) ring[d][p] = wb[(d * 3 + p) * 64];
-    // split parts of k-block kb in slot kb & 1; the next k-block's pair-splits are spread over
+    // split parts of k-block kb in slot kb % SPD; the next k-block's pair-splits are spread over
     // this k-block's steps, so the VALU work interleaves with the MFMAs
-    uint32_t sp[2][NC][3][4];
+    uint32_t sp[SPD][NC][3][4];
+    f32x4 hq[NC][2];
+    if constexpr (HT) ht_enter(out, hq);
     auto split_pair = [&](int kb, int q) {
         const int c = q >> 2, m = q & 3;
         float v[8];
         getb(c, kb, v);
-        split2(v[2 * m], v[2 * m + 1], sp[kb & 1][c][0][m], sp[kb & 1][c][1][m], sp[kb & 1][c][2][m]);
+        split2(v[2 * m], v[2 * m + 1], sp[kb % SPD][c][0][m], sp[kb % SPD][c][1][m], sp[kb % SPD][c][2][m]);
     };
 #pragma unroll
     for (int q = 0; q < NP; ++q) split_pair(0, q);
@@ -433,7 +500,7 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
         for (int c = 0; c < NC; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                bq[c][p] = as_bf16x8(make_uint4(sp[kb & 1][c][p][0], sp[kb & 1][c][p][1], sp[kb & 1][c][p][2], sp[kb & 1][c][p][3]));
+                bq[c][p] = as_bf16x8(make_uint4(sp[kb % SPD][c][p][0], sp[kb % SPD][c][p][1], sp[kb % SPD][c][p][2], sp[kb % SPD][c][p][3]));
         bf16x8 a[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = as_bf16x8(ring[u % D][p]);
@@ -446,9 +513,17 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
             for (int q = NP * T / NT_OUT; q < NP * (T + 1) / NT_OUT; ++q) split_pair(kb + 1, q);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (HT) {
+            if (T == 3) {
+                if ((kb & 1) || kb == NKB - 1) ht_mfma<PARTS>(a, sp[(kb & ~1) % SPD], sp[kb % SPD], (kb & 1) != 0, hq);
+                continue;
+            }
+        }
+        if (SPWGNN_PAD_DBG && NT_OUT == 4 && T == 3) continue;   // diagnosis: the 100-wide layers' padding tile
 #pragma unroll
         for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6<PARTS>(a, bq[c], out[c][T]);
     }
+    if constexpr (HT) ht_leave(hq, out);
 }
 // ---- the same product with the weight image shared by the NW waves of a workgroup through LDS.
 // Every wave of the workgroup calls the same tgemm_x6_wg sequence (no early exit: a wave with no
@@ -472,9 +547,11 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-template <int NT_OUT, int NKB, int NC, int NW, int PARTS = 3, class GetB>
+template <int NT_OUT, int NKB, int NC, int NW, int PARTS = 3, bool HT = false, class GetB>
 __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img,
                                             int lane, const WgRing<NW>& wr) {
+    static_assert(!HT || NT_OUT == 4, "half tile: 4-tile products");
+    constexpr int SPD = HT ? 3 : 2;
     constexpr int LP = PARTS == 1 ? 1 : 3;    // parts held in LDS
     constexpr int KPS = PARTS == 1 ? 3 : 1;   // k-blocks per slice
     static_assert(KPS * NT_OUT * LP * 64 <= kWgSlot, "slot size");
@@ -501,12 +578,14 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
     asm volatile("" ::: "memory");  // no memory op moves below: the vmcnt counts below see only DMAs
 #pragma unroll
     for (int sl = 0; sl < R - 1 && sl < NSL; ++sl) issue(sl);
-    uint32_t sp[2][NC][3][4];
+    uint32_t sp[SPD][NC][3][4];
+    f32x4 hq[NC][2];
+    if constexpr (HT) ht_enter(out, hq);
     auto split_pair = [&](int kb, int q) {
         const int c = q >> 2, m = q & 3;
         float v[8];
         getb(c, kb, v);
-        split2(v[2 * m], v[2 * m + 1], sp[kb & 1][c][0][m], sp[kb & 1][c][1][m], sp[kb & 1][c][2][m]);
+        split2(v[2 * m], v[2 * m + 1], sp[kb % SPD][c][0][m], sp[kb % SPD][c][1][m], sp[kb % SPD][c][2][m]);
     };
 #pragma unroll
     for (int q = 0; q < NP; ++q) split_pair(0, q);
@@ -522,7 +601,7 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
         for (int c = 0; c < NC; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                bq[c][p] = as_bf16x8(make_uint4(sp[kb & 1][c][p][0], sp[kb & 1][c][p][1], sp[kb & 1][c][p][2], sp[kb & 1][c][p][3]));
+                bq[c][p] = as_bf16x8(make_uint4(sp[kb % SPD][c][p][0], sp[kb % SPD][c][p][1], sp[kb % SPD][c][p][2], sp[kb % SPD][c][p][3]));
         bf16x8 a[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = as_bf16x8(fr[u & 1][p]);
@@ -544,15 +623,23 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
             for (int q = NP * T / NT_OUT; q < NP * (T + 1) / NT_OUT; ++q) split_pair(kb + 1, q);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (HT) {
+            if (T == 3) {
+                if ((kb & 1) || kb == NKB - 1) ht_mfma<PARTS>(a, sp[(kb & ~1) % SPD], sp[kb % SPD], (kb & 1) != 0, hq);
+                continue;
+            }
+        }
+        if (SPWGNN_PAD_DBG && NT_OUT == 4 && T == 3) continue;
 #pragma unroll
         for (int c = 0; c < NC; ++c) out[c][T] = mfma32_x6<PARTS>(a, bq[c], out[c][T]);
     }
+    if constexpr (HT) ht_leave(hq, out);
 }
-template <int NT_OUT, int NKB, int NT_IN, int NC, int NW, int PARTS = 3>
+template <int NT_OUT, int NKB, int NT_IN, int NC, int NW, int PARTS = 3, bool HT = false>
 __device__ __forceinline__ void tchain_x6_wg(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
                                              const uint4* __restrict__ img, int lane, const WgRing<NW>& wr) {
     static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");
-    tgemm_x6_wg<NT_OUT, NKB, NC, NW, PARTS>(
+    tgemm_x6_wg<NT_OUT, NKB, NC, NW, PARTS, HT>(
         [&](int c, int kb, float (&v)[8]) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = in[c][kb >> 1][8 * (kb & 1) + e];
@@ -563,11 +650,11 @@ __device__ __forceinline__ void tchain_x6_wg(const f32x16 (&in)[NC][NT_IN], f32x
 // Chain layer: B = the C layout of the previous layer; k-block kb of tile t = kb>>1 is registers
 // 8(kb&1) .. +7 of in[c][t] (element e of lane half h = feature 16kb + 8(e>>2) + 4h + (e&3): image
 // kind X6_CHAIN).
-template <int NT_OUT, int NKB, int NT_IN, int NC, int D = kX6Ring, int PARTS = 3>
+template <int NT_OUT, int NKB, int NT_IN, int NC, int D = kX6Ring, int PARTS = 3, bool HT = false>
 __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
                                           const uint4* __restrict__ img, int lane) {
     static_assert(NKB <= 2 * NT_IN, "k-blocks beyond the input tiles");
-    tgemm_x6<NT_OUT, NKB, NC, D, PARTS>(
+    tgemm_x6<NT_OUT, NKB, NC, D, PARTS, HT>(
         [&](int c, int kb, float (&v)[8]) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = in[c][kb >> 1][8 * (kb & 1) + e];
@@ -577,18 +664,20 @@ __device__ __forceinline__ void tchain_x6(const f32x16 (&in)[NC][NT_IN], f32x16 
 
 // Kernels templated on the weight source: NW = 0 → each wave streams the image itself (tgemm_x6's
 // register ring, depth D), NW > 0 → the workgroup's shared LDS ring (tgemm_x6_wg).
-template <int NT_OUT, int NKB, int NC, int D, int PARTS, int NW, class GetB>
+// HT: the half-tile form (4-tile products on the ht images, kernels.h X6Desc)
+template <int NT_OUT, int NKB, int NC, int D, int PARTS, int NW, bool HT = false, class GetB>
 __device__ __forceinline__ void tgemm_x6s(GetB&& getb, f32x16 (&out)[NC][NT_OUT], const uint4* __restrict__ img, int lane,
                                           const WgRing<NW>& wr) {
-    if constexpr (NW > 0) tgemm_x6_wg<NT_OUT, NKB, NC, NW, PARTS>(getb, out, img, lane, wr);
-    else tgemm_x6<NT_OUT, NKB, NC, D, PARTS>(getb, out, img, lane);
+    if constexpr (NW > 0) tgemm_x6_wg<NT_OUT, NKB, NC, NW, PARTS, HT>(getb, out, img, lane, wr);
+    else tgemm_x6<NT_OUT, NKB, NC, D, PARTS, HT>(getb, out, img, lane);
 }
-template <int NT_OUT, int NKB, int NT_IN, int NC, int D, int PARTS, int NW>
+template <int NT_OUT, int NKB, int NT_IN, int NC, int D, int PARTS, int NW, bool HT = false>
 __device__ __forceinline__ void tchain_x6s(const f32x16 (&in)[NC][NT_IN], f32x16 (&out)[NC][NT_OUT],
                                            const uint4* __restrict__ img, int lane, const WgRing<NW>& wr) {
-    if constexpr (NW > 0) tchain_x6_wg<NT_OUT, NKB, NT_IN, NC, NW, PARTS>(in, out, img, lane, wr);
-    else tchain_x6<NT_OUT, NKB, NT_IN, NC, D, PARTS>(in, out, img, lane);
+    if constexpr (NW > 0) tchain_x6_wg<NT_OUT, NKB, NT_IN, NC, NW, PARTS, HT>(in, out, img, lane, wr);
+    else tchain_x6<NT_OUT, NKB, NT_IN, NC, D, PARTS, HT>(in, out, img, lane);
 }
+// the chain kernels' 4-tile products in the half-tile form: kHT (kernels.h, build flag SPWGNN_HT)
 
 // Half-row operand of tgemm_x6: lane half h of column tile c holds features KH·h .. KH·h + KH-1
 // of its row (chunk-major: chunk q of a 32-row block at + 256q), loaded whole up front.

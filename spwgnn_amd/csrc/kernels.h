@@ -27,6 +27,9 @@ struct PrepArgs {
 // element e of lane (i, h) = W[k(kb, e, h)][32T + i] with
 //   kh == 0 (chain: B is a C layout)          k = 16kb + 8(e>>2) + 4h + (e&3)
 //   kh > 0  (half rows: lane half h holds features kh·h ..)  k = kh·h + 8kb + e, zero if 8kb + e ≥ kh
+// ht (half tile, 4-tile images of the chain kernels): slot T = 3 of k-block kb holds,
+// when kb is odd or the last, the 16x16x32 A operand of k-block pair P = kb >> 1 for output columns
+// 96..111: lane (i, g) = W[k(2P + (g&1), e, g>>1)][96 + i] (zero for a k-block ≥ nkb), otherwise zeros
 enum X6Id : int {
     X6_RM1 = 0, X6_RM2, X6_RM3, X6_W1A,          // relation encoder (chains)
     X6_W1AT, X6_RM3T, X6_RM2T, X6_RM1T,           // its backward
@@ -35,10 +38,13 @@ enum X6Id : int {
     X6_W1BT, X6_W1CT, X6_WO2T, X6_WO1PT, X6_WO1CT, X6_WO1AT, X6_W3T,   // its backward
     X6_OM1,                                       // object encoder
     X6_OM1T,                                      // its backward
+    // half-tile forms of the 4-tile images (the chain kernels; the fused team kernels read the above)
+    X6_W3A_H, X6_WO1C_H, X6_WO1A_H, X6_WO1P_H, X6_WO2_H,
+    X6_W1BT_H, X6_W1CT_H, X6_WO2T_H, X6_WO1PT_H, X6_WO1CT_H, X6_WO1AT_H, X6_OM1_H, X6_OM1T_H,
     X6_COUNT
 };
-// (image, fp32 pack, output tiles, k-blocks, kh) — the images every x6 run builds
-struct X6Spec { int id, pack, nt_out, nkb, kh; };
+// (image, fp32 pack, output tiles, k-blocks, kh, ht) — the images every x6 run builds
+struct X6Spec { int id, pack, nt_out, nkb, kh, ht = 0; };
 constexpr X6Spec kX6Specs[X6_COUNT] = {
     {X6_RM1, PK_RM1, 5, 10, 0},    {X6_RM2, PK_RM2, 5, 10, 0},    {X6_RM3, PK_RM3, 5, 10, 0},
     {X6_W1A, PK_W1A, 5, 10, 0},    {X6_W1AT, PK_W1AT, 5, 10, kKhE}, {X6_RM3T, PK_RM3T, 5, 10, 0},
@@ -50,11 +56,23 @@ constexpr X6Spec kX6Specs[X6_COUNT] = {
     {X6_WO1PT, PK_WO1PT, 4, 7, 0}, {X6_WO1CT, PK_WO1CT, 4, 7, 0}, {X6_WO1AT, PK_WO1AT, 4, 7, 0},
     {X6_W3T, PK_W3T, 5, 7, 0},     {X6_OM1, PK_OM1, 4, 7, 0},
     {X6_OM1T, PK_OM1T, 4, 7, 0},
+    {X6_W3A_H, PK_W3A, 4, 10, kKhE, 1}, {X6_WO1C_H, PK_WO1C, 4, 7, kKhN, 1}, {X6_WO1A_H, PK_WO1A, 4, 7, 0, 1},
+    {X6_WO1P_H, PK_WO1P, 4, 7, kKhN, 1}, {X6_WO2_H, PK_WO2, 4, 7, 0, 1},
+    {X6_W1BT_H, PK_W1BT, 4, 10, kKhE, 1}, {X6_W1CT_H, PK_W1CT, 4, 10, kKhE, 1}, {X6_WO2T_H, PK_WO2T, 4, 7, 0, 1},
+    {X6_WO1PT_H, PK_WO1PT, 4, 7, 0, 1}, {X6_WO1CT_H, PK_WO1CT, 4, 7, 0, 1}, {X6_WO1AT_H, PK_WO1AT, 4, 7, 0, 1},
+    {X6_OM1_H, PK_OM1, 4, 7, 0, 1},     {X6_OM1T_H, PK_OM1T, 4, 7, 0, 1},
 };
+// The half-tile form is a build option (-DSPWGNN_HT=1): measured −0.5 % at the
+// headline, and it ends the bitwise equality of the chain and team kernels. Off, its images are empty.
+#ifndef SPWGNN_HT
+#define SPWGNN_HT 0
+#endif
+constexpr bool kHT = SPWGNN_HT != 0;
+inline int x6_nkb(const X6Spec& s) { return s.ht && !kHT ? 0 : s.nkb; }
 struct X6Desc {
     int32_t pack;       // source fp32 pack (PackId): element (k, col) of it
     int32_t nt_out, nkb;
-    int32_t kh;
+    int32_t kh, ht;
     int64_t dst;        // uint4 offset into the image buffer
 };
 struct PrepX6Args {
@@ -71,6 +89,7 @@ struct EncNodeArgs {
     const int32_t* node_local;
     const float *w_om0, *b_om0, *w_om1, *b_om1, *w1b, *w1c;
     const uint4 *x_om1, *x_w1b, *x_w1c;   // x6 images (x6 math)
+    const uint4* xh_om1;                  // its half-tile form (the chain kernel, §3w)
     float *zo1, *co, *P0, *U0, *V0;
     int dropout_on;
     uint32_t thresh;
@@ -128,6 +147,7 @@ struct NodeFwdArgs {
     float* cw_out;
     const float *w3a, *wo1c, *wo1a, *wo1p, *wo2, *w1b, *w1c, *bo1, *bo2p;
     const uint4 *x_w3a, *x_wo1c, *x_wo1a, *x_wo1p, *x_wo2, *x_w1b, *x_w1c;   // x6 images
+    const uint4 *xh_w3a, *xh_wo1c, *xh_wo1a, *xh_wo1p, *xh_wo2;            // half-tile forms (chain kernel, §3w)
     int n16;        // bf16 math (training, wide kernels): H2s read and o1 stored as bf16 (§3g, node side)
 };
 
@@ -143,6 +163,7 @@ struct NodeBwdArgs {
     int dco_sum;    // x6: no dco here; k_enc_node_bwd applies Wo1cᵀ once to Σ_s do1_s (linear)
     const float *w1bt, *w1ct, *wo2t, *wo1ct, *wo1at, *wo1pt, *w3t;
     const uint4 *x_w1bt, *x_w1ct, *x_wo2t, *x_wo1ct, *x_wo1at, *x_wo1pt, *x_w3t;   // x6 images
+    const uint4 *xh_w1bt, *xh_w1ct, *xh_wo2t, *xh_wo1ct, *xh_wo1at, *xh_wo1pt;      // half-tile forms (§3w)
     int n16;        // bf16 math (training, wide kernels): dU, dV, o1 read and dx, g stored as bf16 (§3g)
 };
 
@@ -196,6 +217,7 @@ struct EncNodeBwdArgs {
     float *dzo2, *dzo1;
     float scale;
     const uint4 *x_wo1ct, *x_om1t;    // split-bf16 maths: x6 images of Wo1cᵀ and om.1ᵀ
+    const uint4 *xh_wo1ct, *xh_om1t;  // their half-tile forms (the chain kernel, §3w)
 };
 
 // ---- weight gradients: dW = Σ_rows X[row]ᵀ·Y[row] (deterministic split-row slabs) ----

@@ -155,12 +155,12 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
         {
             HalfRowsT<kKhE, NC, N16> hr;
             hr.load_at(a.dU, off, lane);
-            tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, D, a.x_w1bt, lane, wr);
+            tgemm_x6s<4, 10, NC, kX6Ring, NP, NW, kHT>(hr, D, kHT ? a.xh_w1bt : a.x_w1bt, lane, wr);
         }
         {
             HalfRowsT<kKhE, NC, N16> hr;
             hr.load_at(a.dV, off, lane);
-            tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, D, a.x_w1ct, lane, wr);
+            tgemm_x6s<4, 10, NC, kX6Ring, NP, NW, kHT>(hr, D, kHT ? a.xh_w1ct : a.x_w1ct, lane, wr);
         }
     }
     if (a.tail) {  // dP0 = d/d 'propagation' (ld 100)
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
         }
     }
     zero2(G);
-    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(D, G, a.x_wo2t, lane, wr);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW, kHT>(D, G, kHT ? a.xh_wo2t : a.x_wo2t, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 O1[4];
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // P part of omp's input → dP_s
     zero2(D);
-    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(G, D, a.x_wo1pt, lane, wr);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW, kHT>(G, D, kHT ? a.xh_wo1pt : a.x_wo1pt, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 T[4];
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     // Wo1cᵀ is linear in do1 and runs once on Σ_s do1_s (k_enc_node_bwd)
     if (!a.dco_sum) {
         zero2(D);
-        tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(G, D, a.x_wo1ct, lane, wr);
+        tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW, kHT>(G, D, kHT ? a.xh_wo1ct : a.x_wo1ct, lane, wr);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             if (a.dco_accumulate) {
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_bwd_x6(NodeBwdArg
     }
     // effect part → g = da ⊙ (1 - a²) → G3 = g·W3ᵀ
     zero2(D);
-    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(G, D, a.x_wo1at, lane, wr);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW, kHT>(G, D, kHT ? a.xh_wo1at : a.x_wo1at, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         f32x16 Aa[4];
@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
     }
     if (has) store_cm<4>(a.dco + bN, E[0], lane, valid);
     zero_tiles(D[0]);
-    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW>(E, D, a.x_wo1ct, lane, wr);   // dc_o = (Σ_s do1_s)·Wo1cᵀ
+    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW, kHT>(E, D, kHT ? a.xh_wo1ct : a.x_wo1ct, lane, wr);   // dc_o = (Σ_s do1_s)·Wo1cᵀ
     load_cm<4>(a.co + bN, Z, lane);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_bwd_x6(EncNodeBwdArgs a) {
         for (int r = 0; r < 16; ++r) D[0][t][r] = Z[t][r] > 0.f ? D[0][t][r] * a.scale : 0.f;
     if (has) store_cm<4>(a.dzo2 + bN, D[0], lane, valid);
     zero_tiles(E[0]);
-    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW>(D, E, a.x_om1t, lane, wr);
+    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW, kHT>(D, E, kHT ? a.xh_om1t : a.x_om1t, lane, wr);
     if (a.zo1) {
         load_cm<4>(a.zo1 + bN, Z, lane);
     } else {   // the forward's own first-layer arithmetic (k_enc_node_x6), not a stored row

@@ -51,12 +51,16 @@ __global__ void k_prep(PrepArgs a, PrepX6Args x) {
     const int n = d.nkb * d.nt_out * 64;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
         const int lane = idx & 63, u = idx >> 6, kb = u / d.nt_out, T = u - kb * d.nt_out;
-        const int col = 32 * T + (lane & 31), h = lane >> 5;
+        // half-tile slot (kernels.h X6Desc ht): lane (i, g) of the 16x16x32 operand of k-block pair kb >> 1
+        const bool half = d.ht && T == 3;
+        const bool live = !half || (kb & 1) || kb == d.nkb - 1;
+        const int kbe = half ? (kb & ~1) + ((lane >> 4) & 1) : kb;
+        const int col = half ? 96 + (lane & 15) : 32 * T + (lane & 31), h = half ? lane >> 5 : lane >> 5;
         float w[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int k = d.kh ? d.kh * h + 8 * kb + e : 16 * kb + 8 * (e >> 2) + 4 * h + (e & 3);
-            const bool in = !d.kh || 8 * kb + e < d.kh;
+            const int k = d.kh ? d.kh * h + 8 * kbe + e : 16 * kbe + 8 * (e >> 2) + 4 * h + (e & 3);
+            const bool in = live && kbe < d.nkb && (!d.kh || 8 * kbe + e < d.kh);
             w[e] = in ? pack_elem(pd, a.params, k, col) : 0.f;
         }
         uint32_t hw[4], mw[4], lw[4];
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     const int64_t bN = (int64_t)nbk * kCmBlkN, bE = (int64_t)nbk * kCmBlk;   // chunk-major node blocks
     if (a.zo1 && has) store_cm<4>(a.zo1 + bN, Z[0], lane, valid);
     zero_tiles(C[0]);
-    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW>(Z, C, a.x_om1, lane, wr);
+    tchain_x6s<4, 7, 4, 1, kX6Ring, NP, NW, kHT>(Z, C, kHT ? a.xh_om1 : a.x_om1, lane, wr);
     bias_act_rho<4, true>(C[0], a.b_om1, h);  // relu(om(.)) — Networks.py:76
     if (a.dropout_on) {                       // Networks.py:78
         const uint32_t key = drop_row_key(run_seed(a), 2u, (uint32_t)a.node_tower[nc], (uint32_t)a.node_local[nc], 0xffffu);
@@ -700,7 +704,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
         for (int c = 0; c < NC; ++c) off[c] = bE(c);
         hr.load_at(a.H2s, off, lane);
-        tgemm_x6s<4, 10, NC, kX6Ring, NP, NW>(hr, E, a.x_w3a, lane, wr);
+        tgemm_x6s<4, 10, NC, kX6Ring, NP, NW, kHT>(hr, E, kHT ? a.xh_w3a : a.x_w3a, lane, wr);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -723,20 +727,20 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
 #pragma unroll
         for (int c = 0; c < NC; ++c) blk[c] = a.co + bN(c);
         hr.load(blk, lane);
-        tgemm_x6s<4, 7, NC, kX6Ring, NP, NW>(hr, O, a.x_wo1c, lane, wr);
+        tgemm_x6s<4, 7, NC, kX6Ring, NP, NW, kHT>(hr, O, kHT ? a.xh_wo1c : a.x_wo1c, lane, wr);
         if (a.cw_out)
 #pragma unroll
             for (int c = 0; c < NC; ++c)
                 if (has[c]) store_cm<4>(a.cw_out + bN(c), O[c], lane, true);
     }
-    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(E, O, a.x_wo1a, lane, wr);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW, kHT>(E, O, kHT ? a.xh_wo1a : a.x_wo1a, lane, wr);
     {
         HalfRows<kKhN, NC> hr;
         const float* blk[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) blk[c] = a.P + bN(c);
         hr.load(blk, lane);
-        tgemm_x6s<4, 7, NC, kX6Ring, NP, NW>(hr, O, a.x_wo1p, lane, wr);
+        tgemm_x6s<4, 7, NC, kX6Ring, NP, NW, kHT>(hr, O, kHT ? a.xh_wo1p : a.x_wo1p, lane, wr);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -749,7 +753,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
     // X reuses E's registers: x' = o1·Wo2' + b, then P' = tanh(x' + P) into E
     f32x16 (&X)[NC][4] = E;
     zero2(X);
-    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW>(O, X, a.x_wo2, lane, wr);
+    tchain_x6s<4, 7, 4, NC, kX6Ring, NP, NW, kHT>(O, X, kHT ? a.xh_wo2 : a.x_wo2, lane, wr);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         bias_act_rho<4, false>(X[c], a.bo2p, h);

@@ -485,3 +485,84 @@ def test_receiver_block_plan_invariants(N, thr):
     auto = TowerBatch.from_edges(dense.pos.numpy()[:, :3], dense.tower_nodes, dense.src, dense.dst, dense.tower_edges,
                                  device="cpu")
     assert (auto.flags == _lib.BATCH_RECV_BLOCKS) == (N > 16 and thr is None and N >= 27)
+
+
+def _swap16(x, y):
+    """v_permlane16_swap on 64-lane registers (lane axis 0): odd 16-lane rows of x <-> even rows of y."""
+    x2, y2 = x.copy(), y.copy()
+    for r in (0, 2):
+        x2[16 * (r + 1):16 * (r + 2)] = y[16 * r:16 * (r + 1)]
+        y2[16 * r:16 * (r + 1)] = x[16 * (r + 1):16 * (r + 2)]
+    return x2, y2
+
+
+def _swap32(x, y):
+    """v_permlane32_swap: upper 32 lanes of x <-> lower 32 lanes of y."""
+    x2, y2 = x.copy(), y.copy()
+    x2[32:], y2[:32] = y[:32], x[32:]
+    return x2, y2
+
+
+@pytest.mark.parametrize("kh,nkb", [(0, 7), (0, 8), (76, 10), (56, 7)])
+def test_half_tile_layout_algebra(kh, nkb):
+    """The half-tile products (gemm_blocks.h ht_*, k_prep's ht slots) restated lane by
+    lane in numpy: the 16x16x32 operands built by one permlane16 swap per k-block pair, multiplied
+    with the image's ht slot, and converted back to the 32x32 C layout give rows 96..111 of Wᵀ·B for
+    every node of the column tile (both k mappings: chain C layout and half rows)."""
+    rng = np.random.default_rng(kh + nkb)
+    K = 2 * kh if kh else 16 * nkb
+    W = rng.standard_normal((K, 128))
+    B = rng.standard_normal((K, 32))
+
+    def kidx(kb, h, e):
+        if kh:
+            return (kh * h + 8 * kb + e) if 8 * kb + e < kh else None
+        return 16 * kb + 8 * (e >> 2) + 4 * h + (e & 3)
+
+    def bop(kb):   # 32x32x16 B operand of k-block kb: [lane][e]
+        v = np.zeros((64, 8))
+        if kb >= nkb:
+            return v
+        for l in range(64):
+            for e in range(8):
+                k = kidx(kb, l >> 5, e)
+                v[l, e] = B[k, l & 31] if k is not None else 0.0
+        return v
+
+    def aop(P):    # the image's ht slot of pair P: lane (i, g) = W[k(2P + (g&1), g>>1, e)][96 + i]
+        a = np.zeros((64, 8))
+        for l in range(64):
+            i, g = l & 15, l >> 4
+            kb = 2 * P + (g & 1)
+            for e in range(8):
+                k = kidx(kb, g >> 1, e) if kb < nkb else None
+                a[l, e] = W[k, 96 + i] if k is not None else 0.0
+        return a
+
+    q = np.zeros((2, 64, 4))   # two 16x16 accumulators: lane (c, g) reg r = row 4g + r, node 16q + c
+    for P in range((nkb + 1) // 2):
+        b0, b1 = _swap16(bop(2 * P), bop(2 * P + 1))
+        a = aop(P)
+        for qi, bq in enumerate((b0, b1)):
+            for l in range(64):
+                c, g = l & 15, l >> 4
+                for r in range(4):
+                    i = 4 * g + r
+                    q[qi, l, r] += sum(a[i + 16 * gg] @ bq[c + 16 * gg] for gg in range(4))
+    out = np.zeros((64, 16))
+    for r in range(4):
+        x, y = _swap16(q[0, :, r], q[1, :, r])
+        lo, hi = _swap32(x, y)
+        out[:, r], out[:, 4 + r] = lo, hi
+    ref = W.T @ B                       # [128 features][32 nodes]
+    for l in range(64):
+        j, h = l & 31, l >> 5
+        for r in range(8):
+            f = 96 + (r & 3) + 8 * (r >> 2) + 4 * h
+            assert abs(out[l, r] - ref[f, j]) < 1e-9, (l, r)
+    # and the inverse conversion (ht_enter) restores the accumulators
+    q2 = np.zeros_like(q)
+    for r in range(4):
+        x, y = _swap32(out[:, r], out[:, 4 + r])
+        q2[0, :, r], q2[1, :, r] = _swap16(x, y)
+    assert np.array_equal(q2, q)
