@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 3   /* 3: spwgnn_batch.flags, receiver-block plans */
+#define SPWGNN_ABI_VERSION 4   /* 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -127,6 +127,22 @@ typedef struct spwgnn_batch {
     const uint8_t* blk_csr;     /* [n_eblocks][128]                                                */
 } spwgnn_batch;
 
+/* A replayed training step's first work, folded into the forward's first launch (spwgnn_run.prologue):
+ * the batch upload of spwgnn_copy_in (copy_bytes from copy_src — pinned, device-mapped — to copy_dst;
+ * both 16-byte aligned, copy_bytes a multiple of 16; 0 = none) and the key/step advance of
+ * spwgnn_step_advance (key NULL = none; mode SPWGNN_STEP_KEY_*). The same effects as those two calls
+ * issued before the forward, two launches fewer; the forward's own kernels run after them. */
+typedef struct spwgnn_prologue {
+    const void* copy_src;
+    void* copy_dst;
+    int64_t copy_bytes;
+    uint64_t* key;
+    int32_t* step;
+    int32_t mode;
+    int32_t rank;
+    uint64_t seed;
+} spwgnn_prologue;
+
 typedef struct spwgnn_run {
     int32_t mp_steps;   /* propagation steps; the reference hard-codes 5 (Networks.py:83)      */
     int32_t training;   /* 1: keep activations for backward + apply dropout                      */
@@ -143,6 +159,8 @@ typedef struct spwgnn_run {
      * run time instead of `seed`, so a captured step draws new masks on every replay once
      * spwgnn_step_advance has moved the key on. NULL = use `seed`. */
     const uint64_t* seed_dev;
+    /* spwgnn_forward only: work to run first (above); NULL = none. Read at call time. */
+    const spwgnn_prologue* prologue;
 } spwgnn_run;
 
 /* Matrix-product arithmetic. F32 and X6 give fp32-class results:

@@ -35,17 +35,25 @@ class BatchC(C.Structure):
     ]
 
 
+class PrologueC(C.Structure):
+    """spwgnn_prologue: a replayed step's batch upload and key/step advance, run by the forward's
+    first launch."""
+    _fields_ = [("copy_src", C.c_void_p), ("copy_dst", C.c_void_p), ("copy_bytes", C.c_int64),
+                ("key", C.c_void_p), ("step", C.c_void_p), ("mode", C.c_int32), ("rank", C.c_int32),
+                ("seed", C.c_uint64)]
+
+
 class RunC(C.Structure):
     _fields_ = [("mp_steps", C.c_int32), ("training", C.c_int32), ("dropout", C.c_float), ("math", C.c_int32),
                 ("seed", C.c_uint64), ("prof_kernel", C.c_int32), ("prof_count", C.c_int32),
-                ("prof_events", C.c_void_p), ("seed_dev", C.c_void_p)]
+                ("prof_events", C.c_void_p), ("seed_dev", C.c_void_p), ("prologue", C.c_void_p)]
 
 
 K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WGRAD_W2, K_DA = 1, 2, 3, 4, 5, 6, 7, 8
 K_WGRAD_WS, K_ENC_NODE, K_ENC_NODE_BWD = 9, 10, 11
 MATH_F32, MATH_X6, MATH_BF16 = 0, 1, 2
 STEP_KEY_COUNTER, STEP_KEY_SPLITMIX = 0, 1
-ABI_VERSION = 3        # SPWGNN_ABI_VERSION this binding's structs follow
+ABI_VERSION = 4        # SPWGNN_ABI_VERSION this binding's structs follow
 BATCH_RECV_BLOCKS = 1  # spwgnn_batch.flags: a receiver-block plan (spwgnn_plan_fill_recv)
 READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 

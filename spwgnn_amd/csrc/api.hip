@@ -346,7 +346,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     PrepX6Args xa{};
     if (r->math != MATH_F32) {
         xa.img = reinterpret_cast<uint4*>(c.f(w.x6));
-        for (int id = 0; id < X6_COUNT; ++id) {
+        for (int id = 0; id < X6_PREP_COUNT; ++id) {
             const X6Spec& sp = kX6Specs[id];
             X6Desc& d = xa.d[id];
             d.pack = sp.pack;
@@ -359,6 +359,21 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
             if ((sp.kh ? 2 * sp.kh : 16 * sp.nkb) > pack_rows(sp.pack) || 32 * sp.nt_out > pack_cols(sp.pack))
                 return SPWGNN_E_SHAPE;
         }
+    }
+    if (const spwgnn_prologue* p = r->prologue) {   // a replayed step's first work, in this launch
+        if (p->copy_bytes < 0 || p->copy_bytes % 16 || (p->copy_bytes && (!p->copy_src || !p->copy_dst)) ||
+            reinterpret_cast<uintptr_t>(p->copy_src) % 16 || reinterpret_cast<uintptr_t>(p->copy_dst) % 16 ||
+            (p->key && (!p->step || p->mode < SPWGNN_STEP_KEY_COUNTER || p->mode > SPWGNN_STEP_KEY_SPLITMIX)))
+            return SPWGNN_E_ARG;
+        pa.pro.src = static_cast<const uint4*>(p->copy_src);
+        pa.pro.dst = static_cast<uint4*>(p->copy_dst);
+        pa.pro.n16 = p->copy_bytes / 16;
+        pa.pro.key = p->key;
+        pa.pro.step = p->step;
+        pa.pro.mode = p->mode;
+        pa.pro.rank = p->rank;
+        pa.pro.seed = p->seed;
+        pa.pro_row = 1;
     }
     SPW_CHECK(launch_prep(pa, r->math != MATH_F32 ? &xa : nullptr, st));
     const bool drop = r->training && r->dropout > 0.f;

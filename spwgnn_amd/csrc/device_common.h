@@ -29,6 +29,30 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 }
 __device__ __forceinline__ constexpr int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Start of a replayable training step (one thread): the optimizer step count moves on and the
+// dropout key is derived for the new step — mode 0: key + 1 (the Keras front end's per-step seed
+// counter); mode 1: splitmix64 chain of (seed, iteration, rank, micro 0), Trainer.run_config's key.
+__device__ __forceinline__ uint64_t splitmix64_dev(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ void step_advance_dev(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank) {
+    const int32_t it = *step;
+    uint64_t k;
+    if (mode == 0) {
+        k = *key + 1ull;
+    } else {
+        k = splitmix64_dev(seed);
+        k = splitmix64_dev(k ^ (uint64_t)(int64_t)it);
+        k = splitmix64_dev(k ^ (uint64_t)(int64_t)rank);
+        k = splitmix64_dev(k ^ 0ull);
+    }
+    *key = k;
+    *step = it + 1;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Split-bf16 products ("x6" math). gfx950's bf16 MFMA runs 16× the f32 MFMA rate;
 // an fp32 operand x is split (round-to-nearest at each stage) into x = h + m + l + O(2^-25·|x|)

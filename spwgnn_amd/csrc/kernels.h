@@ -15,10 +15,24 @@ struct PackDesc {
     int32_t bias_row;  // ≥ 0: destination row filled from a bias vector (PK_W3A row 150 = rmp.2 bias)
     int64_t bias_off;  // floats into the flat params of that bias vector
 };
+// A replayed step's prologue folded into the prep launch (spwgnn_run.prologue): its last row of
+// workgroups copies the batch from pinned, device-mapped staging (as k_copy_in) and one thread
+// advances the dropout key and step words (as k_step_advance) — two launches fewer per step.
+struct PrologueArgs {
+    const uint4* src;
+    uint4* dst;
+    int64_t n16;        // 16-byte units to copy (0: none)
+    uint64_t* key;      // null: no advance
+    int32_t* step;
+    int32_t mode, rank;
+    uint64_t seed;
+};
 struct PrepArgs {
     const float* params;
     float* pk;
     PackDesc desc[PK_COUNT];  // by value (kernel-argument memory): no host→device copy, capturable
+    PrologueArgs pro;
+    int32_t pro_row;          // 1: the launch's last row of workgroups runs `pro`
 };
 
 // Split-bf16 (x6) operand images of the weights, built in the same launch as the fp32 packs (k_prep)
@@ -75,9 +89,11 @@ struct X6Desc {
     int32_t kh, ht;
     int64_t dst;        // uint4 offset into the image buffer
 };
+// the images k_prep builds: the half-tile forms only in kHT builds (kernel-argument space)
+constexpr int X6_PREP_COUNT = kHT ? X6_COUNT : X6_W3A_H;
 struct PrepX6Args {
     uint4* img;
-    X6Desc d[X6_COUNT];
+    X6Desc d[X6_PREP_COUNT];
 };
 inline int64_t x6_chain_uint4(int nt_out, int nkb) { return (int64_t)nkb * nt_out * 3 * 64; }
 

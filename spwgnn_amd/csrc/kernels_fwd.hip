@@ -29,6 +29,13 @@ __device__ __forceinline__ float pack_elem(const PackDesc& d, const float* __res
 // images need not wait for the packs.
 __global__ void k_prep(PrepArgs a, PrepX6Args x) {
     const int id = blockIdx.y;
+    if (a.pro_row && id == (int)gridDim.y - 1) {   // a replayed step's prologue (PrologueArgs)
+        const PrologueArgs& p = a.pro;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n16; i += (int64_t)gridDim.x * blockDim.x)
+            p.dst[i] = p.src[i];
+        if (p.key && blockIdx.x == 0 && threadIdx.x == 0) step_advance_dev(p.key, p.step, p.mode, p.seed, p.rank);
+        return;
+    }
     if (id < PK_COUNT) {
         const PackDesc& d = a.desc[id];
         const int total = d.rows * d.cols;
@@ -1336,7 +1343,8 @@ int edge_grid(int n_wtiles, int waves) {
 #define SPWGNN_PREP_GX 16
 #endif
 hipError_t launch_prep(const PrepArgs& a, const PrepX6Args* x, hipStream_t st) {
-    hipLaunchKernelGGL(k_prep, dim3(SPWGNN_PREP_GX, PK_COUNT + (x ? X6_COUNT : 0)), dim3(256), 0, st, a, x ? *x : PrepX6Args{});
+    const int rows = PK_COUNT + (x ? X6_PREP_COUNT : 0) + (a.pro_row ? 1 : 0);
+    hipLaunchKernelGGL(k_prep, dim3(SPWGNN_PREP_GX, rows), dim3(256), 0, st, a, x ? *x : PrepX6Args{});
     return hipGetLastError();
 }
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {

@@ -1483,29 +1483,9 @@ __global__ void k_adam(AdamArgs a) {
     }
 }
 
-// Start of a replayable training step (one thread): the optimizer step count moves on and the
-// dropout key is derived for the new step — mode 0: key + 1 (the Keras front end's per-step seed
-// counter); mode 1: splitmix64 chain of (seed, iteration, rank, micro 0), Trainer.run_config's key.
-__device__ __forceinline__ uint64_t splitmix64_dev(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
+// Start of a replayable training step (one thread, device_common.h step_advance_dev).
 __global__ void k_step_advance(uint64_t* key, int32_t* step, int mode, uint64_t seed, int32_t rank) {
-    if (threadIdx.x != 0) return;
-    const int32_t it = *step;
-    uint64_t k;
-    if (mode == 0) {
-        k = *key + 1ull;
-    } else {
-        k = splitmix64_dev(seed);
-        k = splitmix64_dev(k ^ (uint64_t)(int64_t)it);
-        k = splitmix64_dev(k ^ (uint64_t)(int64_t)rank);
-        k = splitmix64_dev(k ^ 0ull);
-    }
-    *key = k;
-    *step = it + 1;
+    if (threadIdx.x == 0) step_advance_dev(key, step, mode, seed, rank);
 }
 
 __global__ void k_sigmoid(const float* z, float* p, int64_t n) {

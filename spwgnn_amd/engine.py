@@ -6,6 +6,7 @@ arithmetic happens in libspwgnn_hip.so. Nothing here falls back to CPU.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Optional
@@ -31,6 +32,11 @@ def _require_gpu(t: torch.Tensor, what: str):
 MATH_MODES = {"f32": _lib.MATH_F32, "x6": _lib.MATH_X6, "bf16": _lib.MATH_BF16}
 
 
+# Replayed steps fold their batch upload and key/step advance into the forward's first launch
+# (spwgnn_run.prologue); SPWGNN_NO_PROLOGUE=1 issues them as launches of their own (A/B).
+FOLD_PROLOGUE = os.environ.get("SPWGNN_NO_PROLOGUE", "0") in ("", "0")
+
+
 @dataclass
 class RunConfig:
     mp_steps: int = REF_MP_STEPS
@@ -41,8 +47,9 @@ class RunConfig:
     prof_kernel: int = 0                 # SPWGNN_K_* to bracket with HIP events (bench only)
     prof_events: Optional[list] = None   # raw hipEvent_t handles, 2 per launch
     seed_dev: Optional[torch.Tensor] = None   # (1,) int64 device word holding the dropout key (replayable steps)
+    prologue: Optional["Prologue"] = None      # forward only: a replayed step's upload + key/step advance
 
-    def cstruct(self) -> _lib.RunC:
+    def cstruct(self, with_prologue: bool = False) -> _lib.RunC:
         r = _lib.RunC()
         r.mp_steps = int(self.mp_steps)
         r.training = 1 if self.training else 0
@@ -61,7 +68,42 @@ class RunConfig:
             if self.seed_dev.device.type != "cuda" or self.seed_dev.dtype != torch.int64:
                 raise ValueError("seed_dev must be a (1,) int64 device tensor")
             r.seed_dev = self.seed_dev.data_ptr()
+        if with_prologue and self.prologue is not None:   # spwgnn_forward only
+            self._pro_c = self.prologue.cstruct()   # keep alive for the call
+            r.prologue = C.cast(C.pointer(self._pro_c), C.c_void_p)
         return r
+
+
+@dataclass
+class Prologue:
+    """spwgnn_prologue (include/spwgnn.h): what a replayed step does before its forward, run by the
+    forward's first launch instead of two launches of its own — the batch upload (spwgnn_copy_in:
+    `nbytes` from the pinned, device-mapped `src_dev_ptr` into `dst`) and the key/step advance
+    (spwgnn_step_advance: `key`, `step` device words, `mode` STEP_KEY_*)."""
+    dst: Optional[torch.Tensor] = None
+    src_dev_ptr: int = 0
+    nbytes: int = 0
+    key: Optional[torch.Tensor] = None
+    step: Optional[torch.Tensor] = None
+    mode: int = _lib.STEP_KEY_COUNTER
+    seed: int = 0
+    rank: int = 0
+
+    def cstruct(self) -> _lib.PrologueC:
+        p = _lib.PrologueC()
+        if self.nbytes:
+            if self.dst is None or not self.src_dev_ptr:
+                raise ValueError("prologue copy needs dst and src_dev_ptr")
+            _require_gpu(self.dst, "prologue copy destination")
+            if self.nbytes > self.dst.numel() * self.dst.element_size():
+                raise ValueError("prologue copy beyond its destination")
+            p.copy_src, p.copy_dst, p.copy_bytes = int(self.src_dev_ptr), self.dst.data_ptr(), int(self.nbytes)
+        if self.key is not None:
+            if self.step is None:
+                raise ValueError("prologue advance needs key and step words")
+            p.key, p.step = self.key.data_ptr(), self.step.data_ptr()
+            p.mode, p.seed, p.rank = int(self.mode), int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(self.rank)
+        return p
 
 
 class Workspace:
@@ -121,7 +163,7 @@ def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Wo
     if logits is None:
         logits = torch.empty(batch.n_nodes, dtype=torch.float32, device=batch.device)
     b = batch.cstruct()
-    r = run.cstruct()
+    r = run.cstruct(with_prologue=True)
     st = _lib.lib().spwgnn_forward(flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(),
                                    logits.data_ptr(), _stream(batch.device))
     ws.fwd_key = Workspace.key(batch, run) if st == 0 else None

@@ -143,10 +143,16 @@ class KerasModel:
         read from the device, and the epoch sums accumulated on the device."""
         net, ctr = self.net, self._ctr
 
-        def body(batch, target, ws, bce, z, dz):
+        def body(batch, target, ws, bce, z, dz, pre=None):
             w3 = self._w3[batch.n_towers]        # created before the first (eager) run of a geometry
-            E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_COUNTER)
-            run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key)
+            # the key/step advance (and the replayed batch upload, `pre`) ride in the forward's first launch
+            pro = None
+            if E.FOLD_PROLOGUE:
+                pro = pre if pre is not None else E.Prologue()
+                pro.key, pro.step, pro.mode = ctr.key, ctr.step, _lib.STEP_KEY_COUNTER
+            else:
+                E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_COUNTER)
+            run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key, prologue=pro)
             E.forward(net.flat.data, batch, run, ws, logits=z)
             E.bce(z, target, bce, dlogits=dz, total3=self._tot, weights3=w3)   # loss + epoch sums, one launch
             E.backward(net.flat.data, batch, run, ws, dz, grads=self._grads)

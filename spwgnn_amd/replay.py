@@ -11,11 +11,12 @@ DESIGN.md §3k). What a capture bakes in, and how it stays valid:
   every batch of B towers of N boxes has the same wave-tiles and blocks whatever its relations
   (unused capacity is padding, index −1, which matches no node);
 * addresses — the batch arrays and targets live in static device buffers that each step refills
-  from a pinned staging slot with its own first kernel (spwgnn_copy_in); workspace, BCE scratch,
-  logits, dlogits and gradients belong to the step object;
-* per-step scalars — the dropout key and the Adam step count are device words advanced by
-  spwgnn_step_advance at the start of each step; lr_t comes from a host-built table
-  (spwgnn_adam_lr_table, the expression spwgnn_adam evaluates).
+  from a pinned staging slot inside its forward's first launch (spwgnn_run.prologue, for a body
+  that takes `pre`; otherwise a spwgnn_copy_in kernel of its own); workspace, BCE scratch, logits,
+  dlogits and gradients belong to the step object;
+* per-step scalars — the dropout key and the Adam step count are device words advanced at the
+  start of each step (the same prologue, or spwgnn_step_advance); lr_t comes from a host-built
+  table (spwgnn_adam_lr_table, the expression spwgnn_adam evaluates).
 
 The first call of a geometry runs the step eagerly (a real step), then captures it; `graph=False`
 runs the identical launch sequence eagerly every time, so replayed and eager training agree bit
@@ -23,6 +24,7 @@ for bit (tests/test_gpu_replay.py).
 """
 from __future__ import annotations
 
+import inspect
 from typing import Callable, Dict, Optional
 
 import numpy as np
@@ -166,6 +168,8 @@ class ReplayStep:
         self.z = torch.empty(n, dtype=torch.float32, device=self.device)
         self.dz = torch.empty(n, dtype=torch.float32, device=self.device)
         self.body = body
+        # a body taking `pre` gets the upload as a prologue of its forward's first launch
+        self.fold = E.FOLD_PROLOGUE and "pre" in inspect.signature(body).parameters
         self.use_graph = graph
         self.graphs: list = [None] * StaticBatch.SLOTS
         self.done: list = [None] * StaticBatch.SLOTS   # per slot: event after the last step that read it
@@ -178,8 +182,12 @@ class ReplayStep:
 
     def _issue(self, k: int):
         st = self.static
-        st.copy_in(k)
-        self.body(st.batch, st.target, self.ws, self.bce, self.z, self.dz)
+        if self.fold:   # the body's forward runs the upload in its first launch (spwgnn_run.prologue)
+            pre = E.Prologue(dst=st.buf, src_dev_ptr=st.ring_dev[k], nbytes=st.total)
+            self.body(st.batch, st.target, self.ws, self.bce, self.z, self.dz, pre=pre)
+        else:
+            st.copy_in(k)
+            self.body(st.batch, st.target, self.ws, self.bce, self.z, self.dz)
 
     def __call__(self, plan: HostPlan, target: np.ndarray):
         k = self.calls % StaticBatch.SLOTS

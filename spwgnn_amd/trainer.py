@@ -135,9 +135,16 @@ class Trainer:
         w = n_nodes / (n_global or n_nodes)
         grads = torch.empty_like(self.params)
 
-        def body(batch, target, ws, bce, z, dz):
-            E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_SPLITMIX, self.seed, self.rank)
-            run = E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, math=self.math, seed_dev=ctr.key)
+        def body(batch, target, ws, bce, z, dz, pre=None):
+            # the key/step advance (and the replayed batch upload, `pre`) ride in the forward's first launch
+            pro = None
+            if E.FOLD_PROLOGUE:
+                pro = pre if pre is not None else E.Prologue()
+                pro.key, pro.step, pro.mode, pro.seed, pro.rank = ctr.key, ctr.step, _lib.STEP_KEY_SPLITMIX, self.seed, self.rank
+            else:
+                E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_SPLITMIX, self.seed, self.rank)
+            run = E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, math=self.math, seed_dev=ctr.key,
+                              prologue=pro)
             E.forward(self.params, batch, run, ws, logits=z)
             out3, _ = E.bce(z, target, bce, dlogits=dz)
             E.backward(self.params, batch, run, ws, dz, grads=grads)

@@ -191,3 +191,41 @@ def test_copy_in_kernel_moves_pinned_bytes():
     assert torch.equal(dev.cpu(), host)
     with pytest.raises(Exception):
         E.copy_in(host, dev, n - 8)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_forward_prologue_equals_separate_launches(mode):
+    """spwgnn_run.prologue (a replayed step's batch upload and key/step advance inside the forward's
+    first launch) has the effects of spwgnn_copy_in + spwgnn_step_advance issued before the forward:
+    the same bytes land, the key and step words move on alike, and the forward that reads the key
+    (dropout) gives the same logits bit for bit."""
+    from spwgnn_amd.replay import _mapped_device_ptr
+    params = P.to_flat(O.random_params(9), device="cuda")
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(24, 6, seed=4, fully_connected=False)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    n = 20 * 1024 + 48
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    host.copy_(torch.from_numpy(np.random.default_rng(5).integers(0, 256, n, dtype=np.uint8)))
+    out = []
+    for folded in (False, True):
+        key = torch.tensor([12345], dtype=torch.int64, device="cuda")
+        step = torch.tensor([7], dtype=torch.int32, device="cuda")
+        dev = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        ws = E.Workspace("cuda")
+        run = E.RunConfig(3, training=True, dropout=0.1, seed_dev=key)
+        if folded:
+            run.prologue = E.Prologue(dst=dev, src_dev_ptr=_mapped_device_ptr(host), nbytes=n, key=key, step=step,
+                                      mode=mode, seed=99, rank=1)
+        else:
+            E.copy_in(host, dev, n, src_dev_ptr=_mapped_device_ptr(host))
+            E.step_advance(key, step, mode, 99, 1)
+        z = E.forward(params, batch, run, ws)
+        torch.cuda.synchronize()
+        out.append((dev.cpu(), int(key.item()), int(step.item()), z.cpu()))
+    (d0, k0, s0, z0), (d1, k1, s1, z1) = out
+    assert torch.equal(d0, host) and torch.equal(d1, host)
+    assert (k0, s0) == (k1, s1) and s1 == 8 and k1 != 12345
+    assert torch.equal(z0, z1)
+    with pytest.raises(Exception):   # misaligned size
+        bad = E.RunConfig(3, training=True, prologue=E.Prologue(dst=dev, src_dev_ptr=_mapped_device_ptr(host), nbytes=n - 8))
+        E.forward(params, batch, bad, E.Workspace("cuda"))
