@@ -510,6 +510,9 @@ def main():
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the other-math reference measurements")
     ap.add_argument("--no-kernel-table", action="store_true", help="skip the per-kernel roofline table")
     ap.add_argument("--infer", action="store_true", help="alias of --config 5")
+    ap.add_argument("--graph", action="store_true",
+                    help="small-batch configs: replay each step as one captured hipGraph instead of issuing its "
+                         "launches (the same sequence) eagerly — slower on the MI355X host (DESIGN.md §3x)")
     ap.add_argument("--buckets", type=int, default=1,
                     help="N>1: the flat gradient all-reduced as this many async pieces")
     args = ap.parse_args()
@@ -677,16 +680,18 @@ def run_train(args, cfg, world, rank, device):
 
 
 def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
-    """A launch-bound config (config 1: the reference's own 32-tower batch) timed as it should run:
-    each step one replayed hipGraph (spwgnn_amd/replay.py) after one pinned copy of the step's batch
-    arrays into the graph's static buffers. The batch is planned with every relation slot (N(N−1)
-    per tower); the kernel table and roofline come from eager steps of the same trainer (HIP events
-    cannot time launches inside a replayed graph)."""
+    """A launch-bound config (config 1: the reference's own 32-tower batch) timed as it should run: the
+    replayable step of spwgnn_amd/replay.py — static device buffers refilled from a pinned staging
+    slot by the step's first launch, the dropout key and Adam step as device words — issued eagerly
+    (the host keeps ahead of the GPU; `--graph` replays the same step as one captured hipGraph,
+    ≈ 4 µs slower per step on the MI355X host). The batch is planned with every
+    relation slot (N(N−1) per tower); the kernel table and roofline come from eager steps of the same
+    trainer."""
     from spwgnn_amd.replay import ReplayStep
     S, math = cfg["S"], cfg["math"]
     plans, tg_np, n_global = make_workload(cfg, rank, device, 1, plans=True)
     plan, tgt = plans[0], tg_np[0]
-    rs = ReplayStep(plan, device, trainer.replay_body(plan.n_nodes, n_global))
+    rs = ReplayStep(plan, device, trainer.replay_body(plan.n_nodes, n_global), graph=args.graph)
     for _ in range(args.warmup + 1):             # the first call runs eagerly and captures
         trainer.replay_step(rs, plan, tgt)
     torch.cuda.synchronize()
@@ -708,7 +713,9 @@ def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
         "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16" if math == "bf16" else "f32", "math": MATH_DESC[math],
         "data": "synthetic (Jenga-geometry towers, random labels, glorot weights)",
-        "config": {"workload": wl, "step_mode": "each step one replayed hipGraph (batch arrays copied in per step)",
+        "config": {"workload": wl, "step_mode": ("each step one replayed hipGraph (batch arrays copied in by its first launch)"
+                                                  if args.graph else "each step's launches issued eagerly from static buffers "
+                                                  "(batch arrays copied in by its first launch; --graph: the same step replayed)"),
                    "baseline_config": args.config, "towers_per_gpu": cfg["towers"], "global_batch": cfg["towers"],
                    "nodes_per_tower": cfg["nodes"], "nodes_per_gpu": Nn, "edges_per_gpu": Ne, "mp_steps": S,
                    "math": math, "parallelism": "dp1", "replays": rs.replays, "eblocks_planned": plan.n_eblocks},

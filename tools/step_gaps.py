@@ -1,5 +1,6 @@
 """Per-step kernel time vs wall time from a rocprofv3 --kernel-trace CSV of tools/fit_bench.py:
-splits the trace at each k_step_advance (one per fit step) and prints the median busy time per step
+splits the trace at each step's first kernel (k_step_advance, or k_prep when the replayed step folds
+its upload and key advance into the forward's first launch, spwgnn_run.prologue) and prints the median busy time per step
 (union of kernel intervals), the median wall time from one step's first kernel start to the next
 one's, the idle difference, and the median gap between consecutive launches.
 usage: python tools/step_gaps.py TRACE_DIR"""
@@ -15,7 +16,8 @@ with open(path) as f:
     for r in csv.DictReader(f):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
 rows.sort()
-starts = [i for i, r in enumerate(rows) if "k_step_advance" in r[2]]
+marker = "k_step_advance" if any("k_step_advance" in r[2] for r in rows) else "k_prep"
+starts = [i for i, r in enumerate(rows) if marker in r[2]]
 steps = [rows[a:b] for a, b in zip(starts, starts[1:])]
 busy, wall, gaps = [], [], []
 for s, nxt in zip(steps, steps[1:]):
