@@ -1141,6 +1141,11 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             b0r[k] = ok ? *reinterpret_cast<const float4*>(a.b0 + f) : f4zero();
         }
     }
+    // the stage (s, nb) of the next fetch, advanced by one per call: fetch runs t = 0, 1, 2, … in order
+    // and the tail re-fetches stage T − 1. (A 64-bit division per stage was ≈ 130 scalar instructions
+    // in the staging wave's stream.)
+    int64_t fs = t0 / a.nbs, fnb = t0 - fs * a.nbs;
+    int fdone = 0;
     auto fetch = [&](int t, WsSet4& R) {
         if constexpr (DBG == 1 || DBG == 6) {   // diagnosis: no global loads
             const float c = (float)(rr + t);
@@ -1152,8 +1157,14 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             for (int k = 0; k < W::NKY; ++k) R.y[k] = make_float4(c, c - 1.f, c - 2.f, c - 3.f);
             return;
         }
-        const int64_t tg = t0 + (t < T ? t : T - 1);
-        const int64_t s = tg / a.nbs, nb = tg - s * a.nbs;
+        const int64_t s = fs, nb = fnb;   // stage t0 + min(t, T − 1)
+        if (fdone < T - 1) {
+            ++fdone;
+            if (++fnb == a.nbs) {
+                fnb = 0;
+                ++fs;
+            }
+        }
         if (MASK) R.nvalid = (int)min<int64_t>(32, a.count - nb * 32);
         const int64_t ix = (s * a.x_sb + nb) * (W::KHX * 64) + rr * 4;   // element indices
         const int64_t iy = YROW ? ((s * a.y_sb + nb) * 32 + yr) * 160 : (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
