@@ -1003,6 +1003,7 @@ struct WsStage {
 };
 struct WsSet4 {
     float4 x[5], y[5];
+    uint2 xh[5], yh[5];   // bf16-stored operands in bf16 math: the raw element pairs (no unpack)
     float2 d;
     int nvalid;
 };
@@ -1026,6 +1027,11 @@ struct WsSet4 {
 template <int KXP, int NYP, int YROW, bool MASK, int NP, int XD, int B16>
 __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* smem) {
     constexpr int DBG = SPWGNN_WS_DBG;
+    // bf16 math over bf16-stored operands: the stored element pairs ARE the h parts of the image
+    // (rounding an exactly representable value is the identity), so they go to LDS as loaded — no
+    // unpack, mask select or re-pack per element on the staging wave's VALU stream
+    constexpr bool kRawX = NP == 1 && (B16 & kB16X) && XD == 0 && DBG == 0;
+    constexpr bool kRawY = NP == 1 && (B16 & kB16Y) && DBG == 0;
     using W = WsStage<KXP, NYP, YROW, MASK>;
     using IX = X6Img<KXP>;
     using IY = X6Img<NYP>;
@@ -1182,14 +1188,18 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             R.d = make_float2(p.y, p.z);   // Networks.py:65-71: (y, width)
         } else {
 #pragma unroll
-            for (int k = 0; k < W::NKX; ++k)
-                R.x[k] = (B16 & kB16X) ? unpack4_bf16(*reinterpret_cast<const uint2*>(hx + offx[k]))
-                                       : *reinterpret_cast<const float4*>(px + offx[k]);
+            for (int k = 0; k < W::NKX; ++k) {
+                if constexpr (kRawX) R.xh[k] = *reinterpret_cast<const uint2*>(hx + offx[k]);
+                else if constexpr (B16 & kB16X) R.x[k] = unpack4_bf16(*reinterpret_cast<const uint2*>(hx + offx[k]));
+                else R.x[k] = *reinterpret_cast<const float4*>(px + offx[k]);
+            }
         }
 #pragma unroll
-        for (int k = 0; k < W::NKY; ++k)
-            R.y[k] = (B16 & kB16Y) ? unpack4_bf16(*reinterpret_cast<const uint2*>(hy + offy[k]))
-                                   : *reinterpret_cast<const float4*>(py + offy[k]);
+        for (int k = 0; k < W::NKY; ++k) {
+            if constexpr (kRawY) R.yh[k] = *reinterpret_cast<const uint2*>(hy + offy[k]);
+            else if constexpr (B16 & kB16Y) R.y[k] = unpack4_bf16(*reinterpret_cast<const uint2*>(hy + offy[k]));
+            else R.y[k] = *reinterpret_cast<const float4*>(py + offy[k]);
+        }
     };
     uint32_t dbg_sink = 0u;
     // diagnosis forms of the image writes: raw bits into the parts (no split), or no LDS writes
@@ -1230,6 +1240,17 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
 #pragma unroll
         for (int k = 0; k < W::NKX; ++k) {
             if (!xk_ok(k)) break;
+            if constexpr (kRawX) {
+                uint2 u = R.xh[k];
+                if (MASK && !xin) u = make_uint2(0u, 0u);
+                if (k == ones_k) {   // the bias' ones column: bf16 1.0 = 0x3f80 in half ones_c
+                    uint32_t& w = (ones_c >> 1) ? u.y : u.x;
+                    const int sh = 16 * (ones_c & 1);
+                    w = (w & ~(0xffffu << sh)) | ((xin ? 0x3f80u : 0u) << sh);
+                }
+                *reinterpret_cast<uint2*>(Xs + IX::woff(rr, c0 + 8 * k)) = u;
+                continue;
+            }
             float4 v;
             if (XD) {
                 v.x = relu(dense2(R.d.x, R.d.y, w0r[k].x, w1r[k].x, b0r[k].x));
@@ -1246,6 +1267,12 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
 #pragma unroll
         for (int k = 0; k < W::NKY; ++k) {
             if (!yk_ok(k)) break;
+            if constexpr (kRawY) {
+                uint2 u = R.yh[k];
+                if (MASK && !yin) u = make_uint2(0u, 0u);
+                *reinterpret_cast<uint2*>(Ys + IY::woff(yr, yc0 + 8 * k)) = u;
+                continue;
+            }
             float4 v = R.y[k];
             if (MASK && !yin) v = f4zero();
             puty(Ys, yr, yc0 + 8 * k, v);
