@@ -1233,17 +1233,22 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             IY::template put<NP>(S, row, c4, v);
         }
     };
-    auto build = [&](const WsSet4& R, char* Xs) {
-        if constexpr (DBG == 6) return;
+    // the bias' ones column: its group slot is wave-uniform (a scalar branch per slot), its lane set
+    // is not — one select per stage instead of one per slot and component
+    const int ones_kk = a.x_ones >= 0 ? (a.x_ones >> 5) : -1;
+    const bool ones_lane = ones_k >= 0;
+    // row masks only on a job's last, partial row block (wave-uniform): full stages take no selects
+    auto build_m = [&](const WsSet4& R, char* Xs, auto Mc) {
+        constexpr bool M = MASK && decltype(Mc)::value;
         char* Ys = Xs + W::IMX;
-        const bool xin = !MASK || rr < R.nvalid, yin = !MASK || yr < R.nvalid;
+        const bool xin = !M || rr < R.nvalid, yin = !M || yr < R.nvalid;
 #pragma unroll
         for (int k = 0; k < W::NKX; ++k) {
             if (!xk_ok(k)) break;
             if constexpr (kRawX) {
                 uint2 u = R.xh[k];
-                if (MASK && !xin) u = make_uint2(0u, 0u);
-                if (k == ones_k) {   // the bias' ones column: bf16 1.0 = 0x3f80 in half ones_c
+                if (M && !xin) u = make_uint2(0u, 0u);
+                if (k == ones_kk && ones_lane) {   // the bias' ones column: bf16 1.0 = 0x3f80 in half ones_c
                     uint32_t& w = (ones_c >> 1) ? u.y : u.x;
                     const int sh = 16 * (ones_c & 1);
                     w = (w & ~(0xffffu << sh)) | ((xin ? 0x3f80u : 0u) << sh);
@@ -1260,8 +1265,10 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             } else {
                 v = R.x[k];
             }
-            if (MASK && !xin) v = f4zero();
-            if (k == ones_k) f4set(v, ones_c, xin ? 1.f : 0.f);
+            if (M && !xin) v = f4zero();
+            if (k == ones_kk) {
+                if (ones_lane) f4set(v, ones_c, xin ? 1.f : 0.f);
+            }
             putx(Xs, rr, c0 + 8 * k, v);
         }
 #pragma unroll
@@ -1269,14 +1276,19 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             if (!yk_ok(k)) break;
             if constexpr (kRawY) {
                 uint2 u = R.yh[k];
-                if (MASK && !yin) u = make_uint2(0u, 0u);
+                if (M && !yin) u = make_uint2(0u, 0u);
                 *reinterpret_cast<uint2*>(Ys + IY::woff(yr, yc0 + 8 * k)) = u;
                 continue;
             }
             float4 v = R.y[k];
-            if (MASK && !yin) v = f4zero();
+            if (M && !yin) v = f4zero();
             puty(Ys, yr, yc0 + 8 * k, v);
         }
+    };
+    auto build = [&](const WsSet4& R, char* Xs) {
+        if constexpr (DBG == 6) return;
+        if (MASK && R.nvalid < 32) build_m(R, Xs, std::true_type{});
+        else build_m(R, Xs, std::false_type{});
     };
     if (T == 0) {
         __syncthreads();
