@@ -1152,6 +1152,18 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
     // in the staging wave's stream.)
     int64_t fs = t0 / a.nbs, fnb = t0 - fs * a.nbs;
     int fdone = 0;
+    // operand loads as buffer loads: a stage's block base is wave-uniform (a descriptor built by the
+    // scalar unit), each lane's 32-bit offset within the block is fixed for the whole loop — no 64-bit
+    // address arithmetic per load on the staging wave's vector stream
+    constexpr int XEB = (B16 & kB16X) ? 2 : 4, YEB = (B16 & kB16Y) ? 2 : 4;   // bytes per element
+    int vox[W::NKX], voy[W::NKY];
+#pragma unroll
+    for (int k = 0; k < W::NKX; ++k) vox[k] = (rr * 4 + offx[k]) * XEB;
+#pragma unroll
+    for (int k = 0; k < W::NKY; ++k) voy[k] = (YROW ? yr * 160 + offy[k] : rr * 4 + offy[k]) * YEB;
+    auto rsrc = [](const void* p, int bytes) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+    };
     auto fetch = [&](int t, WsSet4& R) {
         if constexpr (DBG == 1 || DBG == 6) {   // diagnosis: no global loads
             const float c = (float)(rr + t);
@@ -1172,6 +1184,47 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
             }
         }
         if (MASK) R.nvalid = (int)min<int64_t>(32, a.count - nb * 32);
+        if constexpr (DBG == 0) {
+            // stage blocks: bf16 storage keeps the fp32 step starts (the producers write through
+            // per-step pointers), elements within a step at 2 bytes
+            const int64_t bx = (s * a.x_sb + nb) * (W::KHX * 64), sx = s * a.x_sb * (W::KHX * 64);
+            const int64_t by = YROW ? (s * a.y_sb + nb) * (32 * 160) : (s * a.y_sb + nb) * (W::KHY * 64);
+            const int64_t sy = YROW ? 0 : s * a.y_sb * (W::KHY * 64);
+            if (XD == 1) {
+                R.d = a.xd[(s * a.x_sb + nb) * 32 + rr];
+            } else if (XD == 2) {
+                const float4 p = a.xp[min<int64_t>((s * a.x_sb + nb) * 32 + rr, a.count - 1)];
+                R.d = make_float2(p.y, p.z);   // Networks.py:65-71: (y, width)
+            } else {
+                const auto rx = rsrc(reinterpret_cast<const char*>(a.x + sx) + (bx - sx) * XEB, W::KHX * 64 * XEB);
+#pragma unroll
+                for (int k = 0; k < W::NKX; ++k) {
+                    if constexpr (XEB == 2) {
+                        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rx, vox[k], 0, 0);
+                        const uint2 w = make_uint2(u[0], u[1]);
+                        if constexpr (kRawX) R.xh[k] = w;
+                        else R.x[k] = unpack4_bf16(w);
+                    } else {
+                        const auto u = __builtin_amdgcn_raw_buffer_load_b128(rx, vox[k], 0, 0);
+                        R.x[k] = make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
+                    }
+                }
+            }
+            const auto ry = rsrc(reinterpret_cast<const char*>(a.y + sy) + (by - sy) * YEB, (YROW ? 32 * 160 : W::KHY * 64) * YEB);
+#pragma unroll
+            for (int k = 0; k < W::NKY; ++k) {
+                if constexpr (YEB == 2) {
+                    const auto u = __builtin_amdgcn_raw_buffer_load_b64(ry, voy[k], 0, 0);
+                    const uint2 w = make_uint2(u[0], u[1]);
+                    if constexpr (kRawY) R.yh[k] = w;
+                    else R.y[k] = unpack4_bf16(w);
+                } else {
+                    const auto u = __builtin_amdgcn_raw_buffer_load_b128(ry, voy[k], 0, 0);
+                    R.y[k] = make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
+                }
+            }
+            return;
+        }
         const int64_t ix = (s * a.x_sb + nb) * (W::KHX * 64) + rr * 4;   // element indices
         const int64_t iy = YROW ? ((s * a.y_sb + nb) * 32 + yr) * 160 : (s * a.y_sb + nb) * (W::KHY * 64) + rr * 4;
         const float* px = a.x + ix;
