@@ -189,6 +189,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+// relu(x) on a real edge (cap = +inf), 0 on a padding edge (cap = 0): one v_med3_f32 where
+// relu(x) · valid was a v_max_f32 and a v_mul_f32 (the same values)
+__device__ __forceinline__ float relu_valid(float x, float cap) { return __builtin_amdgcn_fmed3f(x, 0.f, cap); }
 // g if bit f of bits is set, else +0: a sign-extended one-bit field as an AND mask (v_bfe_i32 +
 // v_and_b32; written as a select the compiler emits and + compare + cndmask)
 __device__ __forceinline__ float mask_bit(float g, uint32_t bits, int f) {

@@ -505,7 +505,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         // h1 = relu(A + U[s] + V[r]) — rmp layer 1 (Networks.py:84-87), lane = edge, split
         // halves, streamed 4 features at a time straight into h2 = h1·W2 (rmp layer 2).
         const uint64_t vmask = __ballot(valid);
-        const float vf = valid ? 1.f : 0.f;
+        const float vcap = valid ? __builtin_huge_valf() : 0.f;   // relu_valid: 0 on padding edges
         const float* Acm = a.A + (int64_t)blk * kCmBlk + h * 128 + i * 4;   // chunk q at + 256q
         // U[s], V[r]: chunk-major node rows (chunk q at +256q), gathered per lane
         const float4* U4 = reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 4 * 0) + h * 128);
@@ -526,10 +526,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         AUV b0{ldA(0), U4[0], V4[0]}, b1{ldA(1), U4[64], V4[64]}, b2;
         auto chunk = [&](int q, const AUV& cur, AUV& ahead) {
             float xv[4];
-            xv[0] = relu(cur.a.x + cur.u.x + cur.v.x) * vf;
-            xv[1] = relu(cur.a.y + cur.u.y + cur.v.y) * vf;
-            xv[2] = relu(cur.a.z + cur.u.z + cur.v.z) * vf;
-            xv[3] = relu(cur.a.w + cur.u.w + cur.v.w) * vf;
+            xv[0] = relu_valid(cur.a.x + cur.u.x + cur.v.x, vcap);
+            xv[1] = relu_valid(cur.a.y + cur.u.y + cur.v.y, vcap);
+            xv[2] = relu_valid(cur.a.z + cur.u.z + cur.v.z, vcap);
+            xv[3] = relu_valid(cur.a.w + cur.u.w + cur.v.w, vcap);
             if (h1cm) *reinterpret_cast<float4*>(h1cm + 256 * q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
             const int qn = min(q + 2, kKhE / 4 - 1);   // unconditional (clamped) prefetch
             ahead.a = ldA(qn);
@@ -1013,7 +1013,7 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         const int s = cur_sd.x, d = cur_sd.y;
         const bool valid = s >= 0;
         const uint64_t vmask = __ballot(valid);
-        const float vf = valid ? 1.f : 0.f;
+        const float vcap = valid ? __builtin_huge_valf() : 0.f;   // relu_valid: 0 on padding edges
         uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         Src nxt;
@@ -1025,10 +1025,10 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
             float xv[8];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
-                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
-                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
-                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
+                xv[4 * c + 0] = relu_valid(cr.a[c].x + cr.u[c].x + cr.v[c].x, vcap);
+                xv[4 * c + 1] = relu_valid(cr.a[c].y + cr.u[c].y + cr.v[c].y, vcap);
+                xv[4 * c + 2] = relu_valid(cr.a[c].z + cr.u[c].z + cr.v[c].z, vcap);
+                xv[4 * c + 3] = relu_valid(cr.a[c].w + cr.u[c].w + cr.v[c].w, vcap);
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
@@ -1195,7 +1195,7 @@ void k_edge_fwd_rb_x6(EdgeFwdArgs a) {
         const int nxt_s = a.esrc[(int64_t)nb * 32 + i];
         const bool valid = cur_s >= 0;
         const uint64_t vmask = __ballot(valid);
-        const float vf = valid ? 1.f : 0.f;
+        const float vcap = valid ? __builtin_huge_valf() : 0.f;   // relu_valid: 0 on padding edges
         uint32_t* mrow = MASKS && a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         Src nxt;
@@ -1207,10 +1207,10 @@ void k_edge_fwd_rb_x6(EdgeFwdArgs a) {
             float xv[8];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                xv[4 * c + 0] = relu(cr.a[c].x + cr.u[c].x + cr.v[c].x) * vf;
-                xv[4 * c + 1] = relu(cr.a[c].y + cr.u[c].y + cr.v[c].y) * vf;
-                xv[4 * c + 2] = relu(cr.a[c].z + cr.u[c].z + cr.v[c].z) * vf;
-                xv[4 * c + 3] = relu(cr.a[c].w + cr.u[c].w + cr.v[c].w) * vf;
+                xv[4 * c + 0] = relu_valid(cr.a[c].x + cr.u[c].x + cr.v[c].x, vcap);
+                xv[4 * c + 1] = relu_valid(cr.a[c].y + cr.u[c].y + cr.v[c].y, vcap);
+                xv[4 * c + 2] = relu_valid(cr.a[c].z + cr.u[c].z + cr.v[c].z, vcap);
+                xv[4 * c + 3] = relu_valid(cr.a[c].w + cr.u[c].w + cr.v[c].w, vcap);
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll

@@ -823,7 +823,7 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
         const int s = a.esrc[(int64_t)blk * 32 + i], d = a.edst[(int64_t)blk * 32 + i];
         const bool valid = s >= 0;
         const uint64_t vmask = __ballot(valid);
-        const float vf = valid ? 1.f : 0.f;
+        const float vcap = valid ? __builtin_huge_valf() : 0.f;   // relu_valid: 0 on padding edges
         {   // k-blocks 2T, 2T+1: chunks q = 4T .. 4T+3 (q < 19)
             const int sc = valid ? s : n0, dc = valid ? d : n0;
             const int64_t ai = (int64_t)blk * kCmBlk + h * 128 + i * 4;
@@ -848,10 +848,10 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const float4 av = ra[2 * k + c], uv = ru[2 * k + c], vv = rv[2 * k + c];
-                    xv[4 * c + 0] = relu(av.x + uv.x + vv.x) * vf;
-                    xv[4 * c + 1] = relu(av.y + uv.y + vv.y) * vf;
-                    xv[4 * c + 2] = relu(av.z + uv.z + vv.z) * vf;
-                    xv[4 * c + 3] = relu(av.w + uv.w + vv.w) * vf;
+                    xv[4 * c + 0] = relu_valid(av.x + uv.x + vv.x, vcap);
+                    xv[4 * c + 1] = relu_valid(av.y + uv.y + vv.y, vcap);
+                    xv[4 * c + 2] = relu_valid(av.z + uv.z + vv.z, vcap);
+                    xv[4 * c + 3] = relu_valid(av.w + uv.w + vv.w, vcap);
                 }
                 uint32_t sp[3][4];
 #pragma unroll
