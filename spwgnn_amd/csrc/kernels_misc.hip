@@ -544,6 +544,25 @@ __global__ __launch_bounds__(kWgThreads, OCC) void k_wgrad_x6(WgradArgs a) {
 constexpr int kW2gThreads = 512;
 constexpr int kW2gImg = 3 * X6Img<160>::PART;   // one operand's split image (30 KB)
 
+// A rows of 32-edge block b (fp32, or bf16 at the fp32 element index) through a buffer descriptor
+// built from wave-uniform values: the lane's offsets within a block stay fixed over the stage loop,
+// so a load costs no 64-bit address arithmetic on the staging wave
+template <bool AB16>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t w2_rows_rsrc(const float* A, int64_t b) {
+    constexpr int EB = AB16 ? 2 : 4;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(reinterpret_cast<const char*>(A) + b * kCmBlk * EB), (short)0,
+                                             kCmBlk * EB, 0x00020000);
+}
+template <bool AB16>
+__device__ __forceinline__ void w2_row_load(__amdgpu_buffer_rsrc_t r, int vo, uint2& ah, float4& af) {
+    if constexpr (AB16) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, vo, 0, 0);
+        ah = make_uint2(u[0], u[1]);
+    } else {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0);
+        af = make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
+    }
+}
 struct W2gSet {
     float4 a[5], u[5], v[5], g[5];
     uint2 ah[5];   // A rows stored as bf16 (AB16): unpacked where they are used (build)
@@ -624,6 +643,9 @@ __device__ __forceinline__ void w2grad_ws_body(const WgradArgs& a, int64_t blk_p
     int off[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) off[k] = (k < 4 || k4ok) ? cm_offk<kKhE>(0, 4 * (c0 + 8 * k)) : 0;
+    int voa[5];   // byte offsets of the lane's A-row groups within a 32-edge block
+#pragma unroll
+    for (int k = 0; k < 5; ++k) voa[k] = (rr * 4 + off[k]) * (AB16 ? 2 : 4);
     const int64_t nstep_n = a.RN * kRowE;
     auto stage_of = [&](int t, int64_t& b, int& s) {
         const uint32_t tc = (uint32_t)(t < T ? t : T - 1);
@@ -644,9 +666,6 @@ __device__ __forceinline__ void w2grad_ws_body(const WgradArgs& a, int64_t blk_p
         stage_of(t, b, s);
         R.in = idx.x >= 0;
         const int sn = R.in ? idx.x : 0, dn = R.in ? idx.y : 0;
-        const int64_t ia = b * kCmBlk + rr * 4;
-        const float* pa = a.A + ia;
-        const uint16_t* ha = reinterpret_cast<const uint16_t*>(a.A) + ia;
         const int64_t ns = (int64_t)s * nstep_n;
         const float* pu = a.U + ns + (int64_t)(sn >> 5) * kCmBlk + (sn & 31) * 4;
         const int64_t dno = ns + (int64_t)(dn >> 5) * kCmBlk + (dn & 31) * 4;
@@ -654,10 +673,11 @@ __device__ __forceinline__ void w2grad_ws_body(const WgradArgs& a, int64_t blk_p
         const float* pg = a.G3 + dno;
         uint32_t mw[5];
         load_m2(a.mask2 + ((int64_t)s * nblk + b) * kM2Blk, rr, mw);
+        // A rows: buffer loads from the block's (wave-uniform) base at fixed lane offsets
+        const auto rA = w2_rows_rsrc<AB16>(a.A, b);
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(ha + off[k]);   // re-read by the
-            else R.a[k] = *reinterpret_cast<const float4*>(pa + off[k]);                // block's next steps
+            w2_row_load<AB16>(rA, voa[k], R.ah[k], R.a[k]);   // re-read by the block's next steps
             R.u[k] = *reinterpret_cast<const float4*>(pu + off[k]);
             R.v[k] = *reinterpret_cast<const float4*>(pv + off[k]);
             R.g[k] = *reinterpret_cast<const float4*>(pg + off[k]);
@@ -844,6 +864,9 @@ void k_w2grad_tile(WgradArgs a, int64_t blk_per_wg) {
     int off[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) off[k] = (k < 4 || k4ok) ? cm_offk<kKhE>(0, 4 * (c0 + 8 * k)) : 0;
+    int voa[5];   // byte offsets of the lane's A-row groups within a 32-edge block
+#pragma unroll
+    for (int k = 0; k < 5; ++k) voa[k] = (rr * 4 + off[k]) * (AB16 ? 2 : 4);
     const int64_t nstep_n = a.RN * kRowE;
     if (T == 0) {   // the matrix waves' two barriers (they write a zero slab)
         __syncthreads();
@@ -871,13 +894,10 @@ void k_w2grad_tile(WgradArgs a, int64_t blk_per_wg) {
         const int64_t b = (int64_t)it.info.x + it.bb;
         R.src = a.esrc[32 * b + rr];
         R.dst = a.edst[32 * b + rr];
-        const int64_t ia = b * kCmBlk + rr * 4;
         load_m2(a.mask2 + ((int64_t)it.s * nblk + b) * kM2Blk, rr, R.m);
+        const auto rA = w2_rows_rsrc<AB16>(a.A, b);
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            if constexpr (AB16) R.ah[k] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.A) + ia + off[k]);
-            else R.a[k] = *reinterpret_cast<const float4*>(a.A + ia + off[k]);
-        }
+        for (int k = 0; k < 5; ++k) w2_row_load<AB16>(rA, voa[k], R.ah[k], R.a[k]);
     };
     // one group's node rows: unit u = (arr·38 + chunk)·16 + node (node fastest: coalesced per chunk)
     float4 pf[kW2tPf];
