@@ -461,6 +461,13 @@ __device__ __forceinline__ void ht_mfma(const bf16x8 (&a)[3], const uint32_t (&x
     }
 }
 
+// B sources that hand over a k-block's element pair m as stored bf16 bits (a `word(c, kb, m)`
+// member): in bf16 math (one part) that word already is the operand — no unpack and re-pack per pair
+template <class T, class = void>
+struct has_b16_words : std::false_type {};
+template <class T>
+struct has_b16_words<T, std::void_t<decltype(std::declval<const std::decay_t<T>&>().word(0, 0, 0))>> : std::true_type {};
+
 // ---- transposed orientation in split-bf16 math (x6), NC column tiles of 32 rows per wave:
 // out[c][T] += Wᵀ·B[c] over NKB k-blocks of 16. getb(c, kb, v) supplies the 8 fp32 B values of
 // lane (j, h) for k-block kb (split into three bf16 parts here, once per k-block); the weight image
@@ -486,9 +493,14 @@ __device__ __forceinline__ void tgemm_x6(GetB&& getb, f32x16 (&out)[NC][NT_OUT],
     if constexpr (HT) ht_enter(out, hq);
     auto split_pair = [&](int kb, int q) {
         const int c = q >> 2, m = q & 3;
-        float v[8];
-        getb(c, kb, v);
-        split2(v[2 * m], v[2 * m + 1], sp[kb % SPD][c][0][m], sp[kb % SPD][c][1][m], sp[kb % SPD][c][2][m]);
+        if constexpr (PARTS == 1 && has_b16_words<GetB>::value) {   // bf16 math: the stored pair is the h part
+            sp[kb % SPD][c][0][m] = getb.word(c, kb, m);
+            sp[kb % SPD][c][1][m] = sp[kb % SPD][c][2][m] = 0u;
+        } else {
+            float v[8];
+            getb(c, kb, v);
+            split2(v[2 * m], v[2 * m + 1], sp[kb % SPD][c][0][m], sp[kb % SPD][c][1][m], sp[kb % SPD][c][2][m]);
+        }
     };
 #pragma unroll
     for (int q = 0; q < NP; ++q) split_pair(0, q);
@@ -583,9 +595,14 @@ __device__ __forceinline__ void tgemm_x6_wg(GetB&& getb, f32x16 (&out)[NC][NT_OU
     if constexpr (HT) ht_enter(out, hq);
     auto split_pair = [&](int kb, int q) {
         const int c = q >> 2, m = q & 3;
-        float v[8];
-        getb(c, kb, v);
-        split2(v[2 * m], v[2 * m + 1], sp[kb % SPD][c][0][m], sp[kb % SPD][c][1][m], sp[kb % SPD][c][2][m]);
+        if constexpr (PARTS == 1 && has_b16_words<GetB>::value) {   // bf16 math: the stored pair is the h part
+            sp[kb % SPD][c][0][m] = getb.word(c, kb, m);
+            sp[kb % SPD][c][1][m] = sp[kb % SPD][c][2][m] = 0u;
+        } else {
+            float v[8];
+            getb(c, kb, v);
+            split2(v[2 * m], v[2 * m + 1], sp[kb % SPD][c][0][m], sp[kb % SPD][c][1][m], sp[kb % SPD][c][2][m]);
+        }
     };
 #pragma unroll
     for (int q = 0; q < NP; ++q) split_pair(0, q);

@@ -543,7 +543,31 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_bwd_x6(EncEdg
     __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     f32x16 D[NC][5], E[NC][5];
-    {
+    if constexpr (B16 && NP == 1) {
+        // bf16 math over bf16-stored dA: the stored element pairs are the MFMA operand words as they are
+        struct Rows {
+            uint2 raw[NC][kKhE / 4];
+            __device__ uint32_t word(int c, int kb, int m) const {
+                const int q = 2 * kb + (m >> 1);
+                return q < kKhE / 4 ? ((m & 1) ? raw[c][q].y : raw[c][q].x) : 0u;
+            }
+            __device__ void operator()(int c, int kb, float (&v)[8]) const {   // (unused: word() is taken)
+                const float4 x = unpack4_bf16(raw[c][2 * kb]);
+                const float4 y = 2 * kb + 1 < kKhE / 4 ? unpack4_bf16(raw[c][2 * kb + 1]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+                v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+            }
+        } rows;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int64_t e = (int64_t)min(blk0 + c, a.n_eblocks - 1) * 32 + j;
+            const uint2* row = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.dA) + e * kLdE + kKhE * h);
+#pragma unroll
+            for (int q = 0; q < kKhE / 4; ++q) rows.raw[c][q] = row[q];
+            zero_tiles(D[c]);
+        }
+        tgemm_x6s<5, (kKhE + 7) / 8, NC, 6, NP, NW>(rows, D, a.x_w1at, lane, wr);   // dc_r = dA·W1aᵀ
+    } else {
         float4 raw[NC][kKhE / 4];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
