@@ -1642,7 +1642,9 @@ __global__ void k_tower_readout(const float* __restrict__ z, const int32_t* __re
 template <int KH, bool NODE, bool B16>
 __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int tid) {
     constexpr int NQH = KH / 2, NK = (NQH + 7) / 8, NYP = KH == kKhE ? 160 : 128, BLK = KH * 64;
-    constexpr int UB = 4;   // blocks whose loads are issued together (the loop is latency-bound)
+    // blocks whose loads are issued together (the loop is latency-bound): bf16 rows are half the bytes
+    // per load, so twice the blocks keep the same bytes in flight
+    constexpr int UB = B16 ? 8 : 4;
     const int i = tid & 31, g = tid >> 5;
     const int64_t b0 = (int64_t)bid * a.blk_per_wg, b1 = min(a.nblk, b0 + a.blk_per_wg);
     float4 s0[NK], s1[NK], s2[NK];
@@ -1651,6 +1653,7 @@ __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int 
     for (int64_t bg = b0; bg < b1; bg += UB) {
         float x0[UB], x1[UB], x2[UB];
         float4 y[UB][NK];
+        uint2 yh[UB][NK];   // B16: the stored pairs, unpacked at their fmas
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const bool in = bg + u < b1;
@@ -1674,18 +1677,22 @@ __device__ __forceinline__ void wgrad_pos3_body(const Pos3Args& a, int bid, int 
             for (int k = 0; k < NK; ++k) {
                 const int qh = min(g + 8 * k, NQH - 1);
                 const int64_t el = b * BLK + (qh * 32 + i) * 4;
-                y[u][k] = B16 ? unpack4_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.y) + el))
-                              : *reinterpret_cast<const float4*>(a.y + el);
                 // rows past the batch are not written by every producer (the fused small-batch
                 // kernels store only their towers' rows): 0·NaN must not reach the sums
-                if (!ok) y[u][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (B16) {
+                    yh[u][k] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.y) + el);
+                    if (!ok) yh[u][k] = make_uint2(0u, 0u);
+                } else {
+                    y[u][k] = *reinterpret_cast<const float4*>(a.y + el);
+                    if (!ok) y[u][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             }
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u)
 #pragma unroll
             for (int k = 0; k < NK; ++k) {
-                const float4 v = y[u][k];
+                const float4 v = B16 ? unpack4_bf16(yh[u][k]) : y[u][k];
                 s0[k] = make_float4(__builtin_fmaf(x0[u], v.x, s0[k].x), __builtin_fmaf(x0[u], v.y, s0[k].y),
                                     __builtin_fmaf(x0[u], v.z, s0[k].z), __builtin_fmaf(x0[u], v.w, s0[k].w));
                 s1[k] = make_float4(__builtin_fmaf(x1[u], v.x, s1[k].x), __builtin_fmaf(x1[u], v.y, s1[k].y),
