@@ -1044,6 +1044,9 @@ struct WsSet4 {
 #ifndef SPWGNN_WS_NSET   // stage sets the staging waves keep in flight (k_wgrad_ws)
 #define SPWGNN_WS_NSET 4
 #endif
+#ifndef SPWGNN_WS_NSET_B16   // the same in bf16 math (half the bytes per load)
+#define SPWGNN_WS_NSET_B16 4
+#endif
 template <int KXP, int NYP, int YROW, bool MASK, int NP, int XD, int B16>
 __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* smem) {
     constexpr int DBG = SPWGNN_WS_DBG;
@@ -1387,7 +1390,7 @@ __device__ __forceinline__ void wgrad_ws_body(const WgWsArgs& a, int bid, char* 
     // u % NS (its stage u was built one iteration ago) and build stage u + 1 into buffer (u + 1) & 1,
     // so a stage's loads are issued NS − 1 iterations before their split (static set names: the
     // loop is unrolled by NS)
-    constexpr int NS = SPWGNN_WS_NSET;
+    constexpr int NS = NP == 1 ? SPWGNN_WS_NSET_B16 : SPWGNN_WS_NSET;
     WsSet4 R[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) fetch(k, R[k]);
