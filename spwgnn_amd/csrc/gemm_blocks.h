@@ -749,5 +749,15 @@ struct HalfRowsB16 {
 // fp32 or bf16 (B16) half rows
 template <int KH, int NC, bool B16>
 using HalfRowsT = typename std::conditional<B16, HalfRowsB16<KH, NC>, HalfRows<KH, NC>>::type;
+// bf16 half rows that also hand their stored pairs to a one-part product as they are (has_b16_words)
+template <int KH, int NC>
+struct HalfRowsB16W : HalfRowsB16<KH, NC> {
+    __device__ __forceinline__ uint32_t word(int c, int kb, int m) const {
+        const int q = 2 * kb + (m >> 1);
+        return q < HalfRowsB16<KH, NC>::Q ? ((m & 1) ? this->raw[c][q].y : this->raw[c][q].x) : 0u;
+    }
+};
+template <int KH, int NC, bool B16>
+using HalfRowsWT = typename std::conditional<B16, HalfRowsB16W<KH, NC>, HalfRows<KH, NC>>::type;
 
 }  // namespace spw

@@ -706,7 +706,7 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
     f32x16 E[NC][4], O[NC][4];
     zero2(E);
     {
-        HalfRowsT<kKhE, NC, N16> hr;
+        HalfRowsWT<kKhE, NC, N16> hr;
         int64_t off[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) off[c] = bE(c);
