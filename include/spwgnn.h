@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 4   /* 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
+#define SPWGNN_ABI_VERSION 5   /* 5: spwgnn_team_max_blocks; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -193,6 +193,14 @@ int64_t spwgnn_workspace_bytes(int32_t n_nodes, int32_t n_eblocks, int32_t mp_st
  * forward's fused small-batch step loop, bit 1 = the backward's; < 0 = an error
  * status. Profilers attribute kernel time and FLOPs by it instead of restating the library's gate. */
 int32_t spwgnn_fused_path(const spwgnn_batch* batch, const spwgnn_run* run);
+
+/* Batches of at most this many 32-row blocks (edge blocks, node blocks, wave-tiles; counted per
+ * launch) run the latency-oriented team kernels, larger ones the wide kernels the large-batch step
+ * runs (both compute the same products in the same order). Default 512 (the
+ * reference's batch 32 is ~30 blocks). set >= 0 sets the limit for the process and returns the
+ * previous one; set < 0 only returns it. 0 puts every batch on the wide kernels (parity tests of the
+ * large-batch path at oracle-sized batches). Read when a call plans its launches. */
+int32_t spwgnn_team_max_blocks(int32_t set);
 
 /* Forward: the whole graph of Networks.py:31-96 → per-node logits z (the model output is
  * sigmoid(z), Networks.py:94). logits: [n_nodes] device fp32. */

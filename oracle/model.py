@@ -176,6 +176,78 @@ def forward_gather(p, pos, src, dst, prop, mp_steps: int = REF_MP_STEPS,
     return x[:, 0]
 
 
+def relu_margins_gather(p, pos, src, dst, prop, tower_of_node, n_towers: int,
+                        mp_steps: int = REF_MP_STEPS, drop_r=None, drop_o=None,
+                        chunk_nodes: int = 1 << 15) -> np.ndarray:
+    """Per tower: the smallest |pre-activation| over every ReLU its forward evaluates (fp64, dropout
+    off) — rm's four (Blocks.py:20-28 + Networks.py:75), om's two (Networks.py:76), rmp's two and omp's
+    one per step (Networks.py:86-90) — and the logit's distance to the BCE clip (Networks.py:102).
+
+    A ReLU's derivative jumps at 0: an fp32 implementation whose pre-activation lands within its own
+    rounding of 0 may take the other side of the kink, and then one edge's or node's term moves
+    between the two sides of a gradient sum. Parity tests of the summed gradients keep towers whose
+    margin is far above fp32 rounding (tests/test_gpu_chain_parity.py). Same forward as
+    `forward_gather` (``drop_r`` (Ne,150) / ``drop_o`` (Nn,100): its dropout masks); evaluated over contiguous node ranges of whole towers (``chunk_nodes``) to bound
+    memory. pos (Nn,3), src/dst (Ne,) global node ids, tower_of_node (Nn,) sorted tower ids."""
+    tower_of_node = np.asarray(tower_of_node, np.int64)
+    src = np.asarray(src, np.int64)
+    dst = np.asarray(dst, np.int64)
+    out = np.full(n_towers, np.inf)
+    Nn = len(tower_of_node)
+    e_order = np.argsort(dst, kind="stable")
+    dst_sorted = dst[e_order]
+    a = 0
+    with torch.no_grad():
+        while a < Nn:
+            b = min(Nn, a + chunk_nodes)
+            while b < Nn and tower_of_node[b] == tower_of_node[b - 1]:   # whole towers only
+                b += 1
+            e_lo, e_hi = np.searchsorted(dst_sorted, [a, b])
+            ei = np.sort(e_order[e_lo:e_hi])
+            s_ = torch.as_tensor(src[ei] - a)
+            d_ = torch.as_tensor(dst[ei] - a)
+            et = torch.as_tensor(tower_of_node[dst[ei]])
+            nt = torch.as_tensor(tower_of_node[a:b])
+            x = torch.as_tensor(np.asarray(pos[a:b], np.float64))
+            P = torch.as_tensor(np.asarray(prop[a:b], np.float64))
+            marg = torch.full((n_towers,), float("inf"), dtype=torch.float64)
+
+            def note(pre, rows_tower):
+                m = pre.abs().amin(dim=1)
+                marg.scatter_reduce_(0, rows_tower, m, reduce="amin")
+
+            h = x[d_, 0:2] - x[s_, 0:2]
+            for i in range(4):
+                h = h @ p[f"rm.{i}.kernel"] + p[f"rm.{i}.bias"]
+                note(h, et)
+                h = torch.relu(h)
+            c_r = h if drop_r is None else h * torch.as_tensor(np.asarray(drop_r[ei], np.float64))
+            h = x[:, 1:3]
+            for i in range(2):
+                h = h @ p[f"om.{i}.kernel"] + p[f"om.{i}.bias"]
+                note(h, nt)
+                h = torch.relu(h)
+            c_o = h if drop_o is None else h * torch.as_tensor(np.asarray(drop_o[a:b], np.float64))
+            z = None
+            for _ in range(mp_steps):
+                h = torch.cat([c_r, P[s_], P[d_]], dim=-1)
+                for i in range(2):
+                    h = h @ p[f"rmp.{i}.kernel"] + p[f"rmp.{i}.bias"]
+                    note(h, et)
+                    h = torch.relu(h)
+                msg = h @ p["rmp.2.kernel"] + p["rmp.2.bias"]
+                agg = torch.zeros(b - a, msg.shape[1], dtype=msg.dtype).index_add_(0, d_, msg)
+                h = torch.cat([c_o, torch.tanh(agg), P], dim=-1) @ p["omp.0.kernel"] + p["omp.0.bias"]
+                note(h, nt)
+                xo = torch.relu(h) @ p["omp.1.kernel"] + p["omp.1.bias"]
+                P = torch.tanh(xo[:, 1:] + P)
+                z = xo[:, 0]
+            note((z.abs() - LOGIT_CLIP)[:, None], nt)
+            out = np.minimum(out, marg.numpy())
+            a = b
+    return out
+
+
 # ---------------------------------------------------------------------------------------
 # Form 3: plain per-tower python loop with explicit sums (small cases only).
 # ---------------------------------------------------------------------------------------

@@ -1164,6 +1164,10 @@ int32_t spwgnn_fused_path(const spwgnn_batch* batch, const spwgnn_run* run) {
     return (fwd_fused_taken(run, batch) ? 1 : 0) | (run->training && bwd_fused_taken(run, batch) ? 2 : 0);
 }
 
+int32_t spwgnn_team_max_blocks(int32_t set) {
+    return team_max_blocks(set);
+}
+
 int32_t spwgnn_forward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run, void* workspace,
                        int64_t workspace_bytes, float* logits, spwgnn_stream_t stream) {
     int32_t stt = validate(batch, run);

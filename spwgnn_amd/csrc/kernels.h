@@ -406,6 +406,7 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
 #endif
 constexpr int kTeamMaxBlocks = SPWGNN_TEAM_MAX_BLOCKS;
 bool team_blocks(int n_blocks);   // 32-row blocks of the launch (edge or node blocks)
+int team_max_blocks(int set);      // set >= 0: the new limit (returns the previous one); < 0: query
 hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st);
 hipError_t launch_edge_bwd_team(const EdgeBwdArgs& a, int math, hipStream_t st);

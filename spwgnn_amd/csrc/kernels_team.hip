@@ -14,6 +14,7 @@
 // image (L2); the next layer's fragment kb is requested as soon as this layer's k-block kb has
 // issued, so it arrives during the rest of the layer, the epilogue and the barrier.
 #include "kernels.h"
+#include <atomic>
 #include <cstdlib>
 
 namespace spw {
@@ -1358,12 +1359,20 @@ __global__ __launch_bounds__(64 * kTeamEdge) void k_bwd_enc_pair_team(DaArgs da,
     }
 }
 
+// The team limit in force (spwgnn_team_max_blocks): the compile-time kTeamMaxBlocks unless a caller
+// moved it, e.g. a parity test that puts a small batch on the wide (chain) kernels the large-batch
+// bench step runs. Read when a call plans its launches; a captured graph keeps the launches it planned.
+static std::atomic<int> g_team_max{kTeamMaxBlocks};
+int team_max_blocks(int set) {
+    return set >= 0 ? g_team_max.exchange(set) : g_team_max.load(std::memory_order_relaxed);
+}
+
 bool team_blocks(int n_blocks) {
 #ifdef SPWGNN_DIAG   // A/B: SPWGNN_NO_TEAM=1 keeps the one-wave-per-block kernels at every size
     static const bool off = getenv("SPWGNN_NO_TEAM") && atoi(getenv("SPWGNN_NO_TEAM"));
     if (off) return false;
 #endif
-    return n_blocks > 0 && n_blocks <= kTeamMaxBlocks;
+    return n_blocks > 0 && n_blocks <= g_team_max.load(std::memory_order_relaxed);
 }
 
 hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st) {

@@ -153,6 +153,26 @@ def fused_path(batch: TowerBatch, run: RunConfig) -> int:
     return int(st)
 
 
+def team_max_blocks(set_to: Optional[int] = None) -> int:
+    """The library's small-batch limit (spwgnn_team_max_blocks): batches of at most this many 32-row
+    blocks run the team kernels, larger ones the wide kernels. With ``set_to`` (>= 0) it is changed for
+    the process and the previous limit is returned."""
+    return int(_lib.lib().spwgnn_team_max_blocks(-1 if set_to is None else int(set_to)))
+
+
+class wide_kernels:
+    """``with wide_kernels(): ...`` — every call inside plans the wide (large-batch) kernels whatever the
+    batch size (team limit 0), then the previous limit is restored."""
+
+    def __enter__(self):
+        self._prev = team_max_blocks(0)
+        return self
+
+    def __exit__(self, *exc):
+        team_max_blocks(self._prev)
+        return False
+
+
 def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Workspace,
             logits: Optional[torch.Tensor] = None) -> torch.Tensor:
     _require_gpu(flat_params, "params")

@@ -566,3 +566,20 @@ def test_half_tile_layout_algebra(kh, nkb):
         x, y = _swap32(out[:, r], out[:, 4 + r])
         q2[0, :, r], q2[1, :, r] = _swap16(x, y)
     assert np.array_equal(q2, q)
+
+
+def test_team_limit_is_a_runtime_setting():
+    """spwgnn_team_max_blocks (ABI 5): the small-batch limit defaults to 512 blocks, can be moved at run
+    time (0 = every batch on the wide kernels) and is restored; spwgnn_fused_path follows it (host
+    planning only, no device work — the batch arrays may live in host memory for this query)."""
+    from spwgnn_amd import engine as E
+    assert E.team_max_blocks() == 512
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(4, 6, seed=1)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cpu")
+    run = E.RunConfig(5, training=True, math="x6")
+    assert E.fused_path(batch, run) == 3
+    with E.wide_kernels():
+        assert E.team_max_blocks() == 0
+        assert E.fused_path(batch, run) == 0
+    assert E.team_max_blocks() == 512
+    assert E.team_max_blocks(7) == 512 and E.team_max_blocks(512) == 7
