@@ -134,7 +134,7 @@ def step_flops(Ne: int, Nn: int, S: int) -> float:
 
 class HipEvents:
     def __init__(self, n):
-        self.hip = C.CDLL("libamdhip64.so")
+        self.hip = _lib.hip_runtime()   # the runtime torch and the library run on
         self.ev = []
         for _ in range(n):
             e = C.c_void_p()

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 5   /* 5: spwgnn_team_max_blocks; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
+#define SPWGNN_ABI_VERSION 5   /* 5: spwgnn_team_max_blocks, spwgnn_host_device_ptr; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -264,6 +264,10 @@ int32_t spwgnn_sigmoid(const float* logits, float* probs, int64_t n, spwgnn_stre
  * device-mapped memory (hipHostMalloc), both pointers 16-byte aligned, bytes a multiple of 16. A
  * replayed small-batch step makes it its first node, so the batch upload rides inside the graph. */
 int32_t spwgnn_copy_in(const void* host, void* dev, int64_t bytes, spwgnn_stream_t stream);
+/* The device address of pinned, device-mapped host memory (hipHostGetDevicePointer through the HIP
+ * runtime this library runs on — the one the caller's allocator used), for spwgnn_copy_in and
+ * spwgnn_prologue.copy_src. 0, or the hipError_t of a host range that is not device-mapped. */
+int32_t spwgnn_host_device_ptr(const void* host, void** dev);
 
 /* Per-tower readout over contiguous node ranges [tower_offsets[t], tower_offsets[t+1]):
  *   SUM_PROB   out[t] = Σ sigmoid(z)  — the stability sum of JengaBuilder.remove_to_demolish /

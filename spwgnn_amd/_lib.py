@@ -78,6 +78,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_workspace_bytes": (i64, [i32, i32, i32, i32]),
         "spwgnn_fused_path": (i32, [C.POINTER(BatchC), C.POINTER(RunC)]),
         "spwgnn_team_max_blocks": (i32, [i32]),
+        "spwgnn_host_device_ptr": (i32, [vp, C.POINTER(vp)]),
         "spwgnn_forward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp]),
         "spwgnn_backward": (i32, [vp, C.POINTER(BatchC), C.POINTER(RunC), vp, i64, vp, vp, vp, vp]),
         "spwgnn_bce_scratch_bytes": (i64, [i64]),
@@ -117,6 +118,31 @@ def lib() -> C.CDLL:
                                   f"({lib_.spwgnn_struct_size(which)} vs {C.sizeof(st)} bytes): rebuild it")
         _lib = lib_
     return _lib
+
+
+_hip = None
+
+
+def hip_runtime() -> C.CDLL:
+    """The HIP runtime already mapped into this process — the copy torch and libspwgnn_hip.so run on —
+    opened by its mapped path (never a second runtime found by soname). For the event calls of the
+    bench's timing hook."""
+    global _hip
+    if _hip is None:
+        lib()
+        with open("/proc/self/maps") as f:
+            paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+        if not paths:
+            raise SpwgnnError("the HIP runtime is not mapped into this process")
+        _hip = C.CDLL(sorted(paths)[0])
+    return _hip
+
+
+def host_device_ptr(ptr: int) -> int:
+    """spwgnn_host_device_ptr: the device address of pinned, device-mapped host memory."""
+    out = C.c_void_p()
+    check(lib().spwgnn_host_device_ptr(C.c_void_p(ptr), C.byref(out)), "host_device_ptr (not device-mapped?)")
+    return int(out.value)
 
 
 def check(status: int, what: str = "") -> None:

@@ -1164,6 +1164,19 @@ int32_t spwgnn_fused_path(const spwgnn_batch* batch, const spwgnn_run* run) {
     return (fwd_fused_taken(run, batch) ? 1 : 0) | (run->training && bwd_fused_taken(run, batch) ? 2 : 0);
 }
 
+int32_t spwgnn_host_device_ptr(const void* host, void** dev) {
+    if (!host || !dev) return SPWGNN_E_ARG;
+    void* p = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&p, const_cast<void*>(host), 0);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();   // not this thread's next launch error
+        return (int32_t)e;
+    }
+    if (!p) return SPWGNN_E_ARG;
+    *dev = p;
+    return SPWGNN_OK;
+}
+
 int32_t spwgnn_team_max_blocks(int32_t set) {
     return team_max_blocks(set);
 }

@@ -99,6 +99,16 @@ __device__ __forceinline__ uint4 ld_nt_u4(const void* p) {
     return make_uint4(v[0], v[1], v[2], v[3]);
 #endif
 }
+// 16 bytes of pinned, device-mapped HOST memory that the host rewrites between launches (a replayed
+// step's upload slot): two system-scope relaxed atomic loads, which the compiler issues as global loads
+// with the system-coherence cache bits — never a stale L2 line from an earlier read of the same slot,
+// whether or not the allocation is fine-grained and whatever acquire the launch began with.
+__device__ __forceinline__ uint4 ld_sys_u4(const uint4* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
 __device__ __forceinline__ uint32_t ld_nt_u1(const uint32_t* p) {
 #ifdef SPWGNN_NO_NT
     return *p;

@@ -32,7 +32,7 @@ __global__ void k_prep(PrepArgs a, PrepX6Args x) {
     if (a.pro_row && id == (int)gridDim.y - 1) {   // a replayed step's prologue (PrologueArgs)
         const PrologueArgs& p = a.pro;
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n16; i += (int64_t)gridDim.x * blockDim.x)
-            p.dst[i] = p.src[i];
+            p.dst[i] = ld_sys_u4(p.src + i);   // host staging: system-coherent reads
         if (p.key && blockIdx.x == 0 && threadIdx.x == 0) step_advance_dev(p.key, p.step, p.mode, p.seed, p.rank);
         return;
     }

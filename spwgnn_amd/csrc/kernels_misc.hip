@@ -1970,7 +1970,8 @@ hipError_t launch_tower_readout(const float* z, const int32_t* off, int n_towers
 // buffer, as the step's first kernel: the loads cross PCIe once, all in flight together (a few µs),
 // where a DMA copy between two replays left the GPU idle for ≈ 26 µs.
 __global__ __launch_bounds__(256) void k_copy_in(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
+        dst[i] = ld_sys_u4(src + i);   // host staging the host rewrites between replays: system-coherent reads
 }
 hipError_t launch_copy_in(const void* src, void* dst, int64_t n16, hipStream_t st) {
     const int wgs = (int)std::min<int64_t>(64, (n16 + 1023) / 1024);   // ≤ 4 pieces per thread

@@ -69,21 +69,10 @@ class DeviceCounters:
             self.hyper = hyper
 
 
-_HIP = None
-
-
 def _mapped_device_ptr(host: torch.Tensor) -> int:
-    """The device address of a pinned host tensor (hipHostGetDevicePointer): kernels read it over
+    """The device address of a pinned host tensor (spwgnn_host_device_ptr): kernels read it over
     PCIe. Raises if the allocation is not device-mapped (the kernel would fault)."""
-    global _HIP
-    import ctypes as C
-    if _HIP is None:
-        _HIP = C.CDLL("libamdhip64.so")
-    p = C.c_void_p()
-    st = _HIP.hipHostGetDevicePointer(C.byref(p), C.c_void_p(host.data_ptr()), C.c_uint(0))
-    if st != 0 or not p.value:
-        raise _lib.SpwgnnError(f"pinned staging buffer is not device-mapped (hipHostGetDevicePointer {st})")
-    return int(p.value)
+    return _lib.host_device_ptr(host.data_ptr())
 
 
 class StaticBatch:

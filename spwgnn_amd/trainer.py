@@ -240,7 +240,11 @@ class Trainer:
             g = self.engine.backward(self.params, b, run, dz)
             w = b.n_nodes / n_global
             if acc is None:
-                acc = g.mul(w)            # own buffer: the engine reuses its gradient buffer
+                # the engine writes every backward into one buffer (HipEngine.grads), so the sum lives in
+                # a buffer of its own: the Trainer's persistent accumulator, overwritten here
+                if getattr(self, "_acc", None) is None or self._acc.shape != g.shape or self._acc.device != g.device:
+                    self._acc = torch.empty_like(g)
+                acc = torch.mul(g, w, out=self._acc)
             else:
                 acc.add_(g, alpha=w)
         if self.world > 1:

@@ -111,6 +111,26 @@ def _trainer_plans(n):
     return plans, tgts
 
 
+def test_trainer_replay_reuses_staging_slots():
+    """eight different batches of one geometry replayed back to back (graph=True, no host
+    synchronisation between steps), so each of the two pinned staging slots is rewritten by the host
+    and re-read by the upload (system-coherent loads, device_common.h ld_sys_u4) four times ==
+    Trainer.step on the same batches, bit for bit (parameters and both Adam moments)."""
+    params = O.random_params(14)
+    plans, tgts = _trainer_plans(8)
+    assert len({p.geometry for p in plans}) == 1
+    ta = Trainer(P.to_flat(params, device="cuda"), mp_steps=3, dropout=0.1, seed=9, math="x6")
+    for p, t in zip(plans, tgts):
+        ta.step(TowerBatch.from_plan(p, "cuda"), torch.as_tensor(t, device="cuda"))
+    tb = Trainer(P.to_flat(params, device="cuda"), mp_steps=3, dropout=0.1, seed=9, math="x6")
+    rs = ReplayStep(plans[0], "cuda", tb.replay_body(plans[0].n_nodes))
+    for p, t in zip(plans, tgts):
+        tb.replay_step(rs, p, t)
+    torch.cuda.synchronize()
+    assert rs.replays == 7 and rs.static.loads == 8
+    assert torch.equal(ta.params, tb.params) and torch.equal(ta.m, tb.m) and torch.equal(ta.v, tb.v)
+
+
 def test_trainer_replay_mixed_with_step_and_lr_change():
     """replayed steps interleaved with eager Trainer.step calls and an lr change keep
     one step count and the current lr: replay, step, replay (lr halved), step == four eager steps
