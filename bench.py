@@ -514,7 +514,10 @@ def main():
                     help="small-batch configs: replay each step as one captured hipGraph instead of issuing its "
                          "launches (the same sequence) eagerly — slower on the MI355X host (DESIGN.md §3x)")
     ap.add_argument("--buckets", type=int, default=1,
-                    help="N>1: the flat gradient all-reduced as this many async pieces")
+                    help="N>1 with --no-overlap: the flat gradient all-reduced as this many async pieces")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: all-reduce the whole gradient after the backward instead of the early range "
+                         "[rmp.1.kernel, end) during it (Trainer.reduce_split)")
     args = ap.parse_args()
     if args.infer:
         args.config = 5
@@ -555,7 +558,8 @@ def run_train(args, cfg, world, rank, device):
     params = P.to_flat(P.glorot_uniform(0), device=device)
     if world > 1:
         dist.broadcast(params, 0)
-    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math, buckets=args.buckets)
+    trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math, buckets=args.buckets,
+                      overlap=not args.no_overlap)
     step_in = ((batches[0], targets[0]) if len(batches) == 1 else (batches, targets)) + (n_global,)
     n_micro = len(batches)
     for _ in range(args.warmup):
@@ -582,6 +586,9 @@ def run_train(args, cfg, world, rank, device):
     # the line separates the collective (RCCL over xGMI) from the compute
     ar_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
              for _ in range(args.steps)] if world > 1 else None
+    # ... and, when the step overlaps (Trainer.reduce_split), the early piece's all-reduce on its side stream
+    ar_early = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.steps)] if world > 1 and trainer._split() else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -591,6 +598,8 @@ def run_train(args, cfg, world, rank, device):
         evs = ev.ev[per * k: per * (k + 1)]
         if ar_ev:
             trainer.ar_events = ar_ev[k]
+        if ar_early:
+            trainer.ar_early_events = ar_early[k]
         if n_micro == 1:
             trainer.prof_kernel, trainer.prof_events = kid, evs
             out3 = trainer.step(*step_in)
@@ -601,7 +610,7 @@ def run_train(args, cfg, world, rank, device):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    trainer.prof_kernel, trainer.prof_events, trainer.ar_events = 0, None, None
+    trainer.prof_kernel, trainer.prof_events, trainer.ar_events, trainer.ar_early_events = 0, None, None, None
     allreduce = None
     if ar_ev:
         ar_ms = [a.elapsed_time(b) for a, b in ar_ev]
@@ -610,8 +619,23 @@ def run_train(args, cfg, world, rank, device):
         nbytes = params.numel() * params.element_size()
         allreduce = {"allreduce_ms": round(float(ar_t.item()), 4), "bytes": nbytes, "buckets": trainer.buckets,
                      "backend": dist.get_backend(),
-                     "note": "mean per step, max over ranks; HIP events around Trainer.allreduce on the step's "
-                             "stream (includes waiting for the slowest rank to arrive)"}
+                     "note": "mean per step, max over ranks; HIP events on the step's stream from the end of the "
+                             "backward to the gradients summed over ranks (the exposed all-reduce; includes "
+                             "waiting for the slowest rank to arrive)"}
+        if ar_early:
+            lead = [a.elapsed_time(b) for (a, _), (b, _) in zip(ar_early, ar_ev)]
+            dur = [a.elapsed_time(b) for a, b in ar_early]
+            t2 = torch.tensor([float(np.min(lead)), float(np.mean(lead)), float(np.mean(dur))], dtype=torch.float64,
+                              device=device)
+            dist.all_reduce(t2, op=dist.ReduceOp.MIN)
+            allreduce["overlap"] = {
+                "early_range_floats": int(params.numel() - trainer._early_lo),
+                "early_start_before_backward_end_ms": {"min": round(float(t2[0]), 4), "mean": round(float(t2[1]), 4)},
+                "early_piece_ms": round(float(t2[2]), 4),
+                "note": "Trainer.reduce_split: the gradients of [rmp.1.kernel, end) all-reduced on a side stream "
+                        "from the backward's early event (spwgnn_run.grads_early_event); lead = its start to the end "
+                        "of the backward (> 0: it ran while dA, the encoder backward and the encoder-side "
+                        "gradients did), min over ranks"}
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 5   /* 5: spwgnn_team_max_blocks, spwgnn_host_device_ptr; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
+#define SPWGNN_ABI_VERSION 5   /* 5: spwgnn_team_max_blocks, spwgnn_host_device_ptr, spwgnn_run.grads_early_event; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -161,6 +161,14 @@ typedef struct spwgnn_run {
     const uint64_t* seed_dev;
     /* spwgnn_forward only: work to run first (above); NULL = none. Read at call time. */
     const spwgnn_prologue* prologue;
+    /* spwgnn_backward only: a hipEvent_t (NULL = none). When set, the weight gradients are issued in
+     * two groups and this event is recorded on the call's stream as soon as the EARLY range of the
+     * flat gradient buffer is final: from the offset of "rmp.1.kernel" to the end (rmp.1, rmp.2, omp.0,
+     * omp.1 — they need only the propagation-step loop). The dA rebuild, the relation encoder's backward
+     * and the late range (rm, om, rmp.0) follow. A data-parallel caller all-reduces the early range on
+     * another stream after hipStreamWaitEvent, overlapped with the rest of the backward.
+     * Same results as without the event. */
+    void* grads_early_event;
 } spwgnn_run;
 
 /* Matrix-product arithmetic. F32 and X6 give fp32-class results:

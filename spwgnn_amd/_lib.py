@@ -46,7 +46,8 @@ class PrologueC(C.Structure):
 class RunC(C.Structure):
     _fields_ = [("mp_steps", C.c_int32), ("training", C.c_int32), ("dropout", C.c_float), ("math", C.c_int32),
                 ("seed", C.c_uint64), ("prof_kernel", C.c_int32), ("prof_count", C.c_int32),
-                ("prof_events", C.c_void_p), ("seed_dev", C.c_void_p), ("prologue", C.c_void_p)]
+                ("prof_events", C.c_void_p), ("seed_dev", C.c_void_p), ("prologue", C.c_void_p),
+                ("grads_early_event", C.c_void_p)]
 
 
 K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WGRAD_W2, K_DA = 1, 2, 3, 4, 5, 6, 7, 8

@@ -927,7 +927,23 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         enb.xh_om1t = c.x6(X6_OM1T_H);
     }
 
-    if (bwd_fused_taken(r, b)) {
+    // two weight-gradient groups (spwgnn_run.grads_early_event): the node-side and W2/W3 gradients
+    // first, the event, then dA, the relation encoder's backward and the encoder-side gradients
+    const bool split = r->grads_early_event != nullptr;
+    int32_t e = SPWGNN_OK;
+    const bool fused = bwd_fused_taken(r, b);
+    auto edge_encoder_bwd = [&]() -> int32_t {   // dA rebuild + relation encoder backward (wide kernels)
+        if (rebuild) {
+            SPW_CHECK(prof.before(SPWGNN_K_DA));
+            SPW_CHECK(launch_dA(da, kmath(r, kX6EdgeBwd), st));
+            SPW_CHECK(prof.after(SPWGNN_K_DA));
+        }
+        SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
+        SPW_CHECK(launch_enc_edge_bwd(eeb, kmath(r, kX6EncEdgeBwd), st));
+        SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
+        return SPWGNN_OK;
+    };
+    if (fused) {
         // small batch: the step loop, dA and both encoder backwards in one launch (timed as the node backward)
         BwdFusedArgs fa{};
         fa.nb = node_args(0);
@@ -966,14 +982,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             SPW_CHECK(prof.after(SPWGNN_K_EDGE_BWD));
         }
         if (dprop) SPW_CHECK(launch_node_bwd(tl, kmath(r, kX6NodeBwd), st));
-        if (rebuild) {
-            SPW_CHECK(prof.before(SPWGNN_K_DA));
-            SPW_CHECK(launch_dA(da, kmath(r, kX6EdgeBwd), st));
-            SPW_CHECK(prof.after(SPWGNN_K_DA));
-        }
-        SPW_CHECK(prof.before(SPWGNN_K_ENC_EDGE_BWD));
-        SPW_CHECK(launch_enc_edge_bwd(eeb, kmath(r, kX6EncEdgeBwd), st));
-        SPW_CHECK(prof.after(SPWGNN_K_ENC_EDGE_BWD));
+        if (!split && (e = edge_encoder_bwd())) return e;
         SPW_CHECK(prof.before(SPWGNN_K_ENC_NODE_BWD));
         SPW_CHECK(launch_enc_node_bwd(enb, kmath(r, kX6NodeBwd), st));
         SPW_CHECK(prof.after(SPWGNN_K_ENC_NODE_BWD));
@@ -987,44 +996,48 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.rows = RE; g.kx_pad = 160; g.ny_pad = 160;
         g.tk = tk; g.tb = tb; g.k_rows = kFE; g.k_row0 = 0; g.bias_row = kFE;
     };
-    int32_t e;
-    ReduceBatch rb{};
-    WsBatch wsb{};
-    WsBatch* const wsp = getenv_flag("SPWGNN_WS_UNBATCHED") ? nullptr : &wsb;   // A/B: one launch per gradient
+    ReduceBatch rb{};   // every gradient's reduction (its slab slot = its index here)
+    WsBatch wsb{}, wsb2{};   // the batched launch (split: the early group's, then the late group's)
+    const bool unbatched = getenv_flag("SPWGNN_WS_UNBATCHED");   // A/B: one launch per gradient
+    WsBatch* wsp = unbatched ? nullptr : &wsb;
     Pos3Batch p3{};
-    {   // rm.0: X = [d | 1]
+    auto wg = [&](const WgSpec& g) { return run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3); };
+    auto g_rm0 = [&]() {   // rm.0: X = [d | 1]
         WgSpec g; g.xmode = XM_EDGE_D; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 160; g.rows = RE;
         g.y = c.f(w.dz1); g.y_ld = kLdE; g.y_width = kFE; g.y_count = RE;
         g.tk = T_RM0K; g.tb = T_RM0B; g.k_rows = 2; g.bias_row = 2;
         g.b16 = b16 ? kB16Y : 0;   // Y = dz1
         if (z1_rebuilt(r)) g.xd = reinterpret_cast<const float2*>(c.f(w.ed));   // k_wgrad_pos3 reads d
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
+        return wg(g);
+    };
     // encoder layers: chunk-major activations and gradients; W1a: X = c_r (chunk-major), Y = dA (rows)
     auto cm_xy = [&](WgSpec& g) { g.xmode = XM_CM; g.ymode = YM_CM; };
-    {
-        WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g);
-        if (z1_rebuilt(r)) {
-            g.xd = reinterpret_cast<const float2*>(c.f(w.ed));
-            g.w0 = c.pk(PK_RM0);
-            g.b0 = c.pk(PB_RM0);
-        }
-        g.b16 = b16 ? kB16Y : 0;   // X rebuilt from d; Y = dz2
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
     const int b16xy = b16 ? (kB16X | kB16Y) : 0;
-    { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e; }
-    { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e; }
-    { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e; }
-    {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major A and node
-        // rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
+    auto g_rm123_w1a = [&]() -> int32_t {
+        {
+            WgSpec g; edge_row(g, w.z1, w.dz2, T_RM1K, T_RM1B); cm_xy(g);
+            if (z1_rebuilt(r)) {
+                g.xd = reinterpret_cast<const float2*>(c.f(w.ed));
+                g.w0 = c.pk(PK_RM0);
+                g.b0 = c.pk(PB_RM0);
+            }
+            g.b16 = b16 ? kB16Y : 0;   // X rebuilt from d; Y = dz2
+            if ((e = wg(g))) return e;
+        }
+        { WgSpec g; edge_row(g, w.z2, w.dz3, T_RM2K, T_RM2B); cm_xy(g); g.b16 = b16xy; if ((e = wg(g))) return e; }
+        { WgSpec g; edge_row(g, w.z3, w.dz4, T_RM3K, T_RM3B); cm_xy(g); g.b16 = b16xy; if ((e = wg(g))) return e; }
+        { WgSpec g; edge_row(g, w.cr, w.dA, T_RMP0K, T_RMP0B); g.xmode = XM_CM; g.b16 = b16xy; if ((e = wg(g))) return e; }
+        return SPWGNN_OK;
+    };
+    auto g_w2 = [&]() {   // rmp.1 (W2, b2): X = [h1 | 1], Y = dh2pre, both recomputed from the chunk-major
+        // A and node rows (U, V, G3) and the h2>0 mask, over all steps (row = s·RE + e)
         WgSpec g; edge_row(g, -1, -1, T_RMP1K, T_RMP1B);
         g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
         g.b16 = b16 ? kB16A : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
+        return wg(g);
+    };
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,
                        int yw, int kxp, int nyp) {
         g.x = c.f(xoff); g.x_ld = xld; g.x_width = xw; g.x_ones = xones; g.x_count = nN; g.x_stride = xstride;
@@ -1032,59 +1045,62 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.rows = nN * S; g.kx_pad = kxp; g.ny_pad = nyp;
         g.xmode = XM_CM; g.ymode = YM_CM;   // chunk-major node rows
     };
-    const int grp0 = wsb.n;   // W1b, W1c, omp.0 P part (X = P), omp.0 effect part (Y = do1): one group
-    {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
-        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
-        g.b16 = n16 ? kB16Y : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // rmp.0 rows 250..349 (W1c)
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
-        g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
-        g.b16 = n16 ? kB16Y : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // omp.0 rows 200..299 (P part)
-        WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // omp.0 rows 100..199 (effect part)
-        WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    if (wsp) ws_group(wsp, grp0, wsb.n - grp0);
-    {   // rmp.2 (W3, b3): X = [H2s | deg]
-        WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
-        g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
-        g.b16 = n16 ? (kB16X | kB16Y) : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
-        WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
-        g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
-        if (kmath(r, kX6NodeBwd) != MATH_F32) {   // c_oᵀ·Σ_s do1_s: Σ do1 stored by k_enc_node_bwd
-            g.y = c.f(w.dco);
-            g.rows = nN;
-            g.y_stride = 0;
+    auto g_node = [&]() -> int32_t {
+        const int grp0 = wsp ? wsp->n : 0;   // W1b, W1c, omp.0 P part (X = P), omp.0 effect part (Y = do1): one group
+        {   // rmp.0 rows 150..249 (W1b): Σ_s P_sᵀ dU_s
+            WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dU, kLdE, kFE, 128, 160);
+            g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 150;
+            g.b16 = n16 ? kB16Y : 0;
+            if ((e = wg(g))) return e;
         }
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // omp.1 (Wo2, bo2), x' column order → Keras order
-        WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
-        g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
-        g.b16 = n16 ? (kB16X | kB16Y) : 0;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // om.0: X = [y, w | 1]
+        {   // rmp.0 rows 250..349 (W1c)
+            WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.dV, kLdE, kFE, 128, 160);
+            g.tk = T_RMP0K; g.k_rows = kFN; g.k_row0 = 250;
+            g.b16 = n16 ? kB16Y : 0;
+            if ((e = wg(g))) return e;
+        }
+        {   // omp.0 rows 200..299 (P part)
+            WgSpec g; node_xy(g, w.P, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+            g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 200;
+            if ((e = wg(g))) return e;
+        }
+        {   // omp.0 rows 100..199 (effect part)
+            WgSpec g; node_xy(g, w.a, kLdN, kFN, -1, RN, w.do1, kLdN, kFN, 128, 128);
+            g.tk = T_OMP0K; g.k_rows = kFN; g.k_row0 = 100;
+            if ((e = wg(g))) return e;
+        }
+        if (wsp) ws_group(wsp, grp0, wsp->n - grp0);
+        {   // rmp.2 (W3, b3): X = [H2s | deg]
+            WgSpec g; node_xy(g, w.H2s, kLdE, kFE + 1, -1, RN, w.g, kLdN, kFN, 160, 128);
+            g.tk = T_RMP2K; g.tb = T_RMP2B; g.k_rows = kFE; g.bias_row = kDegCol;
+            g.b16 = n16 ? (kB16X | kB16Y) : 0;
+            if ((e = wg(g))) return e;
+        }
+        {   // omp.0 rows 0..99 (c_o part, broadcast over steps) + bias
+            WgSpec g; node_xy(g, w.co, kLdN, kFN, kFN, 0, w.do1, kLdN, kFN, 128, 128);
+            g.tk = T_OMP0K; g.tb = T_OMP0B; g.k_rows = kFN; g.k_row0 = 0; g.bias_row = kFN;
+            if (kmath(r, kX6NodeBwd) != MATH_F32) {   // c_oᵀ·Σ_s do1_s: Σ do1 stored by k_enc_node_bwd
+                g.y = c.f(w.dco);
+                g.rows = nN;
+                g.y_stride = 0;
+            }
+            if ((e = wg(g))) return e;
+        }
+        {   // omp.1 (Wo2, bo2), x' column order → Keras order
+            WgSpec g; node_xy(g, w.o1, kLdN, kFN, kFN, RN, w.dx, kLdN, kFN + 1, 128, 128);
+            g.tk = T_OMP1K; g.tb = T_OMP1B; g.k_rows = kFN; g.bias_row = kFN; g.perm = 1;
+            g.b16 = n16 ? (kB16X | kB16Y) : 0;
+            if ((e = wg(g))) return e;
+        }
+        return SPWGNN_OK;
+    };
+    auto g_om0 = [&]() {   // om.0: X = [y, w | 1]
         WgSpec g; g.xmode = XM_NODE_O; g.ymode = YM_CM; g.kx_pad = 32; g.ny_pad = 128; g.rows = nN;
         g.y = c.f(w.dzo1); g.y_ld = kLdN; g.y_width = kFN; g.y_count = nN;
         g.tk = T_OM0K; g.tb = T_OM0B; g.k_rows = 2; g.bias_row = 2;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    {   // om.1
+        return wg(g);
+    };
+    auto g_om1 = [&]() {   // om.1
         WgSpec g; node_xy(g, w.zo1, kLdN, kFN, kFN, 0, w.dzo2, kLdN, kFN, 128, 128);
         g.rows = nN; g.y_stride = 0;
         if (z1_rebuilt(r)) {
@@ -1093,42 +1109,54 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
             g.b0 = c.pk(PB_OM0);
         }
         g.tk = T_OM1K; g.tb = T_OM1B; g.k_rows = kFN; g.bias_row = kFN;
-        if ((e = run_wgrad(c, b, g, grads, kmath(r, kX6Wgrad), st, rb, &prof, wsp, &p3))) return e;
-    }
-    // a small batch's rm.0 / om.0 gradients join the batched launch (one dependent launch fewer)
-    const bool p3_in_batch = (wsb.n > 0 || wsb.w2_wgs > 0) && team_blocks(b->n_eblocks) && !getenv_flag("SPWGNN_NO_POS3_MERGE");
-    if (!p3_in_batch) SPW_CHECK(launch_wgrad_pos3(p3, st));
-    if (wsb.n > 0 || wsb.w2_wgs > 0) {
-        SPW_CHECK(prof.before(SPWGNN_K_WGRAD_WS));
-        SPW_CHECK(launch_wgrad_ws_batch(wsb, kmath(r, kX6Wgrad), st, p3_in_batch ? &p3 : nullptr));
-        SPW_CHECK(prof.after(SPWGNN_K_WGRAD_WS));
-    }
-    {   // the float ranges no reduction of this batch writes: alignment gaps, uncovered tensor rows.
-        // More ranges than the launch carries (kMaxZero) or no reduction at all: one memset of the
-        // whole buffer instead (stream-ordered before the reduction, which then writes its ranges)
+        return wg(g);
+    };
+    // the batched launch of `batch` (+ a small batch's rm.0 / om.0 gradients as trailing workgroups)
+    auto launch_ws = [&](WsBatch& batch, bool with_p3) -> int32_t {
+        const bool p3_in_batch = with_p3 && (batch.n > 0 || batch.w2_wgs > 0) && team_blocks(b->n_eblocks) &&
+                                 !getenv_flag("SPWGNN_NO_POS3_MERGE");
+        if (with_p3 && !p3_in_batch) SPW_CHECK(launch_wgrad_pos3(p3, st));
+        if (batch.n > 0 || batch.w2_wgs > 0) {
+            SPW_CHECK(prof.before(SPWGNN_K_WGRAD_WS));
+            SPW_CHECK(launch_wgrad_ws_batch(batch, kmath(r, kX6Wgrad), st, p3_in_batch ? &p3 : nullptr));
+            SPW_CHECK(prof.after(SPWGNN_K_WGRAD_WS));
+        }
+        return SPWGNN_OK;
+    };
+    // the reductions of the gradients whose tensors lie in [t_lo, t_hi), and the zeroing of the float
+    // ranges of those tensors no such reduction writes (alignment gaps, uncovered tensor rows). More
+    // ranges than the launch carries (kMaxZero) or no reduction: one memset of those tensors instead
+    // (stream-ordered before the reduction, which then writes its ranges)
+    auto reduce = [&](int t_lo, int t_hi) -> int32_t {
         const ParamTable& pt = param_table();
-        rb.nzero = 0;
+        const int64_t lo = pt.t[t_lo].offset, hi = t_hi < kNumTensors ? pt.t[t_hi].offset : pt.total;
+        ReduceBatch sub{};
+        for (int k = 0; k < rb.n; ++k) {
+            const int64_t off = rb.r[k].kernel_off >= 0 ? rb.r[k].kernel_off : rb.r[k].bias_off;
+            if (off >= lo && off < hi) sub.r[sub.n++] = rb.r[k];
+        }
+        sub.nzero = 0;
         bool overflow = false;
         auto zero = [&](int64_t off, int64_t len) {
             if (len <= 0) return;
-            if (rb.nzero > 0 && rb.zoff[rb.nzero - 1] + rb.zlen[rb.nzero - 1] == off) {   // merge
-                rb.zlen[rb.nzero - 1] += (int32_t)len;
-            } else if (rb.nzero < kMaxZero) {
-                rb.zoff[rb.nzero] = off;
-                rb.zlen[rb.nzero++] = (int32_t)len;
+            if (sub.nzero > 0 && sub.zoff[sub.nzero - 1] + sub.zlen[sub.nzero - 1] == off) {   // merge
+                sub.zlen[sub.nzero - 1] += (int32_t)len;
+            } else if (sub.nzero < kMaxZero) {
+                sub.zoff[sub.nzero] = off;
+                sub.zlen[sub.nzero++] = (int32_t)len;
             } else {
                 overflow = true;
             }
         };
         constexpr int kMaxRows = 512;   // the largest Keras tensor has 350 rows (rmp.0 kernel)
         uint8_t row[kMaxRows];
-        for (int t = 0; t < kNumTensors && !overflow; ++t) {
+        for (int t = t_lo; t < t_hi && !overflow; ++t) {
             const TensorDesc& d = pt.t[t];
             if (d.rows > kMaxRows) return SPWGNN_E_ARG;
             const int64_t end = t + 1 < kNumTensors ? pt.t[t + 1].offset : pt.total;
             memset(row, 0, d.rows);   // rows (kernels) or the one bias row written by some job
-            for (int k = 0; k < rb.n; ++k) {
-                const ReduceArgs& ra = rb.r[k];
+            for (int k = 0; k < sub.n; ++k) {
+                const ReduceArgs& ra = sub.r[k];
                 if (d.rows > 1 && ra.kernel_off == d.offset)
                     for (int q = 0; q < ra.kernel_rows; ++q)
                         if (ra.kernel_row0 + q < d.rows) row[ra.kernel_row0 + q] = 1;
@@ -1138,13 +1166,37 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
                 if (!row[q]) zero(d.offset + (int64_t)q * d.cols, d.cols);
             zero(d.offset + (int64_t)d.rows * d.cols, end - d.offset - (int64_t)d.rows * d.cols);
         }
-        if (overflow || (rb.n == 0 && rb.nzero > 0)) {
-            SPW_CHECK(hipMemsetAsync(grads, 0, pt.total * sizeof(float), st));
-            rb.nzero = 0;
+        if (overflow || (sub.n == 0 && sub.nzero > 0)) {
+            SPW_CHECK(hipMemsetAsync(grads + lo, 0, (hi - lo) * sizeof(float), st));
+            sub.nzero = 0;
         }
+        SPW_CHECK(launch_wgrad_reduce_all(sub, st));
+        return SPWGNN_OK;
+    };
+    if (!split) {
+        if ((e = g_rm0())) return e;
+        if ((e = g_rm123_w1a())) return e;
+        if ((e = g_w2())) return e;
+        if ((e = g_node())) return e;
+        if ((e = g_om0())) return e;
+        if ((e = g_om1())) return e;
+        if ((e = launch_ws(wsb, true))) return e;
+        return reduce(0, kNumTensors);
     }
-    SPW_CHECK(launch_wgrad_reduce_all(rb, st));
-    return SPWGNN_OK;
+    // split: the early group needs only the step loop and the node encoder's backward (Σ do1, dzo2)
+    if ((e = g_w2())) return e;
+    if ((e = g_node())) return e;
+    if ((e = g_om1())) return e;
+    if ((e = launch_ws(wsb, false))) return e;
+    if ((e = reduce(T_RMP1K, kNumTensors))) return e;
+    SPW_CHECK(hipEventRecord(static_cast<hipEvent_t>(r->grads_early_event), st));
+    if (!fused && (e = edge_encoder_bwd())) return e;
+    wsp = unbatched ? nullptr : &wsb2;
+    if ((e = g_rm0())) return e;
+    if ((e = g_om0())) return e;
+    if ((e = g_rm123_w1a())) return e;
+    if ((e = launch_ws(wsb2, true))) return e;
+    return reduce(0, T_RMP1K);
 }
 
 }  // namespace spw

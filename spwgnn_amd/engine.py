@@ -48,6 +48,7 @@ class RunConfig:
     prof_events: Optional[list] = None   # raw hipEvent_t handles, 2 per launch
     seed_dev: Optional[torch.Tensor] = None   # (1,) int64 device word holding the dropout key (replayable steps)
     prologue: Optional["Prologue"] = None      # forward only: a replayed step's upload + key/step advance
+    grads_early_event: Optional[torch.cuda.Event] = None   # backward only: spwgnn_run.grads_early_event
 
     def cstruct(self, with_prologue: bool = False) -> _lib.RunC:
         r = _lib.RunC()
@@ -68,6 +69,11 @@ class RunConfig:
             if self.seed_dev.device.type != "cuda" or self.seed_dev.dtype != torch.int64:
                 raise ValueError("seed_dev must be a (1,) int64 device tensor")
             r.seed_dev = self.seed_dev.data_ptr()
+        if self.grads_early_event is not None:
+            h = self.grads_early_event.cuda_event
+            if not h:
+                raise ValueError("grads_early_event: record the event once first (it has no hipEvent_t yet)")
+            r.grads_early_event = h
         if with_prologue and self.prologue is not None:   # spwgnn_forward only
             self._pro_c = self.prologue.cstruct()   # keep alive for the call
             r.prologue = C.cast(C.pointer(self._pro_c), C.c_void_p)

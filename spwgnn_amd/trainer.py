@@ -25,7 +25,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from . import _lib, engine as E
+from . import _lib, engine as E, params as P
 from .batch import TowerBatch
 
 
@@ -69,6 +69,15 @@ class HipEngine:
         g, _ = E.backward(params, batch, run, self.ws, dlogits, grads=self.grads)
         return g
 
+    def early_event(self):
+        """The event the library records once the early gradient range is final
+        (spwgnn_run.grads_early_event); created (recorded once) on first use."""
+        ev = getattr(self, "_early_ev", None)
+        if ev is None:
+            ev = self._early_ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))   # creates the underlying hipEvent_t
+        return ev
+
     def adam(self, params, grads, m, v, step, lr, b1, b2, eps, l2, gscale):
         E.adam(params, grads, m, v, step, lr, b1, b2, eps, l2, gscale)
 
@@ -79,7 +88,7 @@ class Trainer:
     def __init__(self, params: torch.Tensor, engine=None, mp_steps: int = E.REF_MP_STEPS,
                  dropout: float = E.REF_DROPOUT, seed: int = 0, lr: float = 5e-4, beta1: float = 0.9,
                  beta2: float = 0.999, eps: float = 1e-7, l2: float = 0.0, group=None, math: str = "x6",
-                 buckets: int = 1):
+                 buckets: int = 1, overlap: bool = True):
         self.params = params
         self.engine = engine if engine is not None else HipEngine(params.device)
         self.m = torch.zeros_like(params)
@@ -98,9 +107,26 @@ class Trainer:
         # (start, end) torch.cuda.Event pair recorded around the all-reduce (bench.py's allreduce_ms)
         self.buckets = max(1, int(buckets))
         self.ar_events = None
+        # overlap (N > 1, an engine with early_event): the backward records an event once the gradients
+        # of the flat range [rmp.1.kernel, end) are final (spwgnn_run.grads_early_event); that range is
+        # all-reduced on a side stream while dA, the encoder backward and the encoder-side gradients run
+        # (SURVEY §8e), the rest after the backward. ar_early_events: an optional (start, end) event
+        # pair recorded on the side stream around the early all-reduce (bench.py's rehearsal trace)
+        self.overlap = overlap
+        self.ar_early_events = None
+        self._side = None
+        self._early_lo = next(off for name, off, _ in P.layout() if name == "rmp.1.kernel")
         self._ctr = None          # replayed steps' device counters (replay_body)
         self._ctr_at = 0          # the host iteration count the device step word holds
         self._w3 = {}             # (n_nodes, 1, 1) fp64 weights of a micro-batch's [loss, correct, n]
+
+    def _early(self, run):
+        """Overlapped steps: the engine's early-gradient event, handed to the backward through `run`."""
+        if not self._split():
+            return None
+        ev = self.engine.early_event()
+        run.grads_early_event = ev
+        return ev
 
     def run_config(self, micro: int = 0) -> E.RunConfig:
         # distinct dropout keys per step, per rank and per micro-batch (different towers)
@@ -176,6 +202,54 @@ class Trainer:
         if ev is not None:
             ev[1].record()
 
+    def _split(self) -> bool:
+        return self.world > 1 and self.overlap and hasattr(self.engine, "early_event")
+
+    def _combine(self, acc, g, w, sl, first):
+        """acc[sl] ← w·g[sl] (first micro-batch) or acc[sl] + w·g[sl]; acc may be g itself."""
+        if first:
+            if acc is g:
+                if w != 1.0:
+                    acc[sl].mul_(w)
+            else:
+                torch.mul(g[sl], w, out=acc[sl])
+        else:
+            acc[sl].add_(g[sl], alpha=w)
+
+    def reduce_split(self, acc, g, w, first, ev):
+        """The last backward's gradient `g` folded into `acc` (weight w) and the sum over ranks, in two
+        pieces: the early range [rmp.1.kernel, end) on a side stream that waits for `ev` (the library
+        records it mid-backward), issued before the late range [0, rmp.1.kernel) on the step's stream.
+        Elementwise the same arithmetic as `allreduce` after the whole backward."""
+        lo = self._early_lo
+        early, late = slice(lo, acc.numel()), slice(0, lo)
+        cuda = acc.is_cuda
+        cur = torch.cuda.current_stream(acc.device) if cuda else None
+        if cuda:
+            if self._side is None:
+                self._side = torch.cuda.Stream(acc.device)
+            self._side.wait_event(ev)
+            ctx = torch.cuda.stream(self._side)
+        else:
+            import contextlib
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if self.ar_early_events is not None:
+                self.ar_early_events[0].record()
+            self._combine(acc, g, w, early, first)
+            work = dist.all_reduce(acc[early], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._combine(acc, g, w, late, first)
+        if self.ar_events is not None:
+            self.ar_events[0].record()
+        dist.all_reduce(acc[late], op=dist.ReduceOp.SUM, group=self.group)
+        work.wait()   # the step's stream (CUDA) / the host (CPU tensors) waits for the early piece
+        if cuda:
+            if self.ar_early_events is not None:
+                self.ar_early_events[1].record(self._side)
+            cur.wait_stream(self._side)
+        if self.ar_events is not None:
+            self.ar_events[1].record()
+
     def replay_step(self, rs, plan, target):
         """One replayed optimizer step (rs: a ReplayStep/ReplayCache over `replay_body`): the
         device words are first brought to the host's counters (a `step()` may have run in
@@ -211,12 +285,16 @@ class Trainer:
             z = self.engine.forward(self.params, b, run)
             out3, dz = self.engine.loss(z, tg)
             res = out3.clone()          # the engine reuses its out3 buffer
+            ev = self._early(run)
             acc = self.engine.backward(self.params, b, run, dz)
             w = b.n_nodes / n_global
-            if w != 1.0:
-                acc.mul_(w)
-            if self.world > 1:
-                self.allreduce(acc)
+            if ev is not None:
+                self.reduce_split(acc, acc, w, True, ev)
+            else:
+                if w != 1.0:
+                    acc.mul_(w)
+                if self.world > 1:
+                    self.allreduce(acc)
             self.iterations += 1
             self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
                              self.l2, 1.0)
@@ -237,8 +315,19 @@ class Trainer:
                 self._w3.pop(next(iter(self._w3)))
             w3 = out3.double() * wt
             tot3 = w3 if tot3 is None else tot3 + w3
+            last = i == len(batches) - 1
+            ev = self._early(run) if last else None
             g = self.engine.backward(self.params, b, run, dz)
             w = b.n_nodes / n_global
+            if ev is not None:   # the last micro-batch: accumulate and reduce in two pieces
+                if acc is None:
+                    if getattr(self, "_acc", None) is None or self._acc.shape != g.shape or self._acc.device != g.device:
+                        self._acc = torch.empty_like(g)
+                    acc = self._acc
+                    self.reduce_split(acc, g, w, True, ev)
+                else:
+                    self.reduce_split(acc, g, w, False, ev)
+                continue
             if acc is None:
                 # the engine writes every backward into one buffer (HipEngine.grads), so the sum lives in
                 # a buffer of its own: the Trainer's persistent accumulator, overwritten here
@@ -247,7 +336,7 @@ class Trainer:
                 acc = torch.mul(g, w, out=self._acc)
             else:
                 acc.add_(g, alpha=w)
-        if self.world > 1:
+        if self.world > 1 and not self._split():
             self.allreduce(acc)
         self.iterations += 1
         self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,

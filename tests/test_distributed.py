@@ -60,6 +60,16 @@ class OracleEngine:
         params.sub_(lr_t * m / (torch.sqrt(v) + eps))
 
 
+class OverlapOracleEngine(OracleEngine):
+    """The oracle engine with an early-gradient 'event' (a CPU step is synchronous: it is reached when
+    backward returns), so the Trainer takes its overlapped two-piece all-reduce (reduce_split)."""
+    calls = 0
+
+    def early_event(self):
+        OverlapOracleEngine.calls += 1
+        return "reached"
+
+
 def _problem(B=8, N=5):
     obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, N, seed=9, fully_connected=False)
     return obj, Rs, Rr, tgt
@@ -77,14 +87,16 @@ def _single(steps):
     return params.numpy()
 
 
-def _worker(rank, world, port, steps, out, buckets=1):
+def _worker(rank, world, port, steps, out, buckets=1, overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     obj, Rs, Rr, tgt = _problem()
     sh = slice(rank * 4, rank * 4 + 4)                      # tower shard of this rank
     batch = TowerBatch.from_dense(obj[sh], Rs[sh], Rr[sh], device="cpu")
     params = P.to_flat(O.random_params(11), dtype=torch.float64)
-    tr = Trainer(params, engine=OracleEngine(), mp_steps=3, dropout=0.0, buckets=buckets)
+    eng = OverlapOracleEngine() if overlap else OracleEngine()
+    tr = Trainer(params, engine=eng, mp_steps=3, dropout=0.0, buckets=buckets)
+    assert tr._split() == overlap
     tr.m = torch.zeros_like(params)
     tr.v = torch.zeros_like(params)
     assert tr.world == world
@@ -94,6 +106,7 @@ def _worker(rank, world, port, steps, out, buckets=1):
         assert all(x[1] == y[0] and x[1] % 64 == 0 for x, y in zip(bb[:-1], bb[1:]))
     for _ in range(steps):
         tr.step(batch, torch.tensor(tgt[sh].reshape(-1), dtype=torch.float64))
+    assert OverlapOracleEngine.calls == (steps if overlap else 0)
     if rank == 0:
         np.save(out, params.numpy())
     dist.barrier()
@@ -125,6 +138,15 @@ def test_dp_gloo_world2_split_buckets_equal_full_batch(tmp_path, buckets):
     out = str(tmp_path / "p.npy")
     mp.start_processes(_worker, args=(2, _free_port(), 3, out, buckets), nprocs=2, join=True,
                        start_method="spawn")
+    assert np.abs(np.load(out) - _single(3)).max() < 1e-9
+
+
+def test_dp_gloo_world2_overlapped_allreduce_equals_full_batch(tmp_path):
+    """SURVEY §8e / VERDICT r5 item 7: the gradient all-reduced in two pieces — the early range
+    [rmp.1.kernel, end) issued first (async), the encoder-side rest after the backward — equals the
+    single-process full batch to 1e-9 over 3 steps."""
+    out = str(tmp_path / "p.npy")
+    mp.start_processes(_worker, args=(2, _free_port(), 3, out, 1, True), nprocs=2, join=True, start_method="spawn")
     assert np.abs(np.load(out) - _single(3)).max() < 1e-9
 
 
@@ -175,10 +197,11 @@ def _ragged_worker(rank, world, port, steps, out, mode):
         n_global = None
     a, b = ranges[rank]
     params = P.to_flat(O.random_params(11), dtype=torch.float64)
-    tr = Trainer(params, engine=OracleEngine(), mp_steps=2, dropout=0.0)
+    tr = Trainer(params, engine=OverlapOracleEngine() if mode == "micro_overlap" else OracleEngine(), mp_steps=2,
+                 dropout=0.0)
     tr.m = torch.zeros_like(params)
     tr.v = torch.zeros_like(params)
-    if mode == "micro":                     # this rank's shard as micro-batches of ≤ 2 towers
+    if mode.startswith("micro"):                     # this rank's shard as micro-batches of ≤ 2 towers
         mbs = micro_batches(a, b, 2)
         bs = [_ragged_batch(objs, raws, x, y) for x, y in mbs]
         ts = [torch.tensor(np.concatenate(tgts[x:y])) for x, y in mbs]
@@ -194,7 +217,7 @@ def _ragged_worker(rank, world, port, steps, out, mode):
 
 
 @pytest.mark.parametrize("world,mode", [(2, "planned"), (2, "unequal"), (4, "planned"), (4, "unequal"),
-                                        (2, "micro")])
+                                        (2, "micro"), (2, "micro_overlap")])
 def test_dp_gloo_ragged_unequal_shards_equal_full_batch(tmp_path, world, mode):
     out = str(tmp_path / "p.npy")
     mp.start_processes(_ragged_worker, args=(world, _free_port(), 2, out, mode), nprocs=world, join=True,
