@@ -73,6 +73,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_plan_size": (i32, [i32, vp, vp, i32, C.POINTER(PlanSizes)]),
         "spwgnn_plan_fill": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
         "spwgnn_plan_size_cap": (i32, [i32, vp, vp, i32, C.POINTER(PlanSizes)]),
+        "spwgnn_plan_order": (i32, [i32, vp, vp, i32, vp]),
         "spwgnn_plan_fill_cap": (i32, [i32, vp, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),
         "spwgnn_plan_size_recv": (i32, [i32, vp, i32, C.POINTER(PlanSizes)]),
         "spwgnn_plan_fill_recv": (i32, [i32, vp, vp, vp, vp, i32, C.POINTER(PlanSizes), vp, vp, vp, vp, vp]),

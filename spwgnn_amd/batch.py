@@ -67,6 +67,38 @@ def upload(arrays, device) -> list:
     return out
 
 
+def pack_order(tower_nodes, tower_edges, nw_max: int = 16) -> np.ndarray:
+    """spwgnn_plan_order: a tower order that packs a ragged batch into fewer 32-edge blocks (towers by
+    decreasing edge count into the wave-tile whose last block has room; include/spwgnn.h)."""
+    tn = np.ascontiguousarray(tower_nodes, dtype=np.int32)
+    te = np.ascontiguousarray(tower_edges, dtype=np.int32)
+    order = np.zeros(len(tn), np.int32)
+    if len(tn):
+        _lib.check(_lib.lib().spwgnn_plan_order(len(tn), _ptr(tn), _ptr(te), int(nw_max), _ptr(order)), "plan_order")
+    return order
+
+
+def reorder_towers(pos, tower_nodes, src, dst, tower_edges, order, prop=None):
+    """The towers of a compact edge-form batch in `order` (order[k] = the k-th tower): node rows,
+    edges (node ids rebased), counts. Returns (pos, tower_nodes, src, dst, tower_edges, prop, node_perm)
+    with node_perm[i] = the input-order index of node i of the reordered batch."""
+    tn = np.asarray(tower_nodes, np.int64)
+    te = np.asarray(tower_edges, np.int64)
+    order = np.asarray(order, np.int64)
+    noff = np.concatenate([[0], np.cumsum(tn)])
+    eoff = np.concatenate([[0], np.cumsum(te)])
+    node_perm = np.concatenate([np.arange(noff[t], noff[t + 1]) for t in order]) if len(order) else np.zeros(0, np.int64)
+    edge_perm = np.concatenate([np.arange(eoff[t], eoff[t + 1]) for t in order]) if len(order) else np.zeros(0, np.int64)
+    new_noff = np.concatenate([[0], np.cumsum(tn[order])])
+    shift = np.repeat(new_noff[:-1] - noff[order], te[order])     # per reordered edge: old → new node base
+    src = np.asarray(src, np.int64)[edge_perm] + shift
+    dst = np.asarray(dst, np.int64)[edge_perm] + shift
+    pos = np.asarray(pos)[node_perm]
+    prop = None if prop is None else np.asarray(prop).reshape(int(noff[-1]), -1)[node_perm]
+    return (pos, tn[order].astype(np.int32), src.astype(np.int32), dst.astype(np.int32), te[order].astype(np.int32),
+            prop, node_perm)
+
+
 @dataclass
 class HostPlan:
     """A batch's host-side arrays in upload order (pos4, node_tower, node_local, wtile, edge_src,
@@ -85,6 +117,7 @@ class HostPlan:
     has_prop: bool
     arrays: list
     flags: int = 0     # spwgnn_batch.flags (_lib.BATCH_RECV_BLOCKS: a receiver-block plan)
+    node_perm: Optional[np.ndarray] = None   # packed plans: node i of the plan = input node node_perm[i]
 
     @property
     def geometry(self) -> tuple:
@@ -94,11 +127,28 @@ class HostPlan:
 
     @staticmethod
     def build(pos, tower_nodes, src, dst, tower_edges, prop=None, nw_max=None, node_shape=None, tower_ids=None,
-              edge_cap=None, recv_blocks=None) -> "HostPlan":
+              edge_cap=None, recv_blocks=None, pack: bool = False) -> "HostPlan":
         """recv_blocks: one 32-edge block per node holding its in-edges (spwgnn_plan_fill_recv; the x6
         edge forward then sums a node's messages as a column sum). None = automatic: for wave-tiles of
         more than 16 nodes whose blocks would be ≥ 80 % full (large, densely connected towers —
-        BASELINE config 5), never with edge_cap."""
+        BASELINE config 5), never with edge_cap.
+        pack: plan the towers in spwgnn_plan_order's order (ragged batches: fewer, fuller blocks). Each
+        tower keeps its id (dropout key) and `node_perm` maps the plan's node rows back to the input's:
+        logits and d/d'propagation' come out in plan order (TowerBatch.to_input_order), targets go in
+        in plan order (TowerBatch.to_plan_order)."""
+        if pack:
+            tn0 = np.asarray(tower_nodes, np.int32)
+            if nw_max is None:
+                nw_max = default_nw_max(int(tn0.max()) if len(tn0) else 1, len(tn0))
+            order = pack_order(tn0, tower_edges, min(int(nw_max), 16) if int(tn0.max()) <= 16 else int(nw_max))
+            tid0 = np.arange(len(tn0), dtype=np.int64) if tower_ids is None else np.asarray(tower_ids, np.int64)
+            pos, tower_nodes, src, dst, tower_edges, prop, perm = reorder_towers(pos, tn0, src, dst, tower_edges, order,
+                                                                                prop)
+            cap = None if edge_cap is None else np.broadcast_to(np.asarray(edge_cap, np.int32), (len(tn0),))[order]
+            plan = HostPlan.build(pos, tower_nodes, src, dst, tower_edges, prop, nw_max, None, tid0[order], cap,
+                                  recv_blocks)
+            plan.node_perm = perm
+            return plan
         L = _lib.lib()
         tower_nodes = np.ascontiguousarray(tower_nodes, dtype=np.int32)
         tower_edges = np.ascontiguousarray(tower_edges, dtype=np.int32)
@@ -188,7 +238,29 @@ class TowerBatch:
     edge_id: np.ndarray              # (n_eblocks*32,) original edge index or -1
     node_shape: Optional[tuple] = None   # (B, N) when built from a uniform-N dense batch
     flags: int = 0                       # spwgnn_batch.flags (the plan's layout)
+    node_perm: Optional[np.ndarray] = None   # packed plans (HostPlan.build pack=True): plan node i = input node node_perm[i]
     _cstruct: Optional[_lib.BatchC] = field(default=None, repr=False)
+
+    def to_plan_order(self, x):
+        """Per-node rows (targets, propagation) in the input's node order → the plan's (identity
+        unless the plan was packed). numpy or torch, first axis = nodes."""
+        if self.node_perm is None:
+            return x
+        if isinstance(x, torch.Tensor):
+            return x[torch.as_tensor(self.node_perm, device=x.device)]
+        return np.asarray(x)[self.node_perm]
+
+    def to_input_order(self, x):
+        """Per-node results (logits, d/d'propagation') in the plan's node order → the input's."""
+        if self.node_perm is None:
+            return x
+        if isinstance(x, torch.Tensor):
+            out = torch.empty_like(x)
+            out[torch.as_tensor(self.node_perm, device=x.device)] = x
+            return out
+        out = np.empty_like(np.asarray(x))
+        out[self.node_perm] = x
+        return out
 
     @property
     def n_edges(self) -> int:
@@ -208,7 +280,7 @@ class TowerBatch:
     @staticmethod
     def from_edges(pos: np.ndarray, tower_nodes, src, dst, tower_edges, prop=None, device="cuda",
                    nw_max: Optional[int] = None, node_shape=None, tower_ids=None, edge_cap=None,
-                   recv_blocks=None) -> "TowerBatch":
+                   recv_blocks=None, pack: bool = False) -> "TowerBatch":
         """pos (Nn, >=3) objects rows (already /170); towers are consecutive node ranges;
         edges tower-major with global node ids. `tower_ids` (T,): each tower's index in the batch it
         was cut from (the dropout masks are keyed by it), so a shard or micro-batch of a larger batch
@@ -216,7 +288,7 @@ class TowerBatch:
         each tower's blocks for that many edges (spwgnn_plan_fill_cap) so same-shape batches share
         one plan geometry (replayed hipGraph steps); default: the actual edge counts."""
         plan = HostPlan.build(pos, tower_nodes, src, dst, tower_edges, prop, nw_max, node_shape, tower_ids, edge_cap,
-                              recv_blocks)
+                              recv_blocks, pack)
         return TowerBatch.from_plan(plan, device)
 
     @staticmethod
@@ -229,7 +301,7 @@ class TowerBatch:
         prop_t = d[7] if m.has_prop else None
         return TowerBatch(m.n_towers, m.n_nodes, m.tower_nodes, m.tower_edges, m.src, m.dst, m.n_wtiles, m.n_eblocks,
                           m.nw_max, dev, d[0], prop_t, d[1], d[2], d[3], d[4], d[5], d[6], m.edge_id, m.node_shape,
-                          m.flags)
+                          m.flags, m.node_perm)
 
     @staticmethod
     def from_dense(objects, sender_relations, receiver_relations, propagation=None, device="cuda",

@@ -163,6 +163,63 @@ static int32_t plan_pack(int32_t n_towers, const int32_t* tower_nodes, const int
     return SPWGNN_OK;
 }
 
+// A tower order that packs ragged towers into fewer 32-edge blocks (spwgnn_plan_order). Towers are
+// placed by decreasing edge count; each joins the open wave-tile whose last block its edges fit
+// without a new block (the tightest such slot, then the tightest node fit), else opens a new tile.
+// The order lists each tile's towers consecutively, tiles in opening order, so plan_pack's in-order
+// packing rebuilds those tiles or merges neighbours — never more blocks: ceil(a+b) <= ceil(a)+ceil(b).
+static int32_t plan_order_impl(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,
+                               int32_t nw_max, int32_t* order) {
+    if (n_towers < 0 || (n_towers > 0 && (!tower_nodes || !tower_edges || !order)) || nw_max < 1 ||
+        nw_max > kNwMaxLimit)
+        return SPWGNN_E_ARG;
+    std::vector<int32_t> by_edges(n_towers);
+    for (int32_t t = 0; t < n_towers; ++t) {
+        if (tower_nodes[t] < 1 || tower_nodes[t] > nw_max) return SPWGNN_E_SHAPE;
+        if (tower_edges[t] < 0) return SPWGNN_E_ARG;
+        by_edges[t] = t;
+    }
+    std::stable_sort(by_edges.begin(), by_edges.end(),
+                     [&](int32_t a, int32_t b) { return tower_edges[a] > tower_edges[b]; });
+    // open tiles by (free nodes, free slots of the last block): stacks of tile ids
+    constexpr int kSlots = 32;
+    std::vector<std::vector<int32_t>> open((size_t)(nw_max + 1) * (kSlots + 1));
+    auto key = [&](int nf, int sf) { return (size_t)nf * (kSlots + 1) + sf; };
+    std::vector<int32_t> tile_nodes, tile_edges;
+    std::vector<std::vector<int32_t>> tile_towers;
+    for (const int32_t t : by_edges) {
+        const int n = tower_nodes[t], e = tower_edges[t];
+        int tid = -1;
+        if (e <= kSlots) {
+            for (int sf = e; sf <= kSlots && tid < 0; ++sf)
+                for (int nf = n; nf <= nw_max; ++nf) {
+                    std::vector<int32_t>& b = open[key(nf, sf)];
+                    if (!b.empty()) {
+                        tid = b.back();
+                        b.pop_back();
+                        break;
+                    }
+                }
+        }
+        if (tid < 0) {
+            tid = (int32_t)tile_nodes.size();
+            tile_nodes.push_back(0);
+            tile_edges.push_back(0);
+            tile_towers.emplace_back();
+        }
+        tile_nodes[tid] += n;
+        tile_edges[tid] += e;
+        tile_towers[tid].push_back(t);
+        const int nb = std::max(1, (tile_edges[tid] + kSlots - 1) / kSlots);
+        const int nf = nw_max - tile_nodes[tid], sf = nb * kSlots - tile_edges[tid];
+        if (nf > 0) open[key(nf, sf)].push_back(tid);   // a full tile takes no tower
+    }
+    int32_t k = 0;
+    for (const auto& tt : tile_towers)
+        for (const int32_t t : tt) order[k++] = t;
+    return SPWGNN_OK;
+}
+
 static int32_t plan_size_impl(int32_t n_towers, const int32_t* tower_nodes, const int32_t* blk_edges,
                               int32_t nw_max, spwgnn_plan_sizes* out) {
     if (!out) return SPWGNN_E_ARG;
@@ -345,6 +402,11 @@ int32_t spwgnn_plan_fill_recv(int32_t n_towers, const int32_t* tower_nodes, cons
                               uint8_t* blk_csr) {
     return plan_fill_recv_impl(n_towers, tower_nodes, tower_edges, src, dst, nw_max, sizes, wtile, edge_src, edge_dst,
                                edge_id, blk_csr);
+}
+
+int32_t spwgnn_plan_order(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges, int32_t nw_max,
+                          int32_t* order) {
+    return plan_order_impl(n_towers, tower_nodes, tower_edges, nw_max, order);
 }
 
 int32_t spwgnn_plan_size(int32_t n_towers, const int32_t* tower_nodes, const int32_t* tower_edges,

@@ -151,9 +151,12 @@ def test_config3_tile_shape_wide_kernels_gradients():
     _check(f"N=12 fc x{n_keep} x6 (wide kernels)", got, ref)
 
 
-def test_ragged_thresholded_wide_kernels_gradients():
+@pytest.mark.parametrize("pack", [False, True])
+def test_ragged_thresholded_wide_kernels_gradients(pack):
     """Config 4's towers (4–16 boxes, relations thresholded at 170 px, main.py:71-81) at 2,500 kept
-    towers, above the team limit on both sides, x6 math, S = 5."""
+    towers, above the team limit on both sides, x6 math, S = 5 — in the input's tower order and packed
+    (spwgnn_plan_order, as the bench plans config 4: targets in, logits out through the plan's node
+    order)."""
     S, n_keep = 5, 2500
     params = O.random_params(44)
     pos, sizes, src, dst, te, _ = D.ragged_batch(5000, 4, 16, seed=9)
@@ -161,13 +164,15 @@ def test_ragged_thresholded_wide_kernels_gradients():
     kpos, ksz, ksrc, kdst, kte, _, _ = _slice(pos, sizes, src, dst, te, keep)
     n = int(ksz.sum())
     tgt = np.random.default_rng(12).integers(0, 2, size=n).astype(np.float32)
-    batch = TowerBatch.from_edges(kpos, ksz, ksrc, kdst, kte, device="cuda")
+    batch = TowerBatch.from_edges(kpos, ksz, ksrc, kdst, kte, device="cuda", pack=pack)
     assert batch.n_eblocks > TEAM_LIMIT and (n + 31) // 32 > TEAM_LIMIT
     assert len(np.unique(ksz)) == 13 and (kte < ksz * (ksz - 1)).any()
-    got = _engine(params, batch, tgt, S, "x6")
+    assert (batch.node_perm is not None) == pack
+    z, loss, g = _engine(params, batch, batch.to_plan_order(tgt), S, "x6")
+    got = (batch.to_input_order(z), loss, g)
     ref = O.loss_and_grads(params, kpos, None, None, np.zeros((n, 100)), tgt, S, form="gather",
                            src=ksrc.astype(np.int64), dst=kdst.astype(np.int64))
-    _check(f"ragged 4-16 thresholded x{n_keep} x6", got, ref)
+    _check(f"ragged 4-16 thresholded x{n_keep} x6 pack={pack} ({batch.n_eblocks} blocks)", got, ref)
 
 
 # tools/ht_probe.py's nine shapes: (towers, N, fully connected, S, seed)
@@ -262,3 +267,36 @@ def test_backward_with_early_gradient_event_is_bitwise_equal(n_towers, math):
         out.append((g, dp))
     assert torch.isfinite(out[1][0]).all()
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("math", ["x6", "bf16"])
+def test_packed_ragged_plan_equals_input_order(math):
+    """The bench's config 4 plan (towers in spwgnn_plan_order's order, 14 % fewer blocks) against the
+    same 3,000 towers in input order, training with dropout 0.1 (each tower keeps its id, so its masks):
+    logits back in input order and every gradient agree to rounding — x6 at the fp32 level; bf16, whose
+    operand rounding turns a changed summation grouping into bf16-ulp steps, within 1 % relative L2."""
+    params = O.random_params(8)
+    pos, sizes, src, dst, te, _ = D.ragged_batch(3000, 4, 16, seed=5)
+    n = int(sizes.sum())
+    tgt = np.random.default_rng(4).integers(0, 2, size=n).astype(np.float32)
+    flat = P.to_flat(params, device="cuda")
+    res = []
+    for pack in (False, True):
+        b = TowerBatch.from_edges(pos, sizes, src, dst, te, device="cuda", pack=pack)
+        ws = E.Workspace("cuda")
+        run = E.RunConfig(5, training=True, math=math, dropout=0.1, seed=99)
+        z = E.forward(flat, b, run, ws)
+        out3, dz = E.bce(z, torch.as_tensor(b.to_plan_order(tgt), device="cuda"), E.BceScratch("cuda"))
+        g, _ = E.backward(flat, b, run, ws, dz)
+        torch.cuda.synchronize()
+        res.append((b.n_eblocks, b.to_input_order(z.cpu().numpy()), float(out3[0]), P.from_flat(g)))
+    (nb0, z0, l0, g0), (nb1, z1, l1, g1) = res
+    assert nb1 < 0.9 * nb0
+    if math == "x6":
+        assert np.abs(z1 - z0).max() <= 2e-6 and abs(l1 - l0) <= 1e-6
+        for k in g0:
+            assert np.abs(g1[k] - g0[k]).max() <= 2e-6 * np.abs(g0[k]).max(), k
+    else:
+        assert np.abs(z1 - z0).max() <= 2e-2 and abs(l1 - l0) <= 1e-3
+        for k in g0:
+            assert np.linalg.norm(g1[k] - g0[k]) <= 1e-2 * np.linalg.norm(g0[k]), k

@@ -583,3 +583,41 @@ def test_team_limit_is_a_runtime_setting():
         assert E.fused_path(batch, run) == 0
     assert E.team_max_blocks() == 512
     assert E.team_max_blocks(7) == 512 and E.team_max_blocks(512) == 7
+
+
+def test_packed_tower_order_fills_blocks():
+    """spwgnn_plan_order (ABI 5): a permutation, deterministic; planned in that order a ragged batch never
+    needs more 32-edge blocks than in its own order, and BASELINE config 4's ragged 4-16-box thresholded
+    towers fill >= 75 % of their blocks (67 % in input order); node rows, edges and tower ids follow."""
+    from spwgnn_amd.batch import HostPlan, pack_order
+    pos, sizes, src, dst, te, _ = D.ragged_batch(8192, 4, 16, seed=4000)
+    o = pack_order(sizes, te, 16)
+    assert np.array_equal(np.sort(o), np.arange(len(sizes))) and np.array_equal(o, pack_order(sizes, te, 16))
+    a = HostPlan.build(pos, sizes, src, dst, te)
+    b = HostPlan.build(pos, sizes, src, dst, te, pack=True)
+    assert b.n_eblocks <= a.n_eblocks and len(src) / (32 * b.n_eblocks) >= 0.75 > len(src) / (32 * a.n_eblocks)
+    perm = b.node_perm
+    assert np.array_equal(np.sort(perm), np.arange(len(pos)))
+    assert np.array_equal(b.arrays[0][:, :3], pos[perm])          # node rows in plan order
+    # every edge of the packed batch is an input edge, rebased: (perm[s], perm[d]) in the input's set
+    inp = set(zip(src.tolist(), dst.tolist()))
+    assert all((int(perm[s]), int(perm[d])) in inp for s, d in zip(b.src, b.dst)) and len(b.src) == len(src)
+    # each node keeps its tower id (the dropout key) and its index inside the tower
+    tower_of = np.repeat(np.arange(len(sizes)), sizes)
+    assert np.array_equal(b.arrays[1], tower_of[perm])
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    assert np.array_equal(b.arrays[2], perm - starts[tower_of[perm]])
+    # random small ragged batches: never more blocks
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        T = int(rng.integers(1, 200))
+        tn = rng.integers(1, 17, T).astype(np.int32)
+        tev = np.array([rng.integers(0, n * (n - 1) + 1) for n in tn], np.int32)
+        sz = _lib.PlanSizes()
+        L = _lib.lib()
+        L.spwgnn_plan_size(T, tn.ctypes.data, tev.ctypes.data, 16, C.byref(sz))
+        n0 = sz.n_eblocks
+        oo = pack_order(tn, tev, 16)
+        tn2, te2 = np.ascontiguousarray(tn[oo]), np.ascontiguousarray(tev[oo])
+        L.spwgnn_plan_size(T, tn2.ctypes.data, te2.ctypes.data, 16, C.byref(sz))
+        assert sz.n_eblocks <= n0
