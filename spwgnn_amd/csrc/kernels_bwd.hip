@@ -720,6 +720,12 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 #ifndef SPWGNN_DA_INTERLEAVE
 #define SPWGNN_DA_INTERLEAVE 1
 #endif
+// The 8 waves of a workgroup take neighbouring blocks (interleave); LOCKSTEP adds a workgroup barrier
+// after each round of 8 blocks so they stay at the same (block round, step): blocks of one tile then
+// gather the same receiver rows at the same time (L1/L2 hits) instead of drifting apart
+#ifndef SPWGNN_DA_LOCKSTEP
+#define SPWGNN_DA_LOCKSTEP 1
+#endif
 // N16 (bf16 math, §3g node side): dU, dV stored as bf16
 template <bool ACCUM, bool NODA = false, int NP = 3, int DBG = 0, bool N16 = false>   // DBG 3 (diagnosis): G3 rows of the tile's first node
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
@@ -970,6 +976,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     constexpr int kStride = kWaves;
     const int perw = ((a.n_eblocks + gridDim.x - 1) / gridDim.x + kWaves - 1) / kWaves * kWaves;
     const int b0 = blockIdx.x * perw + wave, b1 = min(blockIdx.x * perw + perw, a.n_eblocks);
+    // block rounds of this workgroup (wave 0 has the most) and of this wave
+    const int wg_b0 = blockIdx.x * perw;
+    const int rounds = SPWGNN_DA_LOCKSTEP ? max(0, (b1 - wg_b0 + kWaves - 1) / kWaves) : 0;
+    const int mine = SPWGNN_DA_LOCKSTEP ? max(0, (b1 - b0 + kWaves - 1) / kWaves) : 0;
 #else
     // a contiguous range of blocks per wave: a tower's blocks (same receiver rows) stay on one CU
     constexpr int kStride = 1;
@@ -977,7 +987,18 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int per = (a.n_eblocks + nw - 1) / nw;
     const int b0 = gw * per, b1 = min(b0 + per, a.n_eblocks);
 #endif
+#if SPWGNN_DA_INTERLEAVE && SPWGNN_DA_LOCKSTEP
+    // every wave passes `rounds` barriers: one per block it sums, the rest after its last block
+    auto tail_barriers = [&](int done) {
+        for (int k = done; k < rounds; ++k) __syncthreads();
+    };
+    if (b0 >= b1) {
+        tail_barriers(0);
+        return;
+    }
+#else
     if (b0 >= b1) return;
+#endif
     // one (block, step) pair: its receiver row pointer (G3 of that step) and its mask words
     struct Pair { const float4* G4; uint32_t w[5], m1w[5]; };
     auto load_pair = [&](int blk, int s, int d) {
@@ -1078,6 +1099,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     for (int r = 0; r < 16; ++r) dArow[rho(r, h) * kLdE + 32 * t] = dacc[t][r];
             }
             zero_tiles(dacc);
+#if SPWGNN_DA_INTERLEAVE && SPWGNN_DA_LOCKSTEP
+            __syncthreads();   // this block round is done on every wave
+#endif
         }
         if (!has_next) break;
         blk = nblk;
@@ -1085,6 +1109,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         d = nd;
         cur = nxt;
     }
+#if SPWGNN_DA_INTERLEAVE && SPWGNN_DA_LOCKSTEP
+    tail_barriers(mine);
+#endif
 }
 
 hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st) {
