@@ -203,7 +203,9 @@ class Trainer:
             ev[1].record()
 
     def _split(self) -> bool:
-        return self.world > 1 and self.overlap and hasattr(self.engine, "early_event")
+        # any process group (a one-rank group included: its all-reduce is the identity, the choreography
+        # of events, side stream and collectives is the same as at N > 1)
+        return self.distributed and self.overlap and hasattr(self.engine, "early_event")
 
     def _combine(self, acc, g, w, sl, first):
         """acc[sl] ← w·g[sl] (first micro-batch) or acc[sl] + w·g[sl]; acc may be g itself."""
