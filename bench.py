@@ -521,6 +521,9 @@ def main():
                          "launches (the same sequence) eagerly — slower on the MI355X host (DESIGN.md §3x)")
     ap.add_argument("--buckets", type=int, default=1,
                     help="N>1 with --no-overlap: the flat gradient all-reduced as this many async pieces")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group at one rank too (RCCL on the box's one GPU: the N>1 "
+                         "step's collectives and overlap, over an identity all-reduce)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: all-reduce the whole gradient after the backward instead of the early range "
                          "[rmp.1.kernel, end) during it (Trainer.reduce_split)")
@@ -546,7 +549,7 @@ def main():
     backend = os.environ.get("SPWGNN_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    if world > 1 or args.dist:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -562,7 +565,8 @@ def run_train(args, cfg, world, rank, device):
     S, math = cfg["S"], cfg["math"]
     batches, targets, n_global = make_workload(cfg, rank, device, world)
     params = P.to_flat(P.glorot_uniform(0), device=device)
-    if world > 1:
+    dp = dist.is_available() and dist.is_initialized()   # a process group (N > 1, or --dist at one rank)
+    if dp:
         dist.broadcast(params, 0)
     trainer = Trainer(params, mp_steps=S, dropout=args.dropout, seed=7, math=math, buckets=args.buckets,
                       overlap=not args.no_overlap)
@@ -584,18 +588,18 @@ def run_train(args, cfg, world, rank, device):
         table = kernel_table(trainer, step_in, n_micro, S, Ne, Nn, math, args.config, wl)
     kname = args.roofline_kernel or dominant(table)
     kid = KERNELS[kname][0]
-    if cfg.get("replay") and world == 1 and n_micro == 1:
+    if cfg.get("replay") and world == 1 and n_micro == 1 and not dp:
         return run_replay(args, cfg, trainer, rank, device, kname, table, wl)
     ev = HipEvents(2 * MAX_LAUNCHES * n_micro * args.steps)
     per = 2 * MAX_LAUNCHES * n_micro
     # N>1: the gradient all-reduce of every timed step between two events on the step's stream, so
     # the line separates the collective (RCCL over xGMI) from the compute
     ar_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-             for _ in range(args.steps)] if world > 1 else None
+             for _ in range(args.steps)] if dp else None
     # ... and, when the step overlaps (Trainer.reduce_split), the early piece's all-reduce on its side stream
     ar_early = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                for _ in range(args.steps)] if world > 1 and trainer._split() else None
-    if world > 1:
+                for _ in range(args.steps)] if dp and trainer._split() else None
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -613,7 +617,7 @@ def run_train(args, cfg, world, rank, device):
             trainer.prof_kernel, trainer.prof_events = kid, None
             out3 = _micro_step(trainer, *step_in, evs, MAX_LAUNCHES)
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     el = time.perf_counter() - t0
     trainer.prof_kernel, trainer.prof_events, trainer.ar_events, trainer.ar_early_events = 0, None, None, None
@@ -643,7 +647,7 @@ def run_train(args, cfg, world, rank, device):
                         "of the backward (> 0: it ran while dA, the encoder backward and the encoder-side "
                         "gradients did), min over ranks"}
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
-    if world > 1:
+    if dp:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
     kern_ms = recorded_ms(ev, MAX_LAUNCHES * n_micro * args.steps)
@@ -672,7 +676,7 @@ def run_train(args, cfg, world, rank, device):
                    "n_global_nodes": n_global, "shard_plan": "shard.plan_shards (cost-balanced contiguous ranges)",
                    "nodes_per_tower": list(cfg["nodes"]) if isinstance(cfg["nodes"], tuple) else cfg["nodes"],
                    "nodes_per_gpu": Nn, "edges_per_gpu": Ne, "mp_steps": S, "math": math,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}" + (" (one-rank process group)" if dp and world == 1 else "")},
         "step_tflops": round(step_flops(Ne, Nn, S) * world * args.steps / el / 1e12, 2),
         "loss": round(loss, 5),
         "roofline": roof,
@@ -705,7 +709,7 @@ def run_train(args, cfg, world, rank, device):
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 
