@@ -550,6 +550,9 @@ def main():
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
     if world > 1 or args.dist:
+        if world == 1:   # --dist without a launcher: a one-rank group on this host
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29547"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
