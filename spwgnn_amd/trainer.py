@@ -240,14 +240,15 @@ class Trainer:
                 self.ar_early_events[0].record()
             self._combine(acc, g, w, early, first)
             work = dist.all_reduce(acc[early], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if self.ar_early_events is not None:   # timing: the side stream waits for the early piece
+                work.wait()
+                self.ar_early_events[1].record()
         self._combine(acc, g, w, late, first)
         if self.ar_events is not None:
             self.ar_events[0].record()
         dist.all_reduce(acc[late], op=dist.ReduceOp.SUM, group=self.group)
         work.wait()   # the step's stream (CUDA) / the host (CPU tensors) waits for the early piece
         if cuda:
-            if self.ar_early_events is not None:
-                self.ar_early_events[1].record(self._side)
             cur.wait_stream(self._side)
         if self.ar_events is not None:
             self.ar_events[1].record()
