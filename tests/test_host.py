@@ -621,3 +621,23 @@ def test_packed_tower_order_fills_blocks():
         tn2, te2 = np.ascontiguousarray(tn[oo]), np.ascontiguousarray(tev[oo])
         L.spwgnn_plan_size(T, tn2.ctypes.data, te2.ctypes.data, 16, C.byref(sz))
         assert sz.n_eblocks <= n0
+
+
+def test_packed_batch_maps_rows_both_ways():
+    """TowerBatch.from_edges(pack=True) on host memory: 'propagation' rows follow their nodes, and
+    to_plan_order / to_input_order are inverse permutations (numpy and torch)."""
+    import torch
+    pos, sizes, src, dst, te, _ = D.ragged_batch(300, 4, 16, seed=8)
+    n = int(sizes.sum())
+    prop = np.random.default_rng(1).normal(size=(n, 100)).astype(np.float32)
+    b = TowerBatch.from_edges(pos, sizes, src, dst, te, prop=prop, device="cpu", pack=True)
+    assert b.node_perm is not None
+    assert np.array_equal(b.prop.numpy(), prop[b.node_perm])
+    assert np.array_equal(b.pos.numpy()[:, :3], pos[b.node_perm])
+    x = np.arange(n, dtype=np.float32)
+    assert np.array_equal(b.to_input_order(b.to_plan_order(x)), x)
+    t = torch.arange(n, dtype=torch.float32)
+    assert torch.equal(b.to_input_order(b.to_plan_order(t)), t)
+    assert np.array_equal(b.to_plan_order(x), x[b.node_perm])
+    plain = TowerBatch.from_edges(pos, sizes, src, dst, te, device="cpu")
+    assert plain.node_perm is None and plain.to_plan_order(x) is x
