@@ -497,7 +497,22 @@ def timed_steps(trainer, step_in, kid, n_micro, steps, slots):
 
 
 # ------------------------------------------------------------------------------ main
+_JSON_OUT = None
+
+
+def emit(out: dict) -> None:
+    """The contract's ONE JSON line, on the process's original stdout (main() points fd 1 at stderr, so
+    whatever a library prints — RCCL's version banner at communicator init — cannot precede it)."""
+    f = _JSON_OUT if _JSON_OUT is not None else sys.stdout
+    f.write(json.dumps(out) + "\n")
+    f.flush()
+
+
 def main():
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 10; 500 for replayed configs)")
@@ -711,7 +726,7 @@ def run_train(args, cfg, world, rank, device):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dp:
         dist.destroy_process_group()
 
@@ -762,7 +777,7 @@ def run_replay(args, cfg, trainer, rank, device, kname, table, wl):
     out["hbm"] = step_hbm(args.config, out["ms_per_step"], math, wl)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-    print(json.dumps(out), flush=True)
+    emit(out)
 
 
 # kernel families: one SPWGNN_K_* id over several weight-gradient shapes. Batched (the default:
@@ -906,7 +921,7 @@ def run_infer(args, cfg, world, rank, device):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
