@@ -296,7 +296,7 @@ class Trainer:
             else:
                 if w != 1.0:
                     acc.mul_(w)
-                if self.world > 1:
+                if self.distributed:   # any process group (one rank: the identity, through the collective)
                     self.allreduce(acc)
             self.iterations += 1
             self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
@@ -339,7 +339,7 @@ class Trainer:
                 acc = torch.mul(g, w, out=self._acc)
             else:
                 acc.add_(g, alpha=w)
-        if self.world > 1 and not self._split():
+        if self.distributed and not self._split():
             self.allreduce(acc)
         self.iterations += 1
         self.engine.adam(self.params, acc, self.m, self.v, self.iterations, self.lr, self.b1, self.b2, self.eps,
