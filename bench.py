@@ -570,7 +570,11 @@ def main():
                 os.environ.setdefault(k, v)
         torch.cuda.set_device(local)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # RCCL on high-priority streams: the overlapped gradient piece runs beside the backward's
+            # kernels instead of queueing behind them (Trainer.reduce_split)
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
         else:
             dist.init_process_group(backend)
     device = torch.device("cuda", local)

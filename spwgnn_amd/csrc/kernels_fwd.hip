@@ -950,22 +950,12 @@ struct NodeSum16X6 {
 // W8 (≤ 32-node tiles): 8 waves at two per SIMD (256 registers: the 32-node sum and a short ring)
 // instead of 4 at one per SIMD with a 5-k-block ring
 // N16: H2s stored as bf16 (bf16 math, §3o)
-// W4 (≤ 16-node tiles, bf16 experiments): 4 waves at one per SIMD (512 registers: a deeper ring, half
-// the tiles' node rows in flight per CU) instead of 8 at two
-#ifndef SPWGNN_EFWD_B16_W4   // A/B: the bf16-H2s edge forward on 4 waves per CU
-#define SPWGNN_EFWD_B16_W4 0
-#endif
-#ifndef SPWGNN_EFWD_PF_B16_W4
-#define SPWGNN_EFWD_PF_B16_W4 5
-#endif
-template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false, bool W8 = false, bool N16 = false, bool W4 = false>   // AB16: A stored as bf16 (§3g)
-__global__ __launch_bounds__(((NW16 || W8) && !W4) ? 512 : 256, 1)
-__attribute__((amdgpu_waves_per_eu(((NW16 || W8) && !W4) ? 2 : 1, ((NW16 || W8) && !W4) ? 2 : 1)))
+template <bool NW16, int DBG = 0, int NP = 3, bool AB16 = false, bool W8 = false, bool N16 = false>   // AB16: A stored as bf16 (§3g)
+__global__ __launch_bounds__((NW16 || W8) ? 512 : 256, 1) __attribute__((amdgpu_waves_per_eu((NW16 || W8) ? 2 : 1, (NW16 || W8) ? 2 : 1)))
 void k_edge_fwd_x6(EdgeFwdArgs a) {
     // bf16 math (NP = 1): a k-block is 5 MFMAs, too short to cover a load one k-block ahead
-    constexpr int kWaves = ((NW16 || W8) && !W4) ? 8 : 4;
-    constexpr int kX6Pf = NW16 ? (NP == 1 ? (W4 ? SPWGNN_EFWD_PF_B16_W4 : SPWGNN_EFWD_PF_B16) : SPWGNN_EFWD_PF)
-                               : (W8 ? SPWGNN_EFWD32_PF : 5);
+    constexpr int kWaves = (NW16 || W8) ? 8 : 4;
+    constexpr int kX6Pf = NW16 ? (NP == 1 ? SPWGNN_EFWD_PF_B16 : SPWGNN_EFWD_PF) : (W8 ? SPWGNN_EFWD32_PF : 5);
     static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
     __shared__ uint4 wl[DBG == 2 ? 64 : 50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
     if constexpr (DBG != 2) {
@@ -1414,11 +1404,7 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
             return hipGetLastError();
         }
 #endif
-#if SPWGNN_EFWD_B16_W4
-        hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1, true, false, true, true>), dim3(edge_grid(a.n_wtiles, 4)), dim3(256), 0, st, a);
-#else
         hipLaunchKernelGGL((k_edge_fwd_x6<true, 0, 1, true, false, true>), dim3(edge_grid(a.n_wtiles, 8)), dim3(512), 0, st, a);
-#endif
         return hipGetLastError();
     }
     if (math == MATH_BF16) {

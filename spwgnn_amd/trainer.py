@@ -229,7 +229,9 @@ class Trainer:
         cur = torch.cuda.current_stream(acc.device) if cuda else None
         if cuda:
             if self._side is None:
-                self._side = torch.cuda.Stream(acc.device)
+                # high priority: a stream of its own on the device's hardware queues, so its wait on the
+                # mid-backward event is not queued behind the step stream's remaining kernels
+                self._side = torch.cuda.Stream(acc.device, priority=-1)
             self._side.wait_event(ev)
             ctx = torch.cuda.stream(self._side)
         else:
