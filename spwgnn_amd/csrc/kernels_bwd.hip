@@ -535,10 +535,17 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // 76h .. 76h+75, image kind kh = 76), into the registers the second layer's output uses later.
 // B16 (bf16 math): dA is read and dz4..dz1 (the weight gradients' Y operands only) are stored as bf16
 // (exact, §3g).
+#ifndef SPWGNN_ENC_NW_B16   // bf16 math, bf16 storage: waves per workgroup of the relation encoder and its backward
+#define SPWGNN_ENC_NW_B16 4
+#endif
+#ifndef SPWGNN_ENC_NW_X6    // the same in split-bf16 (x6) math
+#define SPWGNN_ENC_NW_X6 4
+#endif
 template <int NC, int NP = 3, bool B16 = false, int NW = 0>
-__global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
+__global__ __launch_bounds__(NW > 4 ? 64 * NW : 256, NC == 1 && NW <= 4 ? 2 : 1) void k_enc_edge_bwd_x6(EncEdgeBwdArgs a) {
+    constexpr int kWaves = NW > 4 ? NW : 4;   // waves per workgroup (NW > 0: all share one weight ring)
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-    const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
+    const int blk0 = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * NC;
     if (NW == 0 && blk0 >= a.n_eblocks) return;   // NW > 0: no early exit (tgemm_x6_wg)
     __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
@@ -1125,16 +1132,18 @@ hipError_t launch_dA(const DaArgs& a, int math, hipStream_t st) {
 hipError_t launch_enc_edge_bwd(const EncEdgeBwdArgs& a, int math, hipStream_t st) {
     // one 32-edge block per wave at two waves per SIMD, weight images shared by the workgroup's 4
     // waves (x6: 2.44 → 2.33 ms against two blocks per wave at one wave per SIMD with per-wave rings)
-    constexpr int NC = 1, NW = 4;
+    constexpr int NC = 1, NW = 4, NWB = SPWGNN_ENC_NW_B16;   // bf16: waves sharing one weight pass
     if ((math == MATH_X6 || math == MATH_BF16) && team_blocks(a.n_eblocks)) return launch_enc_edge_bwd_team(a, math, st);
-    const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
+    const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC)), gb((a.n_eblocks + NWB * NC - 1) / (NWB * NC));
     if (math == MATH_BF16) {
-        if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, true, NW>), g, dim3(256), 0, st, a);
+        if (a.b16) hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, true, NWB>), gb, dim3(64 * NWB), 0, st, a);
         else hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 1, false, NW>), g, dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (math == MATH_X6) {
-        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 3, false, NW>), g, dim3(256), 0, st, a);
+        constexpr int NWX = SPWGNN_ENC_NW_X6;
+        const dim3 gx((a.n_eblocks + NWX * NC - 1) / (NWX * NC));
+        hipLaunchKernelGGL((k_enc_edge_bwd_x6<NC, 3, false, NWX>), gx, dim3(64 * NWX), 0, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_enc_edge_bwd, dim3((a.n_eblocks + 3) / 4), dim3(256), 0, st, a);

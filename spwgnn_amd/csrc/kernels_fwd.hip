@@ -293,10 +293,17 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // MFMAs, in + out activations 320 registers) with per-wave rings is the measured alternative.
 // B16 (bf16 math, training): z2, z3 and c_r — MFMA operands only (the weight gradients' X) — are
 // stored as bf16 (exact), and so is A (rounded once before h1 = relu(A + U + V) adds it; §3g).
+#ifndef SPWGNN_ENC_NW_B16   // bf16 math, bf16 storage: waves per workgroup of the relation encoder and its backward
+#define SPWGNN_ENC_NW_B16 4
+#endif
+#ifndef SPWGNN_ENC_NW_X6    // the same in split-bf16 (x6) math
+#define SPWGNN_ENC_NW_X6 4
+#endif
 template <bool TRAIN, int NC, int NP = 3, bool B16 = false, int NW = 0>
-__global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_enc_edge_x6(EncEdgeArgs a) {
+__global__ __launch_bounds__(NW > 4 ? 64 * NW : 256, NC == 1 && NW <= 4 ? 2 : 1) void k_enc_edge_x6(EncEdgeArgs a) {
+    constexpr int kWaves = NW > 4 ? NW : 4;   // waves per workgroup (NW > 0: all share one weight ring)
     const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-    const int blk0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * NC;
+    const int blk0 = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * NC;
     if (NW == 0 && blk0 >= a.n_eblocks) return;   // NW > 0: no early exit (tgemm_x6_wg)
     __shared__ uint4 wring[NW > 0 ? kWgRing * kWgSlot : 1];
     const WgRing<NW> wr{wring, __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
@@ -1367,14 +1374,16 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
     if (math == MATH_X6 || math == MATH_BF16) {
         // one 32-edge block per wave at two waves per SIMD, weight images shared by the workgroup's
         // 4 waves (x6: 2.48 → 2.11 ms against two blocks per wave at one wave per SIMD, per-wave rings)
-        constexpr int NC = 1, NW = 4;
-        const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC));
+        constexpr int NC = 1, NW = 4, NWB = SPWGNN_ENC_NW_B16;   // bf16: waves sharing one weight pass
+        const dim3 g((a.n_eblocks + 4 * NC - 1) / (4 * NC)), gb((a.n_eblocks + NWB * NC - 1) / (NWB * NC));
         if (math == MATH_BF16) {
-            if (train && a.b16) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1, true, NW>), g, dim3(256), 0, st, a);
+            if (train && a.b16) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1, true, NWB>), gb, dim3(64 * NWB), 0, st, a);
             else if (train) hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 1, false, NW>), g, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((k_enc_edge_x6<false, NC, 1, false, NW>), g, dim3(256), 0, st, a);
         } else if (train) {
-            hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 3, false, NW>), g, dim3(256), 0, st, a);
+            constexpr int NWX = SPWGNN_ENC_NW_X6;
+            const dim3 gx((a.n_eblocks + NWX * NC - 1) / (NWX * NC));
+            hipLaunchKernelGGL((k_enc_edge_x6<true, NC, 3, false, NWX>), gx, dim3(64 * NWX), 0, st, a);
         } else {
             hipLaunchKernelGGL((k_enc_edge_x6<false, NC, 3, false, NW>), g, dim3(256), 0, st, a);
         }
