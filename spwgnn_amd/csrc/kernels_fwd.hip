@@ -293,7 +293,12 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // MFMAs, in + out activations 320 registers) with per-wave rings is the measured alternative.
 // B16 (bf16 math, training): z2, z3 and c_r — MFMA operands only (the weight gradients' X) — are
 // stored as bf16 (exact), and so is A (rounded once before h1 = relu(A + U + V) adds it; §3g).
-#ifndef SPWGNN_ENC_NW_B16   // bf16 math, bf16 storage: waves per workgroup of the relation encoder and its backward
+// waves per workgroup of the relation encoder and its backward (build options): all of a workgroup's
+// waves share one pass of each weight image through the LDS ring. 8 instead of 4 was slower in both
+// maths (round 6, same-box A/B, bitwise equal: bf16 config 3 encoder 4.2 → 4.8 ms, x6 headline 2.1 →
+// 2.28 ms per step): the ring's per-slice barrier couples twice the waves, and halving the weight
+// traffic bought nothing
+#ifndef SPWGNN_ENC_NW_B16   // bf16 math, bf16 storage
 #define SPWGNN_ENC_NW_B16 4
 #endif
 #ifndef SPWGNN_ENC_NW_X6    // the same in split-bf16 (x6) math
