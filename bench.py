@@ -160,6 +160,7 @@ class HipEvents:
 
 # ------------------------------------------------------------------------------ workloads
 PACK_OFF = os.environ.get("SPWGNN_NO_PACK", "0") not in ("", "0")   # A/B: ragged towers in input order
+NW_MAX = int(os.environ.get("SPWGNN_NW_MAX", "0")) or None           # A/B: nodes per wave-tile (default plan)
 
 
 def make_workload(cfg: dict, rank: int, device, world: int = 1, plans: bool = False):
@@ -203,7 +204,7 @@ def make_workload(cfg: dict, rank: int, device, world: int = 1, plans: bool = Fa
             continue
         # ragged towers: planned in spwgnn_plan_order's order (67 % → 78 % block fill at config 4); the
         # targets follow the plan's node order (the loss is a mean over nodes: order-free)
-        bt = TowerBatch.from_edges(*part, device=device, pack=ragged and not PACK_OFF)
+        bt = TowerBatch.from_edges(*part, nw_max=NW_MAX, device=device, pack=ragged and not PACK_OFF)
         batches.append(bt)
         targets.append(torch.tensor(bt.to_plan_order(target_all[off[x]:off[y]]), device=device))
     return batches, targets, n_global
@@ -397,7 +398,7 @@ def step_hbm(config: int, ms_per_step: float, math: str, workload: str):
 
 # Algorithmic (compulsory) HBM bytes PER STEP of each timed kernel: every array it must read or write,
 # once, real rows and real features only (150-wide edge/node-message rows, 100-wide state rows; an
-# fp32 element is 4 B, a bf16-stored operand 2 B — bf16 math's §3g/§3o arrays), h1>0 / h2>0 words 19 B
+# fp32 element is 4 B, a bf16-stored operand 2 B — bf16 math's §3g/§3o arrays and U, V (§3ze) — h1>0 / h2>0 words 19 B
 # per edge each. Not the measured traffic (`traffic`, PMC); the roofline picks the roof whose floor
 # (bytes ÷ 8 TB/s or FLOPs ÷ matrix peak) is the larger — the kernel's arithmetic intensity against
 # the ridge point.
@@ -405,15 +406,15 @@ def kernel_bytes(kernel, Ne, Nn, S, math):
     F, W, WN, MK = 4.0, 150, 100, 19.0
     B = 2.0 if math == "bf16" else F          # operand-only arrays stored as bf16 in bf16 math
     edge = {
-        "edge_fwd": S * (Ne * (W * B + 2 * MK) + Nn * (2 * W * F + (W + 1) * B)),
+        "edge_fwd": S * (Ne * (W * B + 2 * MK) + Nn * (2 * W * B + (W + 1) * B)),
         "edge_bwd": S * (Ne * 2 * MK + Nn * (W * F + 2 * W * B)),
         "dA": Ne * (S * 2 * MK + W * B) + S * Nn * W * F,
-        "wgrad_w2": Ne * W * B + S * (Ne * 2 * MK + Nn * 3 * W * F),
-        "node_fwd": S * Nn * ((W + 1) * B + 2 * WN * F + WN * F + WN * B + WN * F + 2 * W * F),
+        "wgrad_w2": Ne * W * B + S * (Ne * 2 * MK + Nn * (2 * W * B + W * F)),
+        "node_fwd": S * Nn * ((W + 1) * B + 2 * WN * F + WN * F + WN * B + WN * F + 2 * W * B),
         "node_bwd": S * Nn * (2 * WN * F + WN * B + 2 * W * B + WN * B + W * F + 2 * WN * F + WN * B),
         "enc_edge": Ne * (16 + 8 + 4 * W * B + 4 * MK),
         "enc_edge_bwd": Ne * (W * B + 4 * MK + 4 * W * B),
-        "enc_node": Nn * (16 + WN * F + 2 * W * F + 2 * MK),
+        "enc_node": Nn * (16 + WN * F + 2 * W * B + 2 * MK),
         "enc_node_bwd": Nn * (S * WN * F + 3 * WN * F),
         # the weight gradients' X and Y operands: rm.1 (X rebuilt from the 8-B d), rm.2, rm.3, W1a per
         # edge; W1b, W1c, omp.0 P/a parts, omp.1, W3 per node·step; omp.0 c part and om.1 per node

@@ -185,8 +185,9 @@ typedef struct spwgnn_run {
  *   F32  v_mfma_f32_*_f32: one fp32 fma chain per output (the f32 MFMA rate, 157 TF)
  *   X6   each fp32 operand split into three bf16 parts, six bf16 MFMA products per fp32 product,
  *        fp32 accumulation (6/16 of the f32 MFMA cost; error O(2^-24) per product)
- *   BF16 operands rounded to bf16, one bf16 MFMA product, fp32 accumulation (BASELINE configs
- *        3-4 are quoted in bf16; error O(2^-9) per product — not the fp32 parity path)       */
+ *   BF16 operands rounded to bf16, one bf16 MFMA product, fp32 accumulation; in training the
+ *        stored A, U, V (the three terms of h1) rounded to bf16 once (BASELINE configs 3-4 are
+ *        quoted in bf16; error O(2^-9) per product — not the fp32 parity path)                */
 #define SPWGNN_MATH_F32 0
 #define SPWGNN_MATH_X6 1
 #define SPWGNN_MATH_BF16 2

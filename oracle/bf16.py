@@ -16,7 +16,8 @@ sees is a property of the factored form, not of the kernels' tiling):
 
   forward  rm.1-3, W1a, om.1, W1b/W1c, W2, [W3; b3], Wo1c/Wo1a/Wo1p, Wo2 on bf16 operands;
            rm.0 / om.0 (2-wide inputs) in fp32; the receiver sum adds bf16(h2_k) in fp32 (a one-hot
-           product); the stored step-invariant A is bf16 (training)
+           product); the stored step-invariant A and the per-step U = P·W1b, V = P·W1c are bf16
+           (training: rounded once when stored, then summed in fp32 into h1)
   backward every activation-gradient product on bf16(dY) and bf16(Wᵀ); every weight gradient
            bf16(X)ᵀ·bf16(dY), bias gradients Σ bf16(dY) (the ones column of X); the sender/receiver
            sums of dh1pre (into dU/dV) add bf16 values; dA = Σ_s dh1pre_s in fp32
@@ -141,7 +142,8 @@ def forward(p: Dict[str, torch.Tensor], pos, src, dst, prop, mp_steps: int = O.R
             training: bool = True) -> torch.Tensor:
     """Logits (Nn,) of the bf16-operand engine arithmetic. pos (Nn, 3) objects rows, src/dst (Ne,)
     int64 global node ids, prop (Nn, 100); drop_r (Ne, 150) / drop_o (Nn, 100) multiplicative masks.
-    `training` = the A array is stored (and read) as bf16, as the engine's bf16 training forward does."""
+    `training` = the A, U and V arrays are stored (and read) as bf16, as the engine's bf16 training
+    forward does."""
     Nn = pos.shape[0]
     # encoders (Networks.py:58-78)
     d = pos[dst, 0:2] - pos[src, 0:2]
@@ -169,6 +171,8 @@ def forward(p: Dict[str, torch.Tensor], pos, src, dst, prop, mp_steps: int = O.R
     for _ in range(mp_steps):                       # Networks.py:83-91
         U = _MM.apply(P, W1[150:250])
         V = _MM.apply(P, W1[250:350])
+        if training:                                # stored rounded, like A
+            U, V = _Round.apply(U), _Round.apply(V)
         h1 = torch.relu(A + _Gather.apply(U, src) + _Gather.apply(V, dst))
         h2 = dense(h1, p, "rmp.1", True)
         H2s = torch.zeros(Nn, 150, dtype=pos.dtype).index_add(0, dst, _Round.apply(h2))

@@ -320,6 +320,14 @@ static bool store_b16_node(const spwgnn_run* r, const spwgnn_batch* b) {
            !team_blocks(b->n_wtiles) && !team_blocks((b->n_nodes + 31) / 32) && !getenv_flag("SPWGNN_NODE_F32");
 }
 
+// U = P·W1b and V = P·W1c in bf16 math (training): rounded to bf16 when stored (oracle/bf16.py,
+// DESIGN.md §3ze), and stored as bf16 exactly when the node-side arrays are (every writer and reader a
+// wide kernel: the node forward, the object encoder, the N16 edge forward, k_w2grad_tile).
+static int uv_storage(const spwgnn_run* r, const spwgnn_batch* b) {
+    if (!r->training || r->math != MATH_BF16) return kUvF32;
+    return store_b16_node(r, b) ? kUvB16 : kUvRound;
+}
+
 // Whether a forward / backward takes the fused small-batch step loops. One place for
 // the gate: run_forward, run_backward and spwgnn_fused_path (the bench's kernel attribution) use it.
 static bool fwd_fused_taken(const spwgnn_run* r, const spwgnn_batch* b) {
@@ -379,6 +387,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     const bool drop = r->training && r->dropout > 0.f;
     const uint32_t thresh = (uint32_t)std::min(4294967295.0, std::floor((double)r->dropout * 4294967296.0));
     const float scale = drop ? 1.0f / (1.0f - r->dropout) : 1.0f;
+    const int uv16 = uv_storage(r, b);
 
     EncNodeArgs en{};
     en.n_nodes = b->n_nodes;
@@ -403,6 +412,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
     en.P0 = c.f(w.P_at(0));
     en.U0 = c.f(w.U_at(0));
     en.V0 = c.f(w.V_at(0));
+    en.uv16 = uv16;
     en.dropout_on = drop;
     en.thresh = thresh;
     en.scale = scale;
@@ -466,6 +476,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
         ef.h1_out = nullptr;   // the W2 gradient recomputes h1 (XM_H1)
         ef.a_b16 = store_b16(r, b);
         ef.n16 = store_b16_node(r, b);
+        ef.uv16 = uv16;
         ef.n_nodes = b->n_nodes;
         ef.recv_blocks = (b->flags & SPWGNN_BATCH_RECV_BLOCKS) && kmath(r, kX6EdgeFwd) == MATH_X6 &&
                          b->n_eblocks == b->n_nodes && !getenv_flag("SPWGNN_RB_ONEHOT");
@@ -510,6 +521,7 @@ static int32_t run_forward(const float* params, const spwgnn_batch* b, const spw
             nf.x_w1c = c.x6(X6_W1C);
         }
         nf.n16 = store_b16_node(r, b);
+        nf.uv16 = uv16;
         return nf;
     };
     if (fwd_fused_taken(r, b)) {
@@ -641,6 +653,7 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         a.RN = w.RN;
         a.S = (int)(g.rows / w.RE);
         a.a_b16 = (g.b16 & kB16A) != 0;
+        a.uv16 = (g.b16 & kB16UV) != 0;
         a.wtile = b->wtile;
         a.n_wtiles = b->n_wtiles;
         a.nw_max = b->nw_max;
@@ -1035,7 +1048,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         g.xmode = XM_H1; g.ymode = YM_DH2;
         g.x_count = g.y_count = g.rows = RE * S;
         g.recompute = true;
-        g.b16 = b16 ? kB16A : 0;
+        g.b16 = (b16 ? kB16A : 0) | (n16 ? kB16UV : 0);   // U, V rows as the forward stored them (uv_storage)
         return wg(g);
     };
     auto node_xy = [&](WgSpec& g, int64_t xoff, int xld, int xw, int xones, int64_t xstride, int64_t yoff, int yld,

@@ -130,6 +130,32 @@ __device__ __forceinline__ void load_cm_b16(const uint16_t* __restrict__ blk, f3
             X[t][4 * q + 3] = v.w;
         }
 }
+// ---- U = P·W1b and V = P·W1c in bf16 math (training): rounded to bf16 once where
+// they are stored, like A (§3g) — h1 = relu(A + U[s] + V[r]) adds three bf16 values in fp32 — and
+// stored as bf16 (half the bytes of the edge forward's gathers) where every reader is a wide kernel.
+enum : int { kUvF32 = 0, kUvRound = 1, kUvB16 = 2 };
+template <int NT>
+__device__ __forceinline__ void store_cm_uv(float* base, int64_t off, f32x16 (&X)[NT], int lane, bool valid, int uv16) {
+    if (uv16 == kUvB16) {
+        store_cm_b16<NT>(reinterpret_cast<uint16_t*>(base) + off, X, lane, valid);   // element index of fp32
+        return;
+    }
+    if (uv16 == kUvRound)   // X is rounded in place
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) X[t][r] = bf16_round(X[t][r]);
+    store_cm<NT>(base + off, X, lane, valid);
+}
+// the team kernels' form (fp32 storage only): one output tile, rounded in place when uv16 asks
+__device__ __forceinline__ void round_uv_tile(f32x16& X, int uv16) {
+    if (uv16 == kUvRound)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[r] = bf16_round(X[r]);
+}
+__device__ __forceinline__ float4 unpack_uv(float4 v) { return v; }
+__device__ __forceinline__ float4 unpack_uv(uint2 v) { return unpack4_bf16(v); }
+
 // one element of a bf16-stored array (RNE; the element index of the fp32 layout)
 __device__ __forceinline__ void store_b16(float* base, int64_t idx, float v) {
     reinterpret_cast<uint16_t*>(base)[idx] = (uint16_t)(pk_bf16(v, 0.f) & 0xffffu);

@@ -107,6 +107,7 @@ struct EncNodeArgs {
     const uint4 *x_om1, *x_w1b, *x_w1c;   // x6 images (x6 math)
     const uint4* xh_om1;                  // its half-tile form (the chain kernel, §3w)
     float *zo1, *co, *P0, *U0, *V0;
+    int uv16;                   // U0, V0 in bf16 math (training): kUvRound / kUvB16 (gemm_blocks.h store_cm_uv)
     int dropout_on;
     uint32_t thresh;
     float scale;
@@ -150,6 +151,7 @@ struct EdgeFwdArgs {
     float* h1_out;     // training: h1 rows, chunk-major blocks (kCmBlk), for the W2 gradient
     int a_b16;         // bf16 math (training): A stored as bf16
     int n16;           // bf16 math (training, wide kernels): H2s stored as bf16 (§3g, node side)
+    int uv16;          // how U, V were stored (store_cm_uv): kUvB16 exactly when n16 (the N16 kernel reads bf16)
     const uint4* x_w2; // x6 image of W2 (half rows, kh 76) — the LDS B operand (math == MATH_X6)
 };
 
@@ -165,6 +167,7 @@ struct NodeFwdArgs {
     const uint4 *x_w3a, *x_wo1c, *x_wo1a, *x_wo1p, *x_wo2, *x_w1b, *x_w1c;   // x6 images
     const uint4 *xh_w3a, *xh_wo1c, *xh_wo1a, *xh_wo1p, *xh_wo2;            // half-tile forms (chain kernel, §3w)
     int n16;        // bf16 math (training, wide kernels): H2s read and o1 stored as bf16 (§3g, node side)
+    int uv16;       // U, V in bf16 math (training): kUvRound, or kUvB16 (exactly when n16)
 };
 
 struct NodeBwdArgs {
@@ -270,6 +273,7 @@ struct WgradArgs {
     int64_t RE, RN;
     int S;                         // steps (XM_H1 / YM_DH2 walk rows as (edge block, step) stages)
     int a_b16;                     // bf16 math: A stored as bf16 (k_w2grad_ws)
+    int uv16;                      // bf16 math: U, V stored as bf16 (k_w2grad_tile only)
     const int32_t* wtile;          // the batch plan's wave-tiles (k_w2grad_tile walks whole tiles)
     int n_wtiles, nw_max;
     int w2_tile;                   // 1: the W2 gradient with LDS-staged node rows (bf16 math)
@@ -286,7 +290,7 @@ struct WgWsArgs {          // k_wgrad_ws: stages (s, nb) of a [S][nbs] grid of 3
     int x_ones, pad0;
 };
 // bf16 storage of the weight gradients' edge operands (bf16 math, §3g): bit 0 X, bit 1 Y
-enum : int { kB16X = 1, kB16Y = 2, kB16A = 4 };   // kB16A: the W2 gradient's A rows
+enum : int { kB16X = 1, kB16Y = 2, kB16A = 4, kB16UV = 8 };   // kB16A / kB16UV: the W2 gradient's A / U, V rows
 struct ReduceArgs {
     const float* slab;
     int chunks, kx_pad, ny_pad;

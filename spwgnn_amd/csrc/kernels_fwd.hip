@@ -205,10 +205,10 @@ __global__ __launch_bounds__(256, 2) void k_enc_node_x6(EncNodeArgs a) {
     f32x16 U[1][5];
     zero_tiles(U[0]);
     tchain_x6s<5, 7, 4, 1, kX6Ring, NP, NW>(P, U, a.x_w1b, lane, wr);
-    if (has) store_cm<5>(a.U0 + bE, U[0], lane, valid);
+    if (has) store_cm_uv<5>(a.U0, bE, U[0], lane, valid, NP == 1 ? a.uv16 : kUvF32);
     zero_tiles(U[0]);
     tchain_x6s<5, 7, 4, 1, kX6Ring, NP, NW>(P, U, a.x_w1c, lane, wr);
-    if (has) store_cm<5>(a.V0 + bE, U[0], lane, valid);
+    if (has) store_cm_uv<5>(a.V0, bE, U[0], lane, valid, NP == 1 ? a.uv16 : kUvF32);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -795,13 +795,13 @@ __global__ __launch_bounds__(256, NC == 1 ? 2 : 1) void k_node_fwd_x6(NodeFwdArg
         tchain_x6s<5, 7, 4, NC, kX6Ring, NP, NW>(X, U, a.x_w1b, lane, wr);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            if (has[c]) store_cm<5>(a.U + bE(c), U[c], lane, valid[c]);
+            if (has[c]) store_cm_uv<5>(a.U, bE(c), U[c], lane, valid[c], NP == 1 ? a.uv16 : kUvF32);
             zero_tiles(U[c]);
         }
         tchain_x6s<5, 7, 4, NC, kX6Ring, NP, NW>(X, U, a.x_w1c, lane, wr);
 #pragma unroll
         for (int c = 0; c < NC; ++c)
-            if (has[c]) store_cm<5>(a.V + bE(c), U[c], lane, valid[c]);
+            if (has[c]) store_cm_uv<5>(a.V, bE(c), U[c], lane, valid[c], NP == 1 ? a.uv16 : kUvF32);
     }
 }
 
@@ -956,6 +956,10 @@ struct NodeSum16X6 {
 #ifndef SPWGNN_EFWD_PF_B16
 #define SPWGNN_EFWD_PF_B16 2
 #endif
+// bf16 math: the A rows (the streamed HBM operand) may run deeper than the U/V gathers (cache hits)
+#ifndef SPWGNN_EFWD_PFA_B16
+#define SPWGNN_EFWD_PFA_B16 SPWGNN_EFWD_PF_B16
+#endif
 #ifndef SPWGNN_EFWD32_PF
 #define SPWGNN_EFWD32_PF 1
 #endif
@@ -968,7 +972,8 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     // bf16 math (NP = 1): a k-block is 5 MFMAs, too short to cover a load one k-block ahead
     constexpr int kWaves = (NW16 || W8) ? 8 : 4;
     constexpr int kX6Pf = NW16 ? (NP == 1 ? SPWGNN_EFWD_PF_B16 : SPWGNN_EFWD_PF) : (W8 ? SPWGNN_EFWD32_PF : 5);
-    static_assert(10 % kX6Pf == 0, "ring slots carry over between blocks");
+    constexpr int kPfA = NW16 && NP == 1 ? SPWGNN_EFWD_PFA_B16 : kX6Pf;   // A rows' ring depth
+    static_assert(10 % kX6Pf == 0 && 10 % kPfA == 0 && kPfA >= kX6Pf, "ring slots carry over between blocks");
     __shared__ uint4 wl[DBG == 2 ? 64 : 50 * 3 * 64];   // W2 x6 image: [kb·5 + T][part][lane]
     if constexpr (DBG != 2) {
         for (int idx = threadIdx.x; idx < 50 * 3 * 64; idx += blockDim.x) wl[idx] = a.x_w2[idx];
@@ -981,23 +986,37 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     const WlBases wlb(wl + lane);
     auto load_sd = [&](int blk) { return make_int2(a.esrc[(int64_t)blk * 32 + i], a.edst[(int64_t)blk * 32 + i]); };
     // a block's h1 operand sources: A rows and the gathered U[s], V[r] rows (chunk q at +256q / +64q)
-    struct Src { int64_t ai; const float4 *U, *V; };   // ai: element index of the A rows
+    // N16: U, V stored as bf16 (kUvB16, §3ze) — 8-byte pieces at the fp32 element index, unpacked at use
+    using UVT = typename std::conditional<N16, uint2, float4>::type;
+    struct Src { int64_t ai; const UVT *U, *V; };   // ai: element index of the A rows
+    auto uv_at = [&](const float* base, int node) {
+        const int64_t e = cm_index<kKhE>(node, 0) + h * 128;
+        if constexpr (N16) return reinterpret_cast<const UVT*>(reinterpret_cast<const uint16_t*>(base) + e);
+        else return reinterpret_cast<const UVT*>(base + e);
+    };
     auto src_of = [&](int blk, int2 sd, int n0) {
         const int sc = DBG == 3 ? n0 : (sd.x >= 0 ? sd.x : n0), dc = DBG == 3 ? n0 : (sd.x >= 0 ? sd.y : n0);
-        return Src{(int64_t)(DBG == 1 ? (blk & 7) : blk) * kCmBlk + h * 128 + i * 4,
-                   reinterpret_cast<const float4*>(a.U + cm_index<kKhE>(sc, 0) + h * 128),
-                   reinterpret_cast<const float4*>(a.V + cm_index<kKhE>(dc, 0) + h * 128)};
+        return Src{(int64_t)(DBG == 1 ? (blk & 7) : blk) * kCmBlk + h * 128 + i * 4, uv_at(a.U, sc), uv_at(a.V, dc)};
     };
     // k-block kb = chunks 2kb, 2kb+1 (chunk 19 does not exist: clamped, its W2 rows are zero)
-    struct KB { float4 a[2], u[2], v[2]; };
-    auto ld = [&](const Src& sr, int kb, KB& r) {
+    // (bf16 pieces stay packed in the ring and are unpacked where they are used)
+    using AT = typename std::conditional<AB16, uint2, float4>::type;
+    struct KA { AT a[2]; };
+    struct KU { UVT u[2], v[2]; };
+    auto ldA = [&](int64_t ai, int kb, KA& r) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int q = min(2 * kb + c, kKhE / 4 - 1);
             if constexpr (AB16)
-                r.a[c] = unpack4_bf16(ld_nt_u2(reinterpret_cast<const uint16_t*>(a.A) + sr.ai + 256 * q));
+                r.a[c] = ld_nt_u2(reinterpret_cast<const uint16_t*>(a.A) + ai + 256 * q);
             else
-                r.a[c] = ld_nt_f4(a.A + sr.ai + 256 * q);
+                r.a[c] = ld_nt_f4(a.A + ai + 256 * q);
+        }
+    };
+    auto ldUV = [&](const Src& sr, int kb, KU& r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int q = min(2 * kb + c, kKhE / 4 - 1);
             r.u[c] = sr.U[64 * q];
             r.v[c] = sr.V[64 * q];
         }
@@ -1009,9 +1028,13 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
     // previous block (the ring carries over)
     int2 cur_sd = load_sd(info.x);
     Src cur = src_of(info.x, cur_sd, info.z);
-    KB ring[kX6Pf];
+    KA ringA[kPfA];
+    KU ringU[kX6Pf];
 #pragma unroll
-    for (int k = 0; k < kX6Pf; ++k) ld(cur, k, ring[k]);
+    for (int k = 0; k < kPfA; ++k) {
+        ldA(cur.ai, k, ringA[k]);
+        if (k < kX6Pf) ldUV(cur, k, ringU[k]);
+    }
     for (; wt < a.n_wtiles; wt += wstep) {
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];
@@ -1029,27 +1052,31 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         uint32_t* mrow = a.mask1 ? a.mask1 + (int64_t)blk * kLdE : nullptr;
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         Src nxt;
-        f32x16 acc[5];
-        zero_tiles(acc);
+        const int64_t nai = (int64_t)(DBG == 1 ? (nblk & 7) : nblk) * kCmBlk + h * 128 + i * 4;   // = nxt.ai
+        f32x16 acc[5];   // k-block 0's products start from C = 0 (mfma32_x6_group<…, true>)
 #pragma unroll
         for (int kb = 0; kb < 10; ++kb) {
-            KB& cr = ring[kb % kX6Pf];
+            KA& ca = ringA[kb % kPfA];
+            KU& cu = ringU[kb % kX6Pf];
             float xv[8];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                xv[4 * c + 0] = relu_valid(cr.a[c].x + cr.u[c].x + cr.v[c].x, vcap);
-                xv[4 * c + 1] = relu_valid(cr.a[c].y + cr.u[c].y + cr.v[c].y, vcap);
-                xv[4 * c + 2] = relu_valid(cr.a[c].z + cr.u[c].z + cr.v[c].z, vcap);
-                xv[4 * c + 3] = relu_valid(cr.a[c].w + cr.u[c].w + cr.v[c].w, vcap);
+                const float4 av = unpack_uv(ca.a[c]), uv = unpack_uv(cu.u[c]), vv = unpack_uv(cu.v[c]);
+                xv[4 * c + 0] = relu_valid(av.x + uv.x + vv.x, vcap);
+                xv[4 * c + 1] = relu_valid(av.y + uv.y + vv.y, vcap);
+                xv[4 * c + 2] = relu_valid(av.z + uv.z + vv.z, vcap);
+                xv[4 * c + 3] = relu_valid(av.w + uv.w + vv.w, vcap);
             }
             uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], hw[m], mw[m], lw[m]);
+            if (kb + kPfA < 10) ldA(cur.ai, kb + kPfA, ca);
+            else ldA(nai, kb + kPfA - 10, ca);
             if (kb + kX6Pf < 10) {
-                ld(cur, kb + kX6Pf, cr);
+                ldUV(cur, kb + kX6Pf, cu);
             } else {
                 if (kb + kX6Pf == 10) nxt = src_of(nblk, nsd, nn0);
-                ld(nxt, kb + kX6Pf - 10, cr);
+                ldUV(nxt, kb + kX6Pf - 10, cu);
             }
             bf16x8 ap[3];
             ap[0] = as_bf16x8(make_uint4(hw[0], hw[1], hw[2], hw[3]));
@@ -1361,6 +1388,7 @@ hipError_t launch_prep(const PrepArgs& a, const PrepX6Args* x, hipStream_t st) {
 }
 hipError_t launch_enc_node(const EncNodeArgs& a, int math, hipStream_t st) {
     const int waves = (a.n_nodes + 31) / 32;
+    if (a.uv16 && math != MATH_BF16) return hipErrorInvalidValue;   // rounded U0, V0: the bf16 kernels only
     if ((math == MATH_X6 || math == MATH_BF16) && team_blocks(waves)) return launch_enc_node_team(a, math, st);
     if (math == MATH_X6) {
         hipLaunchKernelGGL((k_enc_node_x6<3, 4>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
@@ -1402,6 +1430,7 @@ hipError_t launch_enc_edge(const EncEdgeArgs& a, int math, hipStream_t st) {
 }
 hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     if (a.nw_max > kNwMaxLimit) return hipErrorInvalidValue;  // one-hot rows: ≤ 32 nodes per wave-tile
+    if ((a.uv16 == kUvB16) != (a.n16 != 0)) return hipErrorInvalidValue;   // bf16 U, V: the N16 kernel reads them
     // small batches: a workgroup of five waves per wave-tile, one output tile per wave (kernels_team.hip)
     if ((math == MATH_X6 || math == MATH_BF16) && a.nw_max <= 16 && team_blocks(a.n_wtiles))
         return a.n16 ? hipErrorInvalidValue : launch_edge_fwd_team(a, math, st);   // team kernels: fp32 H2s
@@ -1479,6 +1508,7 @@ hipError_t launch_edge_fwd(const EdgeFwdArgs& a, int math, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_node_fwd(const NodeFwdArgs& a, int math, hipStream_t st) {
+    if ((a.uv16 == kUvB16) != (a.n16 != 0) || (a.uv16 && math != MATH_BF16)) return hipErrorInvalidValue;
     if ((math == MATH_X6 || math == MATH_BF16) && team_blocks((a.n_nodes + 31) / 32))
         return a.n16 ? hipErrorInvalidValue : launch_node_fwd_team(a, math, st);   // team kernels: fp32 arrays
     if (a.n16 && math != MATH_BF16) return hipErrorInvalidValue;

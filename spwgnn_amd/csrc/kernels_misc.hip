@@ -781,7 +781,8 @@ struct W2tIt {   // stage iterator (wave-uniform): tile ti, step s, block bb of 
 // DBG (diagnosis builds, SPWGNN_W2G_DBG with SPWGNN_DIAG; wrong results): 1 no node-row LDS reads,
 // 2 no per-stage global loads (A, h2 words, indices), 4 no node-row loads/stores, 8 no staging
 // stores (nor the arithmetic feeding them), 16 no MFMAs
-template <int NP, bool AB16, int DBG = 0>
+// UV16 (kUvB16, §3ze): U and V rows stored as bf16 (each step's element index from its fp32 step start)
+template <int NP, bool AB16, int DBG = 0, bool UV16 = false>
 __global__ __launch_bounds__(kW2gThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_w2grad_tile(WgradArgs a, int64_t blk_per_wg) {
     using IM = X6Img<160>;
@@ -901,10 +902,33 @@ void k_w2grad_tile(WgradArgs a, int64_t blk_per_wg) {
     };
     // one group's node rows: unit u = (arr·38 + chunk)·16 + node (node fastest: coalesced per chunk)
     float4 pf[kW2tPf];
+    // UV16: per array three slots of 256 units (arr = slot / 3, a compile-time value: the bf16 U/V
+    // pieces and the fp32 G3 pieces land in registers of their own type, so no load result is merged
+    // with another's and the loads' wait stays in node_store)
+    constexpr int kUvSlots = 3, kArrUnits = kW2tChunks * kW2tNodes;   // 608 units per array
+    uint2 pfuv[2 * kUvSlots];
+    float4 pfg[kUvSlots];
     auto node_fetch = [&](int ti, int s) {
         if constexpr ((DBG & 4) != 0) return;
         const int4 inf = tile_info(ti);
         const int64_t ns = (int64_t)s * nstep_n;
+        if constexpr (UV16) {
+#pragma unroll
+            for (int k = 0; k < 3 * kUvSlots; ++k) {
+                const int arr = k / kUvSlots, ua = st + 256 * (k % kUvSlots);
+                const int q = ua >> 4, nd = ua & 15;
+                const int64_t e = cm_index<kKhE>(inf.z + nd, 4 * q);
+                if (arr < 2) {
+                    pfuv[k] = make_uint2(0u, 0u);
+                    if (ua < kArrUnits && nd < inf.w)
+                        pfuv[k] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>((arr == 0 ? a.U : a.V) + ns) + e);
+                } else {
+                    pfg[k - 2 * kUvSlots] = f4zero();
+                    if (ua < kArrUnits && nd < inf.w) pfg[k - 2 * kUvSlots] = *reinterpret_cast<const float4*>(a.G3 + ns + e);
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < kW2tPf; ++j) {
             const int u = st + 256 * j;
@@ -919,6 +943,17 @@ void k_w2grad_tile(WgradArgs a, int64_t blk_per_wg) {
     };
     auto node_store = [&](int par) {
         if constexpr ((DBG & 4) != 0) return;
+        if constexpr (UV16) {
+#pragma unroll
+            for (int k = 0; k < 3 * kUvSlots; ++k) {
+                const int arr = k / kUvSlots, ua = st + 256 * (k % kUvSlots);
+                const int q = ua >> 4, nd = ua & 15;
+                if (ua < kArrUnits)
+                    nodes[par][(arr * kW2tNodes + nd) * kW2tChunks + q] =
+                        arr < 2 ? unpack4_bf16(pfuv[k < 2 * kUvSlots ? k : 0]) : pfg[k < 2 * kUvSlots ? 0 : k - 2 * kUvSlots];
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < kW2tPf; ++j) {
             const int u = st + 256 * j;
@@ -1782,6 +1817,7 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
     constexpr int dbg = 0;
 #endif
     const dim3 g(wgs), b(kW2gThreads);
+    if (a.uv16 && (math != MATH_BF16 || (dbg && dbg < 100))) return hipErrorInvalidValue;
     if (math == MATH_BF16) {
 #ifdef SPWGNN_DIAG
         if (a.a_b16 && dbg && dbg < 100) {
@@ -1801,7 +1837,10 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
 #ifdef SPWGNN_DIAG
             if (a.a_b16 && dbg >= 100) {   // the tile kernel's diagnosis variants: SPWGNN_W2G_DBG = 100 + bits
                 switch (dbg - 100) {
-#define W2T_CASE(d) case d: hipLaunchKernelGGL((k_w2grad_tile<1, true, d>), g, b, 0, st, a, blk_per_wg); break;
+#define W2T_CASE(d) case d: \
+    if (a.uv16) hipLaunchKernelGGL((k_w2grad_tile<1, true, d, true>), g, b, 0, st, a, blk_per_wg); \
+    else hipLaunchKernelGGL((k_w2grad_tile<1, true, d>), g, b, 0, st, a, blk_per_wg); \
+    break;
                     W2T_CASE(1) W2T_CASE(2) W2T_CASE(4) W2T_CASE(8) W2T_CASE(16) W2T_CASE(3) W2T_CASE(6) W2T_CASE(7)
 #undef W2T_CASE
                     default: return hipErrorInvalidValue;
@@ -1809,10 +1848,13 @@ hipError_t launch_w2grad_ws(const WgradArgs& a, int wgs, int64_t blk_per_wg, int
                 return hipGetLastError();
             }
 #endif
-            if (a.a_b16) hipLaunchKernelGGL((k_w2grad_tile<1, true>), g, b, 0, st, a, blk_per_wg);
+            if (a.a_b16 && a.uv16) hipLaunchKernelGGL((k_w2grad_tile<1, true, 0, true>), g, b, 0, st, a, blk_per_wg);
+            else if (a.uv16) return hipErrorInvalidValue;
+            else if (a.a_b16) hipLaunchKernelGGL((k_w2grad_tile<1, true>), g, b, 0, st, a, blk_per_wg);
             else hipLaunchKernelGGL((k_w2grad_tile<1, false>), g, b, 0, st, a, blk_per_wg);
             return hipGetLastError();
         }
+        if (a.uv16) return hipErrorInvalidValue;   // bf16 U, V rows: the tile kernel only
         if (a.a_b16) hipLaunchKernelGGL((k_w2grad_ws<0, 1, true>), g, b, 0, st, a, blk_per_wg);
         else hipLaunchKernelGGL((k_w2grad_ws<0, 1>), g, b, 0, st, a, blk_per_wg);
         return hipGetLastError();

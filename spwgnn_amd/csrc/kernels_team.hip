@@ -497,8 +497,10 @@ __device__ __forceinline__ void enc_node_team_body(const EncNodeArgs& a, const T
         R.store<kKhN>(a.P0, pt, T);
     }
     f32x16 U = team_gemm(F, TeamRegs<4>{P}, [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
+    round_uv_tile(U, a.uv16);   // bf16 math (training): rounded as the wide kernels store them (§3ze)
     R.store<kKhE>(a.U0, U, T);
     U = team_gemm(F, TeamRegs<4>{P}, [&](int) {});
+    round_uv_tile(U, a.uv16);
     R.store<kKhE>(a.V0, U, T);
 }
 template <int NP>
@@ -611,9 +613,11 @@ __device__ __forceinline__ void node_fwd_team_body(const NodeFwdArgs& a, const T
     if (a.U) {   // U' = P'·W1b, V' = P'·W1c for the next step
         f32x16 U = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); },
                              [&](int kb) { F.load_kb(a.x_w1c, 5, T, lane, kb); });
+        round_uv_tile(U, a.uv16);   // bf16 math (training): rounded as the wide kernels store them (§3ze)
         R.store<kKhE>(a.U, U, T);
         TEAM_STAMP(8);
         U = team_gemm<7>(F, [&](int kb, uint32_t (&sp)[3][4]) { act.get(0, kb, sp, lane); }, [&](int) {});
+        round_uv_tile(U, a.uv16);
         R.store<kKhE>(a.V, U, T);
         TEAM_STAMP(9);
     }
@@ -1376,7 +1380,7 @@ bool team_blocks(int n_blocks) {
 }
 
 hipError_t launch_edge_fwd_team(const EdgeFwdArgs& a, int math, hipStream_t st) {
-    if (a.nw_max > 16) return hipErrorInvalidValue;
+    if (a.nw_max > 16 || a.uv16 == kUvB16) return hipErrorInvalidValue;   // team kernels: fp32 U, V
     const dim3 g(a.n_wtiles), b(64 * kTeamEdge);
     if (math == MATH_BF16) {
         if (a.a_b16) hipLaunchKernelGGL((k_edge_fwd_team<1, true>), g, b, 0, st, a);
@@ -1426,6 +1430,7 @@ hipError_t launch_enc_edge_team(const EncEdgeArgs& a, int math, bool train, hipS
     return hipGetLastError();
 }
 hipError_t launch_enc_node_team(const EncNodeArgs& a, int math, hipStream_t st) {
+    if (a.uv16 == kUvB16) return hipErrorInvalidValue;
     const dim3 g((a.n_nodes + 31) / 32), b(64 * kTeamEdge);
     if (math == MATH_BF16) hipLaunchKernelGGL((k_enc_node_team<1>), g, b, 0, st, a);
     else if (math == MATH_X6) hipLaunchKernelGGL((k_enc_node_team<3>), g, b, 0, st, a);
@@ -1436,7 +1441,7 @@ bool enc_pair_team(int n_eblocks, int n_nodes, int math) {
     return (math == MATH_X6 || math == MATH_BF16) && team_blocks(n_eblocks) && team_blocks((n_nodes + 31) / 32);
 }
 hipError_t launch_enc_pair_team(const EncEdgeArgs& e, const EncNodeArgs& n, int math, bool train, hipStream_t st) {
-    if (!enc_pair_team(e.n_eblocks, n.n_nodes, math)) return hipErrorInvalidValue;
+    if (!enc_pair_team(e.n_eblocks, n.n_nodes, math) || n.uv16 == kUvB16) return hipErrorInvalidValue;
     const dim3 g(e.n_eblocks + (n.n_nodes + 31) / 32), b(64 * kTeamEdge);
     if (math == MATH_BF16) {
         if (train && e.b16) hipLaunchKernelGGL((k_enc_pair_team<true, 1, true>), g, b, 0, st, e, n);
@@ -1454,7 +1459,8 @@ bool fwd_fused_team(int n_wtiles, int nw_max, int n_eblocks, int n_nodes, int ma
 }
 hipError_t launch_fwd_fused_team(const FwdFusedArgs& a, int math, bool train, hipStream_t st) {
     if (!fwd_fused_team(a.ef.n_wtiles, a.ef.nw_max, a.ee.n_eblocks, a.en.n_nodes, math) || a.S < 1 || a.ef.n16 ||
-        a.nf.n16 || a.ef.recv_blocks || a.ee.b16 != a.ef.a_b16 || !a.nf.cw_out)
+        a.nf.n16 || a.ef.recv_blocks || a.ee.b16 != a.ef.a_b16 || !a.nf.cw_out || a.en.uv16 == kUvB16 ||
+        a.nf.uv16 == kUvB16 || a.ef.uv16 == kUvB16)
         return hipErrorInvalidValue;
     const dim3 g(a.ef.n_wtiles), b(64 * kTeamEdge);
     if (math == MATH_BF16) {
@@ -1493,6 +1499,7 @@ hipError_t launch_bwd_enc_pair_team(const DaArgs& da, const EncEdgeBwdArgs& eeb,
     return hipGetLastError();
 }
 hipError_t launch_node_fwd_team(const NodeFwdArgs& a, int math, hipStream_t st) {
+    if (a.uv16 == kUvB16) return hipErrorInvalidValue;
     const dim3 g((a.n_nodes + 31) / 32), b(64 * kTeamEdge);
     if (math == MATH_BF16) hipLaunchKernelGGL((k_node_fwd_team<1>), g, b, 0, st, a);
     else if (math == MATH_X6) hipLaunchKernelGGL((k_node_fwd_team<3>), g, b, 0, st, a);
