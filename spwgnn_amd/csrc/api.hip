@@ -62,6 +62,14 @@ static constexpr int kW2gWgs = 256;   // W2 gradient: one workgroup per CU (MI35
 // by the reduction, stays small against its operands) while a job keeps ≥ kWsMinWgs workgroups
 static constexpr int kWsMinStages = 32;
 static constexpr int kWsMinWgs = 32;
+// ... and a small job (a small batch's: fewer than kWsMinWgs·kWsSmallStages stages) gives each
+// workgroup ≥ kWsSmallStages stages: every workgroup writes a whole 160×160 slab (100 KB) that the
+// reduction reads back, ≈ 2.5 stages' worth of operand bytes — one stage per workgroup made the slabs
+// most of the small step's weight-gradient traffic (Keras fit at batch 32: ≈ 360 slabs, 36 MB)
+#ifndef SPWGNN_WS_SMALL_STAGES
+#define SPWGNN_WS_SMALL_STAGES 4
+#endif
+static constexpr int kWsSmallStages = SPWGNN_WS_SMALL_STAGES;
 // Diagnosis switches (A/B of superseded kernels, per-kernel math) exist only in -DSPWGNN_DIAG builds;
 // the shipping library has no environment-dependent code path.
 static bool getenv_flag(const char* name) {
@@ -678,7 +686,10 @@ static int32_t run_wgrad(const Ctx& c, const spwgnn_batch* b, const WgSpec& g, f
         wa.b0 = g.b0;
         const int64_t nst = wa.nbs * wa.S;
         int64_t wgs = std::min<int64_t>(nst, kW2gWgs);
-        if (wsb) wgs = std::min<int64_t>(wgs, std::max<int64_t>(kWsMinWgs, (nst + kWsMinStages - 1) / kWsMinStages));
+        if (wsb) {
+            wgs = std::min<int64_t>(wgs, std::max<int64_t>(kWsMinWgs, (nst + kWsMinStages - 1) / kWsMinStages));
+            wgs = std::min<int64_t>(wgs, (nst + kWsSmallStages - 1) / kWsSmallStages);
+        }
         wa.stages_per_wg = (nst + wgs - 1) / wgs;
         wgs = (nst + wa.stages_per_wg - 1) / wa.stages_per_wg;
         chunks = wgs;

@@ -1053,7 +1053,8 @@ void k_edge_fwd_x6(EdgeFwdArgs a) {
         const int m1off = lane < 4 ? lane : kKhE + lane - 4;
         Src nxt;
         const int64_t nai = (int64_t)(DBG == 1 ? (nblk & 7) : nblk) * kCmBlk + h * 128 + i * 4;   // = nxt.ai
-        f32x16 acc[5];   // k-block 0's products start from C = 0 (mfma32_x6_group<…, true>)
+        f32x16 acc[5];
+        zero_tiles(acc);
 #pragma unroll
         for (int kb = 0; kb < 10; ++kb) {
             KA& ca = ringA[kb % kPfA];

@@ -24,7 +24,9 @@ for bit (tests/test_gpu_replay.py).
 """
 from __future__ import annotations
 
+import ctypes as C
 import inspect
+import os
 from typing import Callable, Dict, Optional
 
 import numpy as np
@@ -135,6 +137,41 @@ class StaticBatch:
         self.copy_in(0)
 
 
+class SlotEvent:
+    """The host's "this staging slot is free again" marker: a HIP event created with
+    hipEventDisableSystemFence (and no timing). The host only needs to know that the step which read
+    the slot has finished — its reads of pinned memory are complete when its kernels are — so the
+    system-scope release a default event performs when it is reached (an L2 write-back between two
+    steps) buys nothing here. `SPWGNN_SLOT_EVENT_FENCE=1` (A/B) uses the default flags."""
+
+    FLAGS = 0x2 | 0x20000000   # hipEventDisableTiming | hipEventDisableSystemFence
+
+    def __init__(self):
+        self.hip = _lib.hip_runtime()
+        flags = 0x2 if os.environ.get("SPWGNN_SLOT_EVENT_FENCE", "0") not in ("", "0") else self.FLAGS
+        h = C.c_void_p()
+        st = self.hip.hipEventCreateWithFlags(C.byref(h), C.c_uint(flags))
+        if st != 0:
+            raise _lib.SpwgnnError(f"hipEventCreateWithFlags failed ({st})")
+        self.h = h
+
+    def record(self, stream: torch.cuda.Stream) -> None:
+        st = self.hip.hipEventRecord(self.h, C.c_void_p(stream.cuda_stream))
+        if st != 0:
+            raise _lib.SpwgnnError(f"hipEventRecord failed ({st})")
+
+    def synchronize(self) -> None:
+        st = self.hip.hipEventSynchronize(self.h)
+        if st != 0:
+            raise _lib.SpwgnnError(f"hipEventSynchronize failed ({st})")
+
+    def __del__(self):
+        try:
+            self.hip.hipEventDestroy(self.h)
+        except Exception:
+            pass
+
+
 class ReplayStep:
     """One batch geometry's training step (forward, BCE, backward, Adam) as a replayed hipGraph.
 
@@ -161,7 +198,7 @@ class ReplayStep:
         self.fold = E.FOLD_PROLOGUE and "pre" in inspect.signature(body).parameters
         self.use_graph = graph
         self.graphs: list = [None] * StaticBatch.SLOTS
-        self.done: list = [None] * StaticBatch.SLOTS   # per slot: event after the last step that read it
+        self.done: list = [None] * StaticBatch.SLOTS   # per slot: SlotEvent after the last step that read it
         self.calls = 0
         self.replays = 0
 
@@ -199,9 +236,9 @@ class ReplayStep:
                     with torch.cuda.graph(g):
                         self._issue(j)
                     self.graphs[j] = g
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        self.done[k] = ev
+        if self.done[k] is None:
+            self.done[k] = SlotEvent()
+        self.done[k].record(cur)
 
 
 class ReplayCache:
