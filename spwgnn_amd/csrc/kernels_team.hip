@@ -20,7 +20,7 @@
 namespace spw {
 
 #ifdef SPWGNN_DIAG   // phase stamps (shader clock) of workgroup 0's waves 0 and 4: spwgnn_diag_team_stamps
-__device__ unsigned long long g_team_stamps[2][16];
+__device__ unsigned long long g_team_stamps[2][32];   // 0-15 node body / step loop, 16-24 edge body
 #define TEAM_STAMP(i)                                                                              \
     do {                                                                                           \
         const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   /* 100 MHz */            \
@@ -813,6 +813,7 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
     const int T = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int4 info = reinterpret_cast<const int4*>(a.wtile)[wt];
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
+    TEAM_STAMP(16);
     uint4 wf[10][NP];   // tile T's W2 fragments, all ten k-blocks
 #pragma unroll
     for (int kb = 0; kb < 10; ++kb)
@@ -828,6 +829,7 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
         const int s = a.esrc[(int64_t)blk * 32 + i], d = a.edst[(int64_t)blk * 32 + i];
         const bool valid = s >= 0;
         const uint64_t vmask = __ballot(valid);
+        TEAM_STAMP(22);
         const float vcap = valid ? __builtin_huge_valf() : 0.f;   // relu_valid: 0 on padding edges
         {   // k-blocks 2T, 2T+1: chunks q = 4T .. 4T+3 (q < 19)
             const int sc = valid ? s : n0, dc = valid ? d : n0;
@@ -858,11 +860,13 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
                     xv[4 * c + 2] = relu_valid(av.z + uv.z + vv.z, vcap);
                     xv[4 * c + 3] = relu_valid(av.w + uv.w + vv.w, vcap);
                 }
+                if (k == 0) TEAM_STAMP(23);
                 uint32_t sp[3][4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) split2(xv[2 * m], xv[2 * m + 1], sp[0][m], sp[1][m], sp[2][m]);
 #pragma unroll
                 for (int p = 0; p < NP; ++p) buf[(kb * 3 + p) * 64 + lane] = make_uint4(sp[p][0], sp[p][1], sp[p][2], sp[p][3]);
+                if (k == 0) TEAM_STAMP(24);
                 if (mrow) {   // h1 > 0 bits of the block's real chunks (as k_edge_fwd_x6)
                     uint64_t bal[2][4];
 #pragma unroll
@@ -891,8 +895,11 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
             }
             if (mrow && T == 0 && lane < 8) mrow[2 * kKhE + lane] = 0u;   // features 152..159 (padding)
         }
+        TEAM_STAMP(17);
         team_sync();   // the block's split h1 (the other buffer is free: every wave passed this barrier)
+        TEAM_STAMP(18);
         f32x16 acc = team_lds_gemm<NP>(buf, wf, lane);
+        TEAM_STAMP(19);
         const uint32_t vh = (uint32_t)vmask >> (4 * h);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -922,6 +929,7 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) m2row[64 * k + lane] = t7 == T ? mw2[k] : 0u;
         }
+        TEAM_STAMP(20);
         // receiver sum of tile T (NodeSum16X6::add for t = T)
         {
             const int g = lane >> 4;
@@ -962,6 +970,7 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
                         ao, as_bf16x8(make_uint4(P[u][p][0], P[u][p][1], P[u][p][2], P[u][p][3])), nacc[u], 0, 0, 0);
         }
     }
+    TEAM_STAMP(21);
     // H2s rows of tile T (NodeSum16X6::store for sub-tiles 2T, 2T+1)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1530,7 +1539,7 @@ hipError_t launch_enc_edge_bwd_team(const EncEdgeBwdArgs& a, int math, hipStream
 }  // namespace spw
 
 #ifdef SPWGNN_DIAG
-extern "C" int32_t spwgnn_diag_team_stamps(unsigned long long* out32) {
-    return hipMemcpyFromSymbol(out32, HIP_SYMBOL(spw::g_team_stamps), sizeof(spw::g_team_stamps)) == hipSuccess ? 0 : -1;
+extern "C" int32_t spwgnn_diag_team_stamps(unsigned long long* out64) {
+    return hipMemcpyFromSymbol(out64, HIP_SYMBOL(spw::g_team_stamps), sizeof(spw::g_team_stamps)) == hipSuccess ? 0 : -1;
 }
 #endif
