@@ -41,6 +41,8 @@ def _step(flat, batch, run, ws, tgt):
     ((6, False), 40, "x6"),       # the fused small-batch loops
     ((6, False), 40, "bf16"),
     ((6, False), 600, "f32"),
+    ((20, True), 300, "x6"),      # 17–32-node wave-tiles (W8 edge forward, fp32 storage)
+    ((20, True), 300, "bf16"),    # … in bf16 math: A, U, V rounded into fp32 storage
 ])
 def test_repeat_on_poisoned_workspace_is_bitwise(kind, B, math):
     batch = _batch(kind, B, seed=21)
@@ -56,3 +58,27 @@ def test_repeat_on_poisoned_workspace_is_bitwise(kind, B, math):
     bad_g = [name for name, o, shape in P.layout()
              if not torch.equal(g0[o:o + int(np.prod(shape))], g1[o:o + int(np.prod(shape))])]
     assert bad_z == 0 and not bad_g, f"logits differing {bad_z}, gradients differing {bad_g}"
+
+
+@pytest.mark.parametrize("N,B,math,recv", [(32, 300, "x6", True), (32, 300, "x6", False), (12, 3000, "x6", False),
+                                            (12, 3000, "bf16", False), (6, 40, "x6", False)])
+def test_inference_repeat_on_poisoned_workspace_is_bitwise(N, B, math, recv):
+    """The inference forward (two-slot P/U/V/H2s rotation, receiver-block plans of config 5)."""
+    obj, Rs, Rr, prop, _ = D.synthetic_batch(B, N, seed=22, fully_connected=True)
+    if N > 16:   # receiver-block plan (spwgnn_plan_fill_recv, as config 5 plans its towers) or not
+        m_idx, j_idx = np.nonzero(~np.eye(N, dtype=bool))
+        src = (np.arange(B)[:, None] * N + m_idx[None]).reshape(-1).astype(np.int32)
+        dst = (np.arange(B)[:, None] * N + j_idx[None]).reshape(-1).astype(np.int32)
+        batch = TowerBatch.from_edges(obj.reshape(B * N, 3), np.full(B, N, np.int32), src, dst,
+                                      np.full(B, N * (N - 1), np.int32), device="cuda", recv_blocks=recv)
+    else:
+        batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    flat = P.to_flat(O.random_params(4), device="cuda")
+    run = E.RunConfig(10 if N == 32 else 5, training=False, math=math)
+    z0 = E.forward(flat, batch, run, E.Workspace("cuda")).clone()
+    ws = E.Workspace("cuda")
+    ws.get(E.workspace_bytes(batch, run)).fill_(0xFF)
+    z1 = E.forward(flat, batch, run, ws).clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(z0).all()
+    assert torch.equal(z0, z1), f"{int((z0 != z1).sum())} logits differ"
