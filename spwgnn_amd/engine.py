@@ -112,6 +112,20 @@ class Prologue:
         return p
 
 
+# SPWGNN_POISON_WORKSPACE=1: fill every newly allocated workspace with 0xFF bytes (and the logits,
+# gradient and d/d'propagation' outputs with NaN), so a kernel that reads workspace it did not write,
+# or leaves part of an output unwritten, turns results into NaN (run the GPU suite with it;
+# tests/test_gpu_determinism.py does the same per case)
+POISON_WORKSPACE = os.environ.get("SPWGNN_POISON_WORKSPACE", "0") not in ("", "0")
+
+
+def _poison(t: torch.Tensor) -> torch.Tensor:
+    """An output buffer the library must write in full: NaN-filled under SPWGNN_POISON_WORKSPACE."""
+    if POISON_WORKSPACE and t.is_floating_point():
+        t.fill_(float("nan"))
+    return t
+
+
 class Workspace:
     """Device scratch for one forward (+ its backward). Sized by spwgnn_workspace_bytes."""
 
@@ -138,6 +152,8 @@ class Workspace:
         if self.buf is None or self.buf.numel() < nbytes:
             self.buf = None
             self.buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            if POISON_WORKSPACE:   # debugging: every fresh workspace byte 0xFF (NaN as fp32)
+                self.buf.fill_(0xFF)
         return self.buf
 
 
@@ -187,7 +203,7 @@ def forward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Wo
     nbytes = workspace_bytes(batch, run)
     buf = ws.get(nbytes)
     if logits is None:
-        logits = torch.empty(batch.n_nodes, dtype=torch.float32, device=batch.device)
+        logits = _poison(torch.empty(batch.n_nodes, dtype=torch.float32, device=batch.device))
     b = batch.cstruct()
     r = run.cstruct(with_prologue=True)
     st = _lib.lib().spwgnn_forward(flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(),
@@ -210,8 +226,8 @@ def backward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: W
     dlogits = dlogits.contiguous().to(torch.float32)
     _require_gpu(dlogits, "dlogits")
     if grads is None:
-        grads = torch.empty_like(flat_params)
-    dprop = torch.empty(batch.n_nodes, 100, dtype=torch.float32, device=batch.device) if want_dprop else None
+        grads = _poison(torch.empty_like(flat_params))
+    dprop = _poison(torch.empty(batch.n_nodes, 100, dtype=torch.float32, device=batch.device)) if want_dprop else None
     b = batch.cstruct()
     r = run.cstruct()
     buf = ws.buf
@@ -236,7 +252,7 @@ def bce(logits: torch.Tensor, targets: torch.Tensor, scratch: BceScratch, dlogit
     same launch also does total3 += out3.double() * weights3 (spwgnn_bce_accumulate)."""
     targets = targets.reshape(-1).to(torch.float32).contiguous()
     if dlogits is None:
-        dlogits = torch.empty_like(logits)
+        dlogits = _poison(torch.empty_like(logits))
     args = (logits.data_ptr(), targets.data_ptr(), logits.numel(), scratch.out3.data_ptr(), dlogits.data_ptr(),
             scratch.scratch.data_ptr())
     if total3 is None:
