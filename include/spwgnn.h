@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define SPWGNN_ABI_VERSION 5   /* 5: spwgnn_team_max_blocks, spwgnn_host_device_ptr, spwgnn_plan_order, spwgnn_run.grads_early_event; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
+#define SPWGNN_ABI_VERSION 6   /* 6: spwgnn_bce_backward; 5: spwgnn_team_max_blocks, spwgnn_host_device_ptr, spwgnn_plan_order, spwgnn_run.grads_early_event; 4: spwgnn_run.prologue; 3: spwgnn_batch.flags, receiver-block plans */
 
 #define SPWGNN_OK 0
 #define SPWGNN_E_ARG (-1)           /* bad argument (null pointer, negative size, …)          */
@@ -245,6 +245,17 @@ int32_t spwgnn_bce(const float* logits, const float* targets, int64_t n, float* 
 int32_t spwgnn_bce_accumulate(const float* logits, const float* targets, int64_t n, float* out3,
                               float* dlogits, void* scratch, const double* weights3, double* total3,
                               spwgnn_stream_t stream);
+/* ABI 6: spwgnn_bce (weights3 = total3 = NULL) or spwgnn_bce_accumulate, then spwgnn_backward on the
+ * dlogits it wrote — one call, the same results bit for bit (logits: the forward's output on this
+ * workspace). Where the backward runs its fused small-batch loop and the loss fits one workgroup
+ * (n <= 256, the reference's batch 32), the loop computes dlogits itself (still stored to dlogits)
+ * and the loss sums ride in the backward's last launch: a training step needs no loss launch of its
+ * own (Keras fit, main.py:92-98). Replaces the Keras loss + autodiff pair of Networks.py:102. */
+int32_t spwgnn_bce_backward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run,
+                            void* workspace, int64_t workspace_bytes, const float* logits,
+                            const float* targets, int64_t n, float* out3, float* dlogits, void* bce_scratch,
+                            const double* weights3, double* total3, float* grads, float* dprop,
+                            spwgnn_stream_t stream);
 
 /* Keras-2.x Adam (Networks.py:101: lr=5e-4, decay=0): in-place on the flat buffer.
  * g' = grad_scale*grad + 2*l2*param; lr_t = lr*sqrt(1-b2^t)/(1-b1^t);

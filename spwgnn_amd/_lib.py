@@ -54,7 +54,7 @@ K_EDGE_FWD, K_NODE_FWD, K_EDGE_BWD, K_NODE_BWD, K_ENC_EDGE, K_ENC_EDGE_BWD, K_WG
 K_WGRAD_WS, K_ENC_NODE, K_ENC_NODE_BWD = 9, 10, 11
 MATH_F32, MATH_X6, MATH_BF16 = 0, 1, 2
 STEP_KEY_COUNTER, STEP_KEY_SPLITMIX = 0, 1
-ABI_VERSION = 5        # SPWGNN_ABI_VERSION this binding's structs follow
+ABI_VERSION = 6        # SPWGNN_ABI_VERSION this binding's structs follow
 BATCH_RECV_BLOCKS = 1  # spwgnn_batch.flags: a receiver-block plan (spwgnn_plan_fill_recv)
 READOUT_SUM_PROB, READOUT_MEAN_PROB, READOUT_SUM_LOGIT, READOUT_MEAN_LOGIT = 0, 1, 2, 3
 
@@ -86,6 +86,7 @@ def _declare(lib: C.CDLL) -> None:
         "spwgnn_bce_scratch_bytes": (i64, [i64]),
         "spwgnn_bce": (i32, [vp, vp, i64, vp, vp, vp, vp]),
         "spwgnn_bce_accumulate": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp]),
+        "spwgnn_bce_backward": (i32, [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
         "spwgnn_adam": (i32, [vp, vp, vp, vp, i64, i32, f32, f32, f32, f32, f32, f32, vp]),
         "spwgnn_adam_dev": (i32, [vp, vp, vp, vp, i64, vp, vp, i32, f32, f32, f32, f32, f32, vp]),
         "spwgnn_adam_lr_table": (i32, [f32, f32, f32, i32, vp]),

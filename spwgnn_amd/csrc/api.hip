@@ -790,7 +790,7 @@ static void ws_group(WsBatch* wsb, int first, int n) {
 }
 
 int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_run* r, const Ws& w, char* base,
-                     const float* dlogits, float* grads, float* dprop, hipStream_t st) {
+                     const float* dlogits, float* grads, float* dprop, hipStream_t st, const BceArgs* bce = nullptr) {
     (void)params;  // the packed copies made by the forward on this workspace are used
     Ctx c{w, base};
     const int S = r->mp_steps;
@@ -956,6 +956,10 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     const bool split = r->grads_early_event != nullptr;
     int32_t e = SPWGNN_OK;
     const bool fused = bwd_fused_taken(r, b);
+    // spwgnn_bce_backward: on the fused loop (one loss workgroup) the loop computes dlogits itself and
+    // the loss sums ride in the last reduction launch; anywhere else the loss launch runs first
+    const bool bce_inline = bce && fused && bce->blocks == 1;
+    if (bce && !bce_inline) SPW_CHECK(launch_bce(*bce, st));
     auto edge_encoder_bwd = [&]() -> int32_t {   // dA rebuild + relation encoder backward (wide kernels)
         if (rebuild) {
             SPW_CHECK(prof.before(SPWGNN_K_DA));
@@ -973,6 +977,12 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         fa.nb = node_args(0);
         fa.nb.dU = c.f(w.dU_at(1));   // step 0's incoming dU/dV (BwdFusedArgs)
         fa.nb.dV = c.f(w.dV_at(1));
+        if (bce_inline) {
+            fa.nb.bce_logits = bce->logits;
+            fa.nb.bce_targets = bce->targets;
+            fa.nb.bce_dlogits = bce->dlogits;
+            fa.nb.bce_n = bce->n;
+        }
         fa.tail = tl;
         fa.has_tail = dprop != nullptr;
         fa.eb = edge_args(0);
@@ -1151,10 +1161,15 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     // ranges of those tensors no such reduction writes (alignment gaps, uncovered tensor rows). More
     // ranges than the launch carries (kMaxZero) or no reduction: one memset of those tensors instead
     // (stream-ordered before the reduction, which then writes its ranges)
-    auto reduce = [&](int t_lo, int t_hi) -> int32_t {
+    auto reduce = [&](int t_lo, int t_hi, bool last) -> int32_t {
         const ParamTable& pt = param_table();
         const int64_t lo = pt.t[t_lo].offset, hi = t_hi < kNumTensors ? pt.t[t_hi].offset : pt.total;
         ReduceBatch sub{};
+        if (last && bce_inline) {   // the loss sums: one more row of this launch
+            sub.bce_row = 1;
+            sub.bce = *bce;
+            sub.bce.dlogits = nullptr;   // written by the step loop
+        }
         for (int k = 0; k < rb.n; ++k) {
             const int64_t off = rb.r[k].kernel_off >= 0 ? rb.r[k].kernel_off : rb.r[k].bias_off;
             if (off >= lo && off < hi) sub.r[sub.n++] = rb.r[k];
@@ -1205,14 +1220,14 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
         if ((e = g_om0())) return e;
         if ((e = g_om1())) return e;
         if ((e = launch_ws(wsb, true))) return e;
-        return reduce(0, kNumTensors);
+        return reduce(0, kNumTensors, true);
     }
     // split: the early group needs only the step loop and the node encoder's backward (Σ do1, dzo2)
     if ((e = g_w2())) return e;
     if ((e = g_node())) return e;
     if ((e = g_om1())) return e;
     if ((e = launch_ws(wsb, false))) return e;
-    if ((e = reduce(T_RMP1K, kNumTensors))) return e;
+    if ((e = reduce(T_RMP1K, kNumTensors, false))) return e;
     SPW_CHECK(hipEventRecord(static_cast<hipEvent_t>(r->grads_early_event), st));
     if (!fused && (e = edge_encoder_bwd())) return e;
     wsp = unbatched ? nullptr : &wsb2;
@@ -1220,7 +1235,7 @@ int32_t run_backward(const float* params, const spwgnn_batch* b, const spwgnn_ru
     if ((e = g_om0())) return e;
     if ((e = g_rm123_w1a())) return e;
     if ((e = launch_ws(wsb2, true))) return e;
-    return reduce(0, T_RMP1K);
+    return reduce(0, T_RMP1K, true);
 }
 
 }  // namespace spw
@@ -1279,6 +1294,32 @@ int32_t spwgnn_backward(const float* params, const spwgnn_batch* batch, const sp
     if (workspace_bytes < w.total) return SPWGNN_E_WORKSPACE;
     return run_backward(params, batch, run, w, static_cast<char*>(workspace), dlogits, grads, dprop,
                         static_cast<hipStream_t>(stream));
+}
+
+int32_t spwgnn_bce_backward(const float* params, const spwgnn_batch* batch, const spwgnn_run* run, void* workspace,
+                            int64_t workspace_bytes, const float* logits, const float* targets, int64_t n,
+                            float* out3, float* dlogits, void* bce_scratch, const double* weights3, double* total3,
+                            float* grads, float* dprop, spwgnn_stream_t stream) {
+    int32_t stt = validate(batch, run);
+    if (stt) return stt;
+    if (!run->training) return SPWGNN_E_NOTRAIN;
+    if (!params || !workspace || !grads || !logits || !targets || !out3 || !dlogits || !bce_scratch || n < 1 ||
+        (!weights3) != (!total3))
+        return SPWGNN_E_ARG;
+    Ws w = make_ws(batch->n_nodes, batch->n_eblocks, run->mp_steps, 1);
+    if (workspace_bytes < w.total) return SPWGNN_E_WORKSPACE;
+    BceArgs a{};   // as spwgnn_bce_accumulate builds it
+    a.w3 = weights3;
+    a.tot3 = total3;
+    a.logits = logits;
+    a.targets = targets;
+    a.n = n;
+    a.dlogits = dlogits;
+    a.partial = static_cast<float*>(bce_scratch);
+    a.out3 = out3;
+    a.blocks = (int)std::min<int64_t>(256, (n + 255) / 256);
+    return run_backward(params, batch, run, w, static_cast<char*>(workspace), dlogits, grads, dprop,
+                        static_cast<hipStream_t>(stream), &a);
 }
 
 int64_t spwgnn_bce_scratch_bytes(int64_t n) {

@@ -184,6 +184,12 @@ struct NodeBwdArgs {
     const uint4 *x_w1bt, *x_w1ct, *x_wo2t, *x_wo1ct, *x_wo1at, *x_wo1pt, *x_w3t;   // x6 images
     const uint4 *xh_w1bt, *xh_w1ct, *xh_wo2t, *xh_wo1ct, *xh_wo1at, *xh_wo1pt;      // half-tile forms (§3w)
     int n16;        // bf16 math (training, wide kernels): dU, dV, o1 read and dx, g stored as bf16 (§3g)
+    // spwgnn_bce_backward on the fused small-batch loop: the first step computes dlogits from the
+    // logits and targets itself (k_bce_partial's expression, also stored to bce_dlogits) instead of
+    // reading dlogits
+    const float *bce_logits, *bce_targets;
+    float* bce_dlogits;
+    int64_t bce_n;
 };
 
 struct EdgeBwdArgs {
@@ -326,16 +332,6 @@ struct WsBatch {           // the k_wgrad_ws gradients of one backward (k_wgrad_
 
 constexpr int kMaxReduce = 16;
 constexpr int kMaxZero = 48;
-struct ReduceBatch {       // the weight gradients of one backward, reduced in one launch (blockIdx.y)
-    ReduceArgs r[kMaxReduce];
-    int n;
-    // float ranges of the flat gradient buffer no reduction writes (the 64-float alignment gaps between
-    // tensors, tensors without rows in this batch): zeroed by the extra row blockIdx.y == n of the
-    // same launch (was a separate hipMemsetAsync of the whole buffer before the backward)
-    int nzero;
-    int64_t zoff[kMaxZero];
-    int32_t zlen[kMaxZero];
-};
 struct BceArgs {
     const float *logits, *targets;
     int64_t n;
@@ -345,6 +341,27 @@ struct BceArgs {
     int blocks;
     const double* w3;   // non-null: tot3[k] += (double)out3[k] * w3[k] by the thread that writes out3
     double* tot3;
+};
+// Keras binary_crossentropy (Networks.py:102): clip(ŷ, 1e-7, 1-1e-7) ≡ clamp(z, ±ln((1-ε)/ε)).
+constexpr float kLogitClip = 16.11809565f;
+// dL/dz of one node (k_bce_partial's expression; the fused backward's inline form uses it too)
+__device__ __forceinline__ float bce_dlogit(float z0, float t, float inv_n) {
+    const float p = 1.f / (1.f + expf(-z0));
+    return fabsf(z0) < kLogitClip ? (p - t) * inv_n : 0.f;
+}
+struct ReduceBatch {       // the weight gradients of one backward, reduced in one launch (blockIdx.y)
+    ReduceArgs r[kMaxReduce];
+    int n;
+    // 1: the launch's last row (its first workgroup) is k_bce_partial<true> on `bce` (one workgroup's
+    // loss / accuracy sums: spwgnn_bce_backward's loss, off the backward's critical path)
+    int bce_row;
+    BceArgs bce;
+    // float ranges of the flat gradient buffer no reduction writes (the 64-float alignment gaps between
+    // tensors, tensors without rows in this batch): zeroed by the extra row blockIdx.y == n of the
+    // same launch (was a separate hipMemsetAsync of the whole buffer before the backward)
+    int nzero;
+    int64_t zoff[kMaxZero];
+    int32_t zlen[kMaxZero];
 };
 struct AdamArgs {
     float *p, *m, *v;

@@ -1534,8 +1534,13 @@ void k_wgrad_ws_batch(WsBatch b, Pos3Batch p3) {
 // workgroup takes 32 elements × 8 chunk groups: thread (e, g) sums chunks g, g+8, … (four interleaved
 // sums), then the 8 partial sums meet in LDS — a 256-chunk gradient is 8 dependent load rounds per
 // thread instead of 64 (the reduction was latency-bound: 66 µs at config 2, 74 µs at the headline).
+__device__ __forceinline__ void bce_block_final(const BceArgs& a);
 __global__ __launch_bounds__(256) void k_wgrad_reduce_all(ReduceBatch rb) {
     __shared__ float part[8][32];
+    if (rb.bce_row && blockIdx.y == gridDim.y - 1) {   // spwgnn_bce_backward: the loss sums
+        if (blockIdx.x == 0) bce_block_final(rb.bce);
+        return;
+    }
     if ((int)blockIdx.y == rb.n) {   // the ranges no reduction writes: zeros
         for (int z = 0; z < rb.nzero; ++z)
             for (int e = blockIdx.x * 256 + threadIdx.x; e < rb.zlen[z]; e += gridDim.x * 256) rb.r[0].out[rb.zoff[z] + e] = 0.f;
@@ -1571,8 +1576,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_all(ReduceBatch rb) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Keras binary_crossentropy (Networks.py:102): clip(ŷ, 1e-7, 1-1e-7) ≡ clamp(z, ±ln((1-ε)/ε)).
-constexpr float kLogitClip = 16.11809565f;
+// Keras binary_crossentropy (Networks.py:102): kLogitClip and bce_dlogit in kernels.h.
 
 // FINAL (a.blocks == 1, e.g. the reference's batch 32): the one workgroup also writes out3, the
 // same double-precision division k_bce_final does over its one partial — one launch instead of two.
@@ -1586,18 +1590,20 @@ __device__ inline void bce_store_out3(const BceArgs& a, float loss, float correc
     }
 }
 
+// one workgroup (256 threads, `blk` of a.blocks) of the loss: k_bce_partial, and the extra row of the
+// gradient reductions under spwgnn_bce_backward
 template <bool FINAL>
-__global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
+__device__ __forceinline__ void bce_block(const BceArgs& a, int blk) {
     __shared__ float sl[256], sc[256];
     float ls = 0.f, cs = 0.f;
     const float inv_n = 1.0f / (float)a.n;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (int64_t)a.blocks * 256) {
+    for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < a.n; i += (int64_t)a.blocks * 256) {
         const float z0 = a.logits[i], t = a.targets[i];
         const float z = fminf(fmaxf(z0, -kLogitClip), kLogitClip);
         ls += fmaxf(z, 0.f) - z * t + log1pf(expf(-fabsf(z)));
         const float p = 1.f / (1.f + expf(-z0));
         cs += ((p > 0.5f ? 1.f : 0.f) == t) ? 1.f : 0.f;
-        if (a.dlogits) a.dlogits[i] = fabsf(z0) < kLogitClip ? (p - t) * inv_n : 0.f;
+        if (a.dlogits) a.dlogits[i] = bce_dlogit(z0, t, inv_n);
     }
     sl[threadIdx.x] = ls;
     sc[threadIdx.x] = cs;
@@ -1613,11 +1619,16 @@ __global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
         if constexpr (FINAL) {
             bce_store_out3(a, (float)((double)sl[0] / (double)a.n), (float)(double)sc[0]);
         } else {
-            a.partial[2 * blockIdx.x] = sl[0];
-            a.partial[2 * blockIdx.x + 1] = sc[0];
+            a.partial[2 * blk] = sl[0];
+            a.partial[2 * blk + 1] = sc[0];
         }
     }
 }
+template <bool FINAL>
+__global__ __launch_bounds__(256) void k_bce_partial(BceArgs a) {
+    bce_block<FINAL>(a, blockIdx.x);
+}
+__device__ __forceinline__ void bce_block_final(const BceArgs& a) { bce_block<true>(a, 0); }
 
 __global__ void k_bce_final(BceArgs a) {
     if (threadIdx.x != 0) return;
@@ -1951,6 +1962,10 @@ hipError_t launch_wgrad_ws_batch(const WsBatch& b, int math, hipStream_t st, con
 // workgroup dispatch, not its sums, was most of its 11 µs. Deterministic (a fixed order per element).
 constexpr int kReduceSmallChunks = 64;
 __global__ __launch_bounds__(256) void k_wgrad_reduce_small(ReduceBatch rb) {
+    if (rb.bce_row && blockIdx.y == gridDim.y - 1) {   // spwgnn_bce_backward: the loss sums
+        if (blockIdx.x == 0) bce_block_final(rb.bce);
+        return;
+    }
     if ((int)blockIdx.y == rb.n) {   // the ranges no reduction writes: zeros
         for (int z = 0; z < rb.nzero; ++z)
             for (int e = blockIdx.x * 256 + threadIdx.x; e < rb.zlen[z]; e += gridDim.x * 256) rb.r[0].out[rb.zoff[z] + e] = 0.f;
@@ -1976,10 +1991,12 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_small(ReduceBatch rb) {
     if (bias) a.out[a.bias_off + col] = s;
 }
 hipError_t launch_wgrad_reduce_all(const ReduceBatch& rb, hipStream_t st) {
-    if (rb.n <= 0) return rb.nzero > 0 ? hipErrorInvalidValue : hipSuccess;   // the zero row writes through r[0].out
+    if (rb.bce_row && (rb.bce.blocks != 1 || rb.bce.dlogits)) return hipErrorInvalidValue;   // one FINAL workgroup
+    if (rb.n <= 0 && rb.nzero > 0) return hipErrorInvalidValue;   // the zero row writes through r[0].out
+    if (rb.n <= 0 && !rb.bce_row) return hipSuccess;
     int maxc = 0;
     for (int k = 0; k < rb.n; ++k) maxc = rb.r[k].chunks > maxc ? rb.r[k].chunks : maxc;
-    const int rows = rb.n + (rb.nzero > 0 ? 1 : 0);
+    const int rows = rb.n + (rb.nzero > 0 ? 1 : 0) + (rb.bce_row ? 1 : 0);
     if (maxc <= kReduceSmallChunks)
         hipLaunchKernelGGL(k_wgrad_reduce_small, dim3((160 * 160 + 255) / 256, rows), dim3(256), 0, st, rb);
     else

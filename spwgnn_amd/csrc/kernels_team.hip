@@ -678,7 +678,15 @@ __device__ __forceinline__ void node_bwd_team_body(const NodeBwdArgs& a, const T
         // the residual path: dP_s gets dpre directly (Add()([prop_layer(x), prop]))
         R.store<kKhN>(a.dPout, D, T);
         dP = D;
-        if (a.first && T == 3 && h == 1) D[0] = valid ? a.dlogits[R.n] : 0.f;   // x' row 100 = logit
+        if (a.first && T == 3 && h == 1) {   // x' row 100 = logit
+            if (a.bce_logits) {   // spwgnn_bce_backward: dL/dz here (spwgnn_bce's bits), also stored
+                const float dl = valid ? bce_dlogit(a.bce_logits[R.n], a.bce_targets[R.n], 1.0f / (float)a.bce_n) : 0.f;
+                if (valid) a.bce_dlogits[R.n] = dl;
+                D[0] = dl;
+            } else {
+                D[0] = valid ? a.dlogits[R.n] : 0.f;
+            }
+        }
         R.store<kKhN>(a.dx, D, T);
         act.put(0, T, D, lane);
     }

@@ -238,6 +238,41 @@ def backward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: W
     return grads, dprop
 
 
+def bce_backward(flat_params: torch.Tensor, batch: TowerBatch, run: RunConfig, ws: Workspace, logits: torch.Tensor,
+                 targets: torch.Tensor, scratch: "BceScratch", dlogits: Optional[torch.Tensor] = None,
+                 total3: Optional[torch.Tensor] = None, weights3: Optional[torch.Tensor] = None,
+                 grads: Optional[torch.Tensor] = None, want_dprop: bool = False):
+    """bce (or its accumulating form) then backward in one library call (spwgnn_bce_backward, ABI 6):
+    bit-identical to the two calls; on the fused small-batch loop the loss needs no launch of its own.
+    Returns (out3, dlogits, grads, dprop)."""
+    if not run.training:
+        raise _lib.SpwgnnError("backward needs a training forward on the same workspace")
+    if not ws.holds(batch, run):
+        raise _lib.SpwgnnError("backward needs the training forward of the same batch and RunConfig "
+                               f"on this workspace (stored {ws.fwd_key}, asked {Workspace.key(batch, run)})")
+    targets = targets.reshape(-1).to(torch.float32).contiguous()
+    _require_gpu(logits, "logits")
+    if dlogits is None:
+        dlogits = _poison(torch.empty_like(logits))
+    if grads is None:
+        grads = _poison(torch.empty_like(flat_params))
+    if (total3 is None) != (weights3 is None):
+        raise ValueError("total3 and weights3 go together")
+    if total3 is not None:
+        assert total3.dtype == torch.float64 and weights3.dtype == torch.float64
+    dprop = _poison(torch.empty(batch.n_nodes, 100, dtype=torch.float32, device=batch.device)) if want_dprop else None
+    b = batch.cstruct()
+    r = run.cstruct()
+    buf = ws.buf
+    st = _lib.lib().spwgnn_bce_backward(
+        flat_params.data_ptr(), C.byref(b), C.byref(r), buf.data_ptr(), buf.numel(), logits.data_ptr(),
+        targets.data_ptr(), logits.numel(), scratch.out3.data_ptr(), dlogits.data_ptr(), scratch.scratch.data_ptr(),
+        weights3.data_ptr() if weights3 is not None else None, total3.data_ptr() if total3 is not None else None,
+        grads.data_ptr(), dprop.data_ptr() if dprop is not None else None, _stream(batch.device))
+    _lib.check(st, "spwgnn_bce_backward")
+    return scratch.out3, dlogits, grads, dprop
+
+
 class BceScratch:
     def __init__(self, device):
         n = int(_lib.lib().spwgnn_bce_scratch_bytes(1))

@@ -154,8 +154,10 @@ class KerasModel:
                 E.step_advance(ctr.key, ctr.step, _lib.STEP_KEY_COUNTER)
             run = E.RunConfig(net.mp_steps, training=True, dropout=net.dropout, seed_dev=ctr.key, prologue=pro)
             E.forward(net.flat.data, batch, run, ws, logits=z)
-            E.bce(z, target, bce, dlogits=dz, total3=self._tot, weights3=w3)   # loss + epoch sums, one launch
-            E.backward(net.flat.data, batch, run, ws, dz, grads=self._grads)
+            # loss + epoch sums and the backward in one call: on the fused small-batch loop the loss
+            # needs no launch of its own (spwgnn_bce_backward)
+            E.bce_backward(net.flat.data, batch, run, ws, z, target, bce, dlogits=dz, total3=self._tot, weights3=w3,
+                           grads=self._grads)
             E.adam_dev(net.flat.data, self._grads, self.m, self.v, ctr.step, ctr.lr_table, self.beta1, self.beta2,
                        self.eps, self.l2)
         return body

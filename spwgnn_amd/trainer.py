@@ -172,8 +172,9 @@ class Trainer:
             run = E.RunConfig(self.mp_steps, training=True, dropout=self.dropout, math=self.math, seed_dev=ctr.key,
                               prologue=pro)
             E.forward(self.params, batch, run, ws, logits=z)
-            out3, _ = E.bce(z, target, bce, dlogits=dz)
-            E.backward(self.params, batch, run, ws, dz, grads=grads)
+            # the loss and the backward in one call (spwgnn_bce_backward: no loss launch of its own on
+            # the fused small-batch loop; bit-identical to bce then backward)
+            E.bce_backward(self.params, batch, run, ws, z, target, bce, dlogits=dz, grads=grads)
             if w != 1.0:
                 grads.mul_(w)
             E.adam_dev(self.params, grads, self.m, self.v, ctr.step, ctr.lr_table, self.b1, self.b2, self.eps,

@@ -342,3 +342,37 @@ def test_bce_accumulate_equals_bce_then_accumulate(n):
     torch.cuda.synchronize()
     assert torch.equal(tot_a, tot_b)
     assert np.array_equal(tot_a.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("B,N,fully,math,split", [(32, 6, False, "x6", False), (32, 6, False, "bf16", False),
+                                                   (40, 6, True, "x6", True), (3000, 6, False, "x6", False),
+                                                   (64, 12, True, "x6", False)])
+def test_bce_backward_equals_bce_then_backward(B, N, fully, math, split):
+    """spwgnn_bce_backward (ABI 6) against spwgnn_bce_accumulate + spwgnn_backward, bit for bit: loss,
+    epoch sums, dlogits, every gradient and d/d'propagation'. Batch 32 of six boxes runs the folded form
+    (dlogits inside the fused backward loop, the loss sums in its last reduction); 3,000 towers (wide
+    kernels) and 64 towers of 12 boxes (n = 768 > 256: a multi-workgroup loss) take the loss launch
+    first; `split` adds the early gradient event (the loss row then rides in the second reduction)."""
+    obj, Rs, Rr, prop, tgt = D.synthetic_batch(B, N, seed=5, fully_connected=fully)
+    batch = TowerBatch.from_dense(obj, Rs, Rr, prop, device="cuda")
+    flat = P.to_flat(O.random_params(2), device="cuda")
+    run = E.RunConfig(5, training=True, math=math, dropout=0.1, seed=3)
+    if split:
+        run.grads_early_event = torch.cuda.Event()
+        run.grads_early_event.record()
+    t = torch.tensor(tgt.reshape(-1), device="cuda")
+    w3 = torch.tensor([float(B), 1.0, 1.0], dtype=torch.float64, device="cuda")
+    out = []
+    for fold in (False, True):
+        ws, sc = E.Workspace("cuda"), E.BceScratch("cuda")
+        tot = torch.zeros(3, dtype=torch.float64, device="cuda")
+        z = E.forward(flat, batch, run, ws)
+        if fold:
+            o3, dz, g, dp = E.bce_backward(flat, batch, run, ws, z, t, sc, total3=tot, weights3=w3, want_dprop=True)
+        else:
+            o3, dz = E.bce(z, t, sc, total3=tot, weights3=w3)
+            g, dp = E.backward(flat, batch, run, ws, dz, want_dprop=True)
+        torch.cuda.synchronize()
+        out.append((o3.clone(), tot.clone(), dz.clone(), g.clone(), dp.clone()))
+    for a, b, what in zip(out[0], out[1], ("out3", "total3", "dlogits", "grads", "dprop")):
+        assert torch.equal(a, b), what
