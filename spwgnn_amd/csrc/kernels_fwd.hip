@@ -39,17 +39,28 @@ __global__ void k_prep(PrepArgs a, PrepX6Args x) {
     if (id < PK_COUNT) {
         const PackDesc& d = a.desc[id];
         const int total = d.rows * d.cols;
-        for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-            int r, c;
-            if (d.k4) {  // idx = ((r>>2)·cols + c)·4 + (r&3)
-                const int q = idx >> 2, kb = q / d.cols;
-                c = q - kb * d.cols;
-                r = 4 * kb + (idx & 3);
-            } else {
-                r = idx / d.cols;
-                c = idx - r * d.cols;
+        // four elements per thread in flight (the largest pack, rmp.0's 350 × 150, is ≈ 13 elements per
+        // thread: one parameter load's latency each when issued one after the other)
+        const int stride = gridDim.x * blockDim.x;
+        for (int base = blockIdx.x * blockDim.x + threadIdx.x; base < total; base += 4 * stride) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int idx = base + u * stride;
+                int r, c;
+                if (d.k4) {  // idx = ((r>>2)·cols + c)·4 + (r&3)
+                    const int q = idx >> 2, kb = q / d.cols;
+                    c = q - kb * d.cols;
+                    r = 4 * kb + (idx & 3);
+                } else {
+                    r = idx / d.cols;
+                    c = idx - r * d.cols;
+                }
+                v[u] = idx < total ? pack_elem(d, a.params, r, c) : 0.f;
             }
-            a.pk[d.dst_off + idx] = pack_elem(d, a.params, r, c);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (base + u * stride < total) a.pk[d.dst_off + base + u * stride] = v[u];
         }
         return;
     }
