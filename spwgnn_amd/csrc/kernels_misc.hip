@@ -1981,6 +1981,18 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_small(ReduceBatch rb) {
     const float* p = a.slab + idx;
     float s0 = 0.f, s1 = 0.f;
     int c = 0;
+    // eight slabs' loads in flight, added in the same order as two at a time (even chunks into s0, odd
+    // into s1): the same bits, a quarter of the dependent load latencies (the W2 job's 32 slabs)
+    for (; c + 7 < a.chunks; c += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(c + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            s0 += v[u];
+            s1 += v[u + 1];
+        }
+    }
     for (; c + 1 < a.chunks; c += 2) {
         s0 += p[c * stride];
         s1 += p[(c + 1) * stride];
