@@ -175,7 +175,7 @@ class KerasModel:
         spwgnn_amd/replay.py — forward, BCE, backward and Adam per batch geometry on static buffers
         refilled by the step's first launch — issued eagerly (`graph=True`: the same step captured
         once and replayed as a hipGraph; bit-identical results; on the MI355X host eager issue is the
-        faster, 0.286 vs 0.294 ms per step at batch 32); batches are planned with
+        faster, 0.270 vs 0.277 ms per step at batch 32); batches are planned with
         N(N−1) relation slots per tower."""
         objects = np.asarray(x["objects"], np.float32)
         target = np.asarray(y["target"], np.float32).reshape(objects.shape[0], -1)
