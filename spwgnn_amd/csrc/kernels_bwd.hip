@@ -738,6 +738,11 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 #ifndef SPWGNN_DA_LOCKSTEP
 #define SPWGNN_DA_LOCKSTEP 1
 #endif
+// diagnosis builds only (wrong results, timing): 1 = every G3 row is node 0's (cache hits),
+// 2 = also no mask-word loads (constants)
+#ifndef SPWGNN_DA_DBG
+#define SPWGNN_DA_DBG 0
+#endif
 // N16 (bf16 math, §3g node side): dU, dV stored as bf16
 template <bool ACCUM, bool NODA = false, int NP = 3, int DBG = 0, bool N16 = false>   // DBG 3 (diagnosis): G3 rows of the tile's first node
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_edge_bwd_x6(EdgeBwdArgs a) {
@@ -1016,8 +1021,13 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     auto load_pair = [&](int blk, int s, int d) {
         Pair p;
         const bool valid = d >= 0;
-        p.G4 = reinterpret_cast<const float4*>(a.G3 + s * a.g3_step + cm_index<kKhE>(valid ? d : 0, 0) + h * 128);
+        p.G4 = reinterpret_cast<const float4*>(a.G3 + s * a.g3_step + cm_index<kKhE>(valid && SPWGNN_DA_DBG == 0 ? d : 0, 0) + h * 128);
         const uint32_t* m1 = a.mask1 + s * a.m1_step + (int64_t)blk * kLdE + i;
+        if (SPWGNN_DA_DBG >= 2) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t) p.w[t] = p.m1w[t] = valid ? 0x5a5a5a5au ^ (uint32_t)(blk * 5 + t) : 0u;
+            return p;
+        }
         load_m2(a.mask2 + s * a.m2_step + (int64_t)blk * kM2Blk, i, p.w);
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
