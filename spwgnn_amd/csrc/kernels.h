@@ -1,5 +1,11 @@
 // Kernel argument structs and declarations (libspwgnn_hip).
 #pragma once
+
+// one-hot node operands of the wide edge kernels built with ds_bpermute from packed tile-local ids
+// (SPWGNN_ONEHOT_BPERM=0: the readlane form, for A/B)
+#ifndef SPWGNN_ONEHOT_BPERM
+#define SPWGNN_ONEHOT_BPERM 1
+#endif
 #include "gemm_blocks.h"
 
 namespace spw {

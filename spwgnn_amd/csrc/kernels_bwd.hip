@@ -738,6 +738,11 @@ hipError_t launch_node_bwd(const NodeBwdArgs& a, int math, hipStream_t st) {
 #ifndef SPWGNN_DA_LOCKSTEP
 #define SPWGNN_DA_LOCKSTEP 1
 #endif
+// the k-block of the wide edge backward's loop that builds the one-hot node operand (≥ 10: after the loop;
+// A/B on one box, bitwise equal: kb 5 vs after the loop config 3 41.3 → 40.9 ms, config 4 34.2 → 34.0)
+#ifndef SPWGNN_OH_KB
+#define SPWGNN_OH_KB 5
+#endif
 // diagnosis builds only (wrong results, timing): 1 = every G3 row is node 0's (cache hits),
 // 2 = also no mask-word loads (constants)
 #ifndef SPWGNN_DA_DBG
@@ -784,6 +789,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int fb = info.x, nb = info.y, n0 = info.z, nn = info.w;
     const int4 ninfo = wtiles[min(wt + wstep, a.n_wtiles - 1)];
     const int key = i < 16 ? n0 + i : n0 + i - 16;   // one-hot rows: receivers, then senders
+    const int kbits = i < 16 ? 0 : 16;                 // ... their half of a packed local-id word
     f32x16 nacc[5];
     zero_tiles(nacc);
     for (int bb = 0; bb < nb; ++bb) {
@@ -803,6 +809,32 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                                     : ((uint64_t)w[4] << 52 | (uint64_t)w[3] << 20 | (w[2] >> 12));
         const uint32_t mhi = h == 0 ? (w[2] & 0xfffu) : (w[4] >> 12);
         const float4* NG4 = nullptr;
+        // one-hot [node row][edge]: element e of half h ↔ edge rho(8s + e, h)
+        const int s_ = cur.s;
+        uint32_t oh2[2][4];
+#if SPWGNN_ONEHOT_BPERM
+        // the edges' tile-local ids packed (receiver | sender << 16; all ones where an id is not one of
+        // the tile's 16 nodes, padding edges included), fetched per element with one ds_bpermute —
+        // four readlanes and their selects before; the same 0/1 operand. Built inside the k-block loop
+        // (SPWGNN_OH_KB) so the permute latency hides behind its MFMAs.
+        auto build_oh = [&]() {
+            const uint32_t ld_ = (uint32_t)(d - n0) < 16u ? (uint32_t)(d - n0) : 0xffffu;
+            const uint32_t ls_ = (uint32_t)(s_ - n0) < 16u ? (uint32_t)(s_ - n0) : 0xffffu;
+            const int pk = (int)(ld_ | (ls_ << 16));
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    uint32_t wv = 0u;
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * rho(8 * s + 2 * m + q, h), pk);
+                        wv |= (__builtin_amdgcn_ubfe(v, kbits, 16) == (uint32_t)(i & 15) ? 0x3F80u : 0u) << (16 * q);
+                    }
+                    oh2[s][m] = wv;
+                }
+        };
+#endif
         f32x16 acc[5];
         zero_tiles(acc);
 #pragma unroll
@@ -811,6 +843,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
                 for (int t = 0; t < 5; ++t) m1w[t] = m1[32 * t];
             }
+#if SPWGNN_ONEHOT_BPERM && SPWGNN_OH_KB < 10
+            if (kb == SPWGNN_OH_KB) build_oh();
+#endif
             KB& cr = ring[kb % PF];
             float xv[8];
 #pragma unroll
@@ -854,13 +889,17 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int r = 0; r < 16; ++r) acc[t][r] = mask_bit(acc[t][r], mh, rho(r, 0));
         }
         float* dArow = a.dA + (int64_t)blk * 32 * kLdE + i;
-        // one-hot [node row][edge]: element e of half h ↔ edge rho(8s + e, h)
-        const int s_ = cur.s;
+#if SPWGNN_ONEHOT_BPERM && SPWGNN_OH_KB >= 10
+        build_oh();
+#endif
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             uint32_t oh[4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
+#if SPWGNN_ONEHOT_BPERM
+                oh[m] = oh2[s][m];
+#else
                 uint32_t wv = 0u;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
@@ -873,6 +912,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     wv |= (node == key ? 0x3F80u : 0u) << (16 * q);
                 }
                 oh[m] = wv;
+#endif
             }
             const bf16x8 ao = as_bf16x8(make_uint4(oh[0], oh[1], oh[2], oh[3]));
 #pragma unroll

@@ -890,8 +890,9 @@ struct NodeSumX6 {
 template <int NP>
 struct NodeSum16X6 {
     f32x4 acc[10];   // sub-tile u: features 16u + (lane & 15), nodes 4(lane >> 4) + r
-    int key;
-    __device__ __forceinline__ void init(int n0, int lane) {
+    int key, n0;
+    __device__ __forceinline__ void init(int n0_, int lane) {
+        n0 = n0_;
         key = n0 + (lane & 15);
 #pragma unroll
         for (int u = 0; u < 10; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -899,6 +900,11 @@ struct NodeSum16X6 {
     __device__ __forceinline__ void add(const f32x16 (&h2)[5], int d, int lane) {
         const int g = lane >> 4;
         // one-hot A: lane (node i, group g), element e ↔ edge 16(g&1) + 8(e>>2) + 4(g>>1) + (e&3)
+#if SPWGNN_ONEHOT_BPERM
+        // (the receiver's tile-local id fetched with one ds_bpermute per element: d − n0 == lane & 15
+        // exactly when d == key, padding edges (d < 0) never)
+        const int ld = d - n0, gb = 16 * (g & 1) + 4 * (g >> 1);
+#endif
         uint32_t oh[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -906,10 +912,15 @@ struct NodeSum16X6 {
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int e = 2 * m + q, base = 8 * (e >> 2) + (e & 3);
+#if SPWGNN_ONEHOT_BPERM
+                const int dn = __builtin_amdgcn_ds_bpermute(4 * (gb + base), ld);
+                w |= (dn == (lane & 15) ? 0x3F80u : 0u) << (16 * q);
+#else
                 const int d0 = __builtin_amdgcn_readlane(d, base), d1 = __builtin_amdgcn_readlane(d, base + 16);
                 const int d2 = __builtin_amdgcn_readlane(d, base + 4), d3 = __builtin_amdgcn_readlane(d, base + 20);
                 const int dn = g == 0 ? d0 : g == 1 ? d1 : g == 2 ? d2 : d3;
                 w |= (dn == key ? 0x3F80u : 0u) << (16 * q);
+#endif
             }
             oh[m] = w;
         }

@@ -941,6 +941,9 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
         // receiver sum of tile T (NodeSum16X6::add for t = T)
         {
             const int g = lane >> 4;
+#if SPWGNN_ONEHOT_BPERM
+            const int ld = d - n0, gb = 16 * (g & 1) + 4 * (g >> 1);   // (as NodeSum16X6::add)
+#endif
             uint32_t oh[4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -948,10 +951,15 @@ __device__ __forceinline__ void edge_fwd_team_body(const EdgeFwdArgs& a, int wt,
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int e = 2 * m + q, base = 8 * (e >> 2) + (e & 3);
+#if SPWGNN_ONEHOT_BPERM
+                    const int dn = __builtin_amdgcn_ds_bpermute(4 * (gb + base), ld);
+                    w |= (dn == (lane & 15) ? 0x3F80u : 0u) << (16 * q);
+#else
                     const int d0 = __builtin_amdgcn_readlane(d, base), d1 = __builtin_amdgcn_readlane(d, base + 16);
                     const int d2 = __builtin_amdgcn_readlane(d, base + 4), d3 = __builtin_amdgcn_readlane(d, base + 20);
                     const int dn = g == 0 ? d0 : g == 1 ? d1 : g == 2 ? d2 : d3;
                     w |= (dn == key ? 0x3F80u : 0u) << (16 * q);
+#endif
                 }
                 oh[m] = w;
             }
@@ -1123,6 +1131,13 @@ __device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt,
 #pragma unroll
             for (int r = 0; r < 16; ++r) q[r * 64] = (dacc_first ? 0.f : q[r * 64]) + acc[r];
         }
+#if SPWGNN_ONEHOT_BPERM
+        // packed tile-local ids, one ds_bpermute per element (as k_edge_bwd_x6)
+        const uint32_t ld_ = (uint32_t)(d - n0) < 16u ? (uint32_t)(d - n0) : 0xffffu;
+        const uint32_t ls_ = (uint32_t)(s_ - n0) < 16u ? (uint32_t)(s_ - n0) : 0xffffu;
+        const int pk = (int)(ld_ | (ls_ << 16));
+        const int kbits = i < 16 ? 0 : 16;
+#endif
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
             uint32_t oh[4];
@@ -1132,12 +1147,17 @@ __device__ __forceinline__ void edge_bwd_team_body(const EdgeBwdArgs& a, int wt,
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int ee = 2 * m + q;
+#if SPWGNN_ONEHOT_BPERM
+                    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * rho(8 * sh + ee, h), pk);
+                    wv |= (__builtin_amdgcn_ubfe(v, kbits, 16) == (uint32_t)(i & 15) ? 0x3F80u : 0u) << (16 * q);
+#else
                     const int d0 = __builtin_amdgcn_readlane(d, rho(8 * sh + ee, 0));
                     const int d1 = __builtin_amdgcn_readlane(d, rho(8 * sh + ee, 1));
                     const int s0 = __builtin_amdgcn_readlane(s_, rho(8 * sh + ee, 0));
                     const int s1 = __builtin_amdgcn_readlane(s_, rho(8 * sh + ee, 1));
                     const int node = i < 16 ? (h ? d1 : d0) : (h ? s1 : s0);
                     wv |= (node == key ? 0x3F80u : 0u) << (16 * q);
+#endif
                 }
                 oh[m] = wv;
             }
